@@ -1,0 +1,70 @@
+// Shared device/host helpers for the gfx950 kernels (wave64, CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "d2d_hip.h"
+
+namespace d2d {
+
+constexpr int kWave = 64;  // CDNA wavefront: every ballot below is 64-bit
+
+enum : uint32_t { kStreamFlip = 0, kStreamArrival = 1, kStreamAction = 2, kPerEnv = 0xFFFFFFFFu };
+
+struct u32x4 {
+  uint32_t x, y, z, w;
+};
+
+// Philox4x32-10 (Salmon et al., SC'11); identical to oracle/philox.py and
+// oracle/c/d2d_oracle.c, pinned to the Random123 known-answer vectors.
+__device__ __forceinline__ u32x4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint64_t seed) {
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  return {c0, c1, c2, c3};
+}
+
+__device__ __forceinline__ uint32_t pick(const u32x4& r, int i) {
+  return i == 0 ? r.x : (i == 1 ? r.y : (i == 2 ? r.z : r.w));
+}
+
+// Poisson(lam) by sequential CDF inversion of u = r * 2^-32, capped at 255
+// (uint8 buffer cells).  Same IEEE double op order as the oracles; built with
+// -ffp-contract=off so no FMA changes the rounding.
+__device__ __forceinline__ uint32_t poisson_inv(uint32_t r, double lam, double p0) {
+  const double u = (double)r * (1.0 / 4294967296.0);
+  double p = p0, F = p;
+  uint32_t x = 0;
+  while (u >= F && x < 255u) {
+    x += 1u;
+    p = (p * lam) / (double)x;
+    F = F + p;
+  }
+  return x;
+}
+
+}  // namespace d2d
+
+// thread-local last-error string for the C ABI
+void d2d_set_error(const char* fmt, ...);
+
+#define D2D_CHECK_HIP(expr)                                                    \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      d2d_set_error("%s: %s", #expr, hipGetErrorString(_e));                   \
+      return D2D_EHIP;                                                         \
+    }                                                                          \
+  } while (0)

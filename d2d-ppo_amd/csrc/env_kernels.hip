@@ -1,0 +1,725 @@
+// Env reset/step kernels for gfx950 (MI355X, CDNA4, wave64).
+//
+// Replaces the per-slot Python body of
+//   CombinatorialEnv.reset/step    /root/reference/envs/combinatorial_env.py:61-114, 116-124, 127-242
+//   ChannelSelectionEnv.reset/step /root/reference/envs/channel_selection_env.py:49-98, 104-113, 116-214
+// for a batch of E independent envs.  One lane = one agent of one env:
+//   * N <= 64 : an env is a power-of-two lane segment of one wavefront (64/seg
+//               envs per wave); per-channel attempt counts are 64-bit wave
+//               ballots masked to the segment + popcount (no LDS, no barrier).
+//   * N  > 64 : one env per workgroup of ceil(N/64) waves; each wave ballots,
+//               the per-channel counts are combined through LDS.
+// A lane keeps its agent's whole buffer row (DW x uint32 = DW*4 slots, byte j =
+// packets with j slots left) in registers: packet removal, expiry and the
+// shift are byte ops (ctz, funnel shift), arrivals are one byte insert.
+// obs/state rows are staged in LDS and written back as contiguous float4
+// streams, so every HBM write is a full-line coalesced store.
+// Randomness: recorded draws (replay, parity) or Philox4x32-10 (production).
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "common.h"
+
+namespace d2d {
+
+constexpr int kBlock = 256;
+constexpr int kMaxAgents = 1024;
+
+struct EnvArgs {
+  int E, N, C, D, F, S, state_stride, seg, reset, cnt_words;
+  uint32_t rng_step;
+  uint64_t env_base, seed;
+  const d2d_agent_entry* agents;
+  const uint64_t* flip_thr;
+  uint32_t* buf;
+  void* chan;
+  uint32_t* recv;
+  uint32_t* disc;
+  uint32_t* selq;
+  uint32_t* seln;
+  const void* actions;
+  const void* flips;
+  const uint8_t* arrivals;
+  float* obs;
+  float* state;
+  int32_t* reward;
+  void* ack;
+  uint8_t* success;
+  uint64_t draw[kMaxAgents / 64];
+};
+
+// ------------------------------------------------------------ buffer row ops
+template <int DW>
+struct Row {
+  uint32_t w[DW];
+};
+
+template <int DW>
+__device__ __forceinline__ void load_row(Row<DW>& r, const uint32_t* p) {
+  if constexpr (DW == 4) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    r.w[0] = v.x; r.w[1] = v.y; r.w[2] = v.z; r.w[3] = v.w;
+  } else if constexpr (DW == 2) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p);
+    r.w[0] = v.x; r.w[1] = v.y;
+  } else if constexpr (DW == 8) {
+    const uint4 v0 = reinterpret_cast<const uint4*>(p)[0];
+    const uint4 v1 = reinterpret_cast<const uint4*>(p)[1];
+    r.w[0] = v0.x; r.w[1] = v0.y; r.w[2] = v0.z; r.w[3] = v0.w;
+    r.w[4] = v1.x; r.w[5] = v1.y; r.w[6] = v1.z; r.w[7] = v1.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < DW; ++i) r.w[i] = p[i];
+  }
+}
+
+template <int DW>
+__device__ __forceinline__ void store_row(const Row<DW>& r, uint32_t* p) {
+  if constexpr (DW == 4) {
+    *reinterpret_cast<uint4*>(p) = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
+  } else if constexpr (DW == 2) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(r.w[0], r.w[1]);
+  } else if constexpr (DW == 8) {
+    reinterpret_cast<uint4*>(p)[0] = make_uint4(r.w[0], r.w[1], r.w[2], r.w[3]);
+    reinterpret_cast<uint4*>(p)[1] = make_uint4(r.w[4], r.w[5], r.w[6], r.w[7]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < DW; ++i) p[i] = r.w[i];
+  }
+}
+
+template <int DW>
+__device__ __forceinline__ bool row_any(const Row<DW>& r) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < DW; ++i) o |= r.w[i];
+  return o != 0;
+}
+
+// next_buffers[u, col.min()] -= 1   (combinatorial_env.py:169-170)
+template <int DW>
+__device__ __forceinline__ void row_remove_first(Row<DW>& r) {
+  bool done = false;
+#pragma unroll
+  for (int i = 0; i < DW; ++i) {
+    const uint32_t v = r.w[i];
+    if (!done && v) {
+      const uint32_t sh = (uint32_t)__builtin_ctz(v) & ~7u;
+      r.w[i] = v - (1u << sh);
+      done = true;
+    }
+  }
+}
+
+// evolve_buffer: expired = B[:,0]; B = shift_left(B)  (combinatorial_env.py:120-124)
+template <int DW>
+__device__ __forceinline__ uint32_t row_expire_shift(Row<DW>& r) {
+  const uint32_t expired = r.w[0] & 0xFFu;
+#pragma unroll
+  for (int i = 0; i < DW; ++i) {
+    const uint32_t hi = (i + 1 < DW) ? r.w[i + 1] : 0u;
+    r.w[i] = __builtin_amdgcn_alignbyte(hi, r.w[i], 1);
+  }
+  return expired;
+}
+
+// next_buffers[i, d_i - 1] = arrival  (the cell is 0 after the shift)
+template <int DW>
+__device__ __forceinline__ void row_set(Row<DW>& r, int col, uint32_t v) {
+  // branch-free select per word: an `if` here gets sunk into a dynamically
+  // indexed store, which spills the row to scratch
+  const uint32_t ins = (v & 0xFFu) << ((col & 3) * 8);
+  const int wi = col >> 2;
+#pragma unroll
+  for (int i = 0; i < DW; ++i) r.w[i] |= (wi == i) ? ins : 0u;
+}
+
+template <int DW>
+__device__ __forceinline__ float row_byte(const Row<DW>& r, int j) {
+  return (float)((r.w[j >> 2] >> ((j & 3) * 8)) & 0xFFu);
+}
+
+// ------------------------------------------------------------------ draws
+__device__ __forceinline__ bool draws_now(const EnvArgs& a, int k) {
+  return (a.draw[k >> 6] >> (k & 63)) & 1ull;
+}
+
+__device__ __forceinline__ uint32_t arrival_value(const EnvArgs& a, const d2d_agent_entry& ag, size_t row, int k,
+                                                  uint64_t genv) {
+  if (a.arrivals) return a.arrivals[row];
+  const u32x4 r = philox((uint32_t)genv, (uint32_t)k, a.rng_step, kStreamArrival << 24, a.seed);
+  if (ag.arrival_kind == D2D_ARRIVAL_POISSON) return poisson_inv(r.x, ag.lam, ag.pois_p0);
+  return (uint64_t)r.x < ag.arrival_thr ? 1u : 0u;
+}
+
+// ------------------------------------------------------ LDS -> HBM flushing
+// Copy `count` floats from LDS to a contiguous global range with float4 stores
+// when both ends allow it (every obs/state row group of a block is contiguous).
+__device__ __forceinline__ void flush_contig(float* __restrict__ dst, const float* src, int count) {
+  const bool vec = ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) && ((count & 3) == 0);
+  if (vec) {
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    for (int i = threadIdx.x; i < (count >> 2); i += blockDim.x) d4[i] = s4[i];
+  } else {
+    for (int i = threadIdx.x; i < count; i += blockDim.x) dst[i] = src[i];
+  }
+}
+
+__device__ __forceinline__ void flush_rows(float* __restrict__ dst, int stride, const float* src, int rows, int S) {
+  if ((S & 3) == 0 && (stride & 3) == 0 && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
+    const int q = S >> 2;
+    for (int i = threadIdx.x; i < rows * q; i += blockDim.x) {
+      const int r = i / q, j = i - r * q;
+      reinterpret_cast<float4*>(dst + (size_t)r * stride)[j] = reinterpret_cast<const float4*>(src + r * S)[j];
+    }
+  } else {
+    for (int i = threadIdx.x; i < rows * S; i += blockDim.x) {
+      const int r = i / S, j = i - r * S;
+      dst[(size_t)r * stride + j] = src[r * S + j];
+    }
+  }
+}
+
+// ---------------------------------------------------- geometry of a lane
+struct Lane {
+  int env, k, local_env, envs_per_block, lane;
+  bool active;
+  uint64_t segmask;
+};
+
+template <bool LARGE>
+__device__ __forceinline__ Lane lane_geometry(const EnvArgs& a) {
+  Lane L;
+  L.lane = threadIdx.x & (kWave - 1);
+  if (LARGE) {
+    L.env = blockIdx.x;
+    L.k = threadIdx.x;
+    L.local_env = 0;
+    L.envs_per_block = 1;
+    L.segmask = ~0ull;
+  } else {
+    L.local_env = threadIdx.x / a.seg;
+    L.k = threadIdx.x - L.local_env * a.seg;
+    L.envs_per_block = blockDim.x / a.seg;
+    L.env = blockIdx.x * L.envs_per_block + L.local_env;
+    const int seg_base = L.lane & ~(a.seg - 1);
+    L.segmask = (a.seg == kWave) ? ~0ull : (((1ull << a.seg) - 1ull) << seg_base);
+  }
+  L.active = (L.k < a.N) && (L.env < a.E);
+  return L;
+}
+
+// Sum of `v` over the lanes of this lane's env (segment ballot or LDS).
+template <bool LARGE>
+__device__ __forceinline__ int env_count(bool v, const Lane& L, int* lds_acc) {
+  const int part = __popcll(__ballot(v) & L.segmask);
+  if (!LARGE) return part;
+  if (L.lane == 0) atomicAdd(lds_acc, part);
+  __syncthreads();
+  const int tot = *lds_acc;
+  return tot;
+}
+
+// =====================================================================
+// Combinatorial env: action = binary N x C matrix, per-(agent, channel)
+// Markov channel, ACK vector in {-1, 0, 1}.
+// =====================================================================
+template <typename MaskT, int DW, bool LARGE>
+__global__ __launch_bounds__(kMaxAgents) void comb_kernel(EnvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Lane L = lane_geometry<LARGE>(a);
+  // LDS carve: [64 int counters][obs rows][state rows]
+  int* cnt = reinterpret_cast<int*>(lds);  // LARGE: n[32], g[32]; reward at [64]
+  float* lds_obs = lds + a.cnt_words;
+  float* lds_state = lds_obs + ((L.envs_per_block * a.N * a.F + 3) & ~3);
+  const int N = a.N, C = a.C, F = a.F;
+  const size_t row = (size_t)L.env * N + L.k;
+  const uint64_t genv = a.env_base + (uint64_t)L.env;
+  const uint32_t cmask = (C >= 32) ? 0xFFFFFFFFu : ((1u << C) - 1u);
+  const MaskT* chan_in = reinterpret_cast<const MaskT*>(a.chan);
+
+  Row<DW> b;
+#pragma unroll
+  for (int i = 0; i < DW; ++i) b.w[i] = 0;
+  uint32_t h_pre = 0, act = 0, rc = 0, dc = 0;
+  d2d_agent_entry ag{};
+  if (L.active) {
+    ag = a.agents[L.k];
+    if (!a.reset) {
+      load_row<DW>(b, a.buf + row * DW);
+      h_pre = (uint32_t)chan_in[row] & cmask;
+      act = (uint32_t)reinterpret_cast<const MaskT*>(a.actions)[row] & cmask;
+      rc = a.recv[row];
+      dc = a.disc[row];
+    } else {
+      h_pre = cmask;
+    }
+  }
+  if (LARGE) {
+    if (threadIdx.x < 80) cnt[threadIdx.x] = 0;
+    __syncthreads();
+  }
+
+  uint32_t ack_one = 0, ack_zero = 0, h_new = h_pre;
+  bool succ = false;
+  int nsucc = 0;
+  if (!a.reset) {
+    // attempts = actions * has_a_packet; attempts_good_channels = attempts * channel_state (135-138)
+    const uint32_t att = row_any<DW>(b) ? act : 0u;
+    const uint32_t good = att & h_pre;
+    // n_users_per_channel, good-attempt count, acknack (148, 155-157): ballots per channel
+    for (int c = 0; c < C; ++c) {
+      const uint64_t m = __ballot((att >> c) & 1u) & L.segmask;
+      const uint64_t g = __ballot((good >> c) & 1u) & L.segmask;
+      if (!LARGE) {
+        const int n = __popcll(m);
+        ack_zero |= (uint32_t)(n == 0) << c;
+        ack_one |= (uint32_t)(n == 1 && g != 0) << c;
+      } else if (L.lane == 0) {
+        atomicAdd(&cnt[c], __popcll(m));
+        atomicAdd(&cnt[32 + c], __popcll(g));
+      }
+    }
+    if (LARGE) {
+      __syncthreads();
+      for (int c = 0; c < C; ++c) {
+        const int n = cnt[c];
+        ack_zero |= (uint32_t)(n == 0) << c;
+        ack_one |= (uint32_t)(n == 1 && cnt[32 + c] == 1) << c;
+      }
+    }
+    // successful_attempts = (acknack * attempts_good) == 1; one packet per user (160-170)
+    succ = L.active && ((good & ack_one) != 0);
+    nsucc = env_count<LARGE>(succ, L, cnt + 64);
+    if (succ) row_remove_first<DW>(b);
+    dc += row_expire_shift<DW>(b);  // discarded_packets += expired (173-174)
+    // evolve_channel: channel_state = |channel_state - Bernoulli(channel_switch)| (116-118, 175)
+    uint32_t f = 0;
+    if (L.active) {
+      if (a.flips) {
+        f = (uint32_t)reinterpret_cast<const MaskT*>(a.flips)[row];
+      } else {
+        for (int blk = 0; blk * 4 < C; ++blk) {
+          const u32x4 r = philox((uint32_t)genv, (uint32_t)L.k, a.rng_step, (kStreamFlip << 24) | (uint32_t)blk, a.seed);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int c = blk * 4 + i;
+            if (c < C) f |= (uint32_t)((uint64_t)pick(r, i) < a.flip_thr[(size_t)L.k * C + c]) << c;
+          }
+        }
+      }
+    }
+    h_new = (h_pre ^ f) & cmask;
+  }
+  // arrivals (reset 66-85, step 178-196)
+  if (L.active && draws_now(a, L.k)) {
+    const uint32_t x = arrival_value(a, ag, row, L.k, genv);
+    row_set<DW>(b, (int)ag.deadline - 1, x);
+    rc = (a.reset ? 0u : rc) + x;
+  }
+  if (a.reset) {
+    rc = L.active && draws_now(a, L.k) ? rc : 0u;
+    dc = 0;
+    ack_one = cmask;  // reset obs/state carry ones(C) in the feedback slot (108-112)
+  }
+  // ---- state update
+  if (L.active) {
+    store_row<DW>(b, a.buf + row * DW);
+    reinterpret_cast<MaskT*>(a.chan)[row] = (MaskT)h_new;
+    a.recv[row] = rc;
+    a.disc[row] = dc;
+    if (a.success) a.success[row] = succ ? 1 : 0;
+    if (L.k == 0 && !a.reset) {
+      if (a.reward) a.reward[L.env] = nsucc;  // rewards = len(successful_users) (211)
+      if (a.ack) {
+        int8_t* ak = reinterpret_cast<int8_t*>(a.ack) + (size_t)L.env * C;
+        for (int c = 0; c < C; ++c) ak[c] = ((ack_one >> c) & 1) ? 1 : (((ack_zero >> c) & 1) ? 0 : -1);
+      }
+    }
+  }
+  // ---- emission: obs_k = [B'[k,:w_k], channel_obs[k] (pre-evolve), acknack] (199-206)
+  const int env0 = LARGE ? blockIdx.x : blockIdx.x * L.envs_per_block;
+  const int nenv = min(L.envs_per_block, a.E - env0);
+  if (a.obs) {
+    if (L.active) {
+      float* o = lds_obs + (L.local_env * N + L.k) * F;
+      const int w = ag.obs_width;
+#pragma unroll
+      for (int j = 0; j < DW * 4; ++j)
+        if (j < w) o[j] = row_byte<DW>(b, j);
+      for (int c = 0; c < C; ++c) {
+        o[w + c] = (float)((h_pre >> c) & 1u);
+        o[w + C + c] = ((ack_one >> c) & 1u) ? 1.f : (((ack_zero >> c) & 1u) ? 0.f : -1.f);
+      }
+      for (int j = w + 2 * C; j < F; ++j) o[j] = 0.f;
+    }
+  }
+  // state = [concat_k B'[k,:d_k], channel_state (post-evolve).flatten(), acknack] (207-209)
+  if (a.state) {
+    if (L.active) {
+      float* s = lds_state + L.local_env * a.S;
+      const int off = ag.state_offset, d = ag.deadline;
+#pragma unroll
+      for (int j = 0; j < DW * 4; ++j)
+        if (j < d) s[off + j] = row_byte<DW>(b, j);
+      const int sb = a.S - C * (N + 1);
+      for (int c = 0; c < C; ++c) s[sb + L.k * C + c] = (float)((h_new >> c) & 1u);
+      if (L.k == 0)
+        for (int c = 0; c < C; ++c)
+          s[sb + N * C + c] = ((ack_one >> c) & 1u) ? 1.f : (((ack_zero >> c) & 1u) ? 0.f : -1.f);
+    }
+  }
+  if (a.obs || a.state) {
+    __syncthreads();
+    if (a.obs && nenv > 0) flush_contig(a.obs + (size_t)env0 * N * F, lds_obs, nenv * N * F);
+    if (a.state && nenv > 0) flush_rows(a.state + (size_t)env0 * a.state_stride, a.state_stride, lds_state, nenv, a.S);
+  }
+}
+
+// =====================================================================
+// Channel-selection env: action = channel id 0..C, one Markov state per
+// channel shared by all agents, ACK = 1/n on good attempted channels.
+// =====================================================================
+template <int DW, bool LARGE>
+__global__ __launch_bounds__(kMaxAgents) void chsel_kernel(EnvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Lane L = lane_geometry<LARGE>(a);
+  const int N = a.N, C = a.C, F = a.F;
+  // LDS carve: [per-env counts: 33 ints + reward][obs rows][state rows]
+  int* cnt_all = reinterpret_cast<int*>(lds);
+  int* cnt = cnt_all + L.local_env * 34;
+  float* lds_obs = lds + a.cnt_words;
+  float* lds_state = lds_obs + ((L.envs_per_block * N * F + 3) & ~3);
+  const size_t row = (size_t)L.env * N + L.k;
+  const uint64_t genv = a.env_base + (uint64_t)L.env;
+  const uint32_t hmask = (C + 1 >= 32) ? 0xFFFFFFFFu : ((1u << (C + 1)) - 1u);
+  uint32_t* chan = reinterpret_cast<uint32_t*>(a.chan);
+  const bool env_ok = L.env < a.E;
+
+  Row<DW> b;
+#pragma unroll
+  for (int i = 0; i < DW; ++i) b.w[i] = 0;
+  uint32_t H = hmask, act = 0, rc = 0, dc = 0;
+  d2d_agent_entry ag{};
+  if (L.active) {
+    ag = a.agents[L.k];
+    if (!a.reset) {
+      load_row<DW>(b, a.buf + row * DW);
+      act = reinterpret_cast<const uint8_t*>(a.actions)[row];
+      rc = a.recv[row];
+      dc = a.disc[row];
+    }
+  }
+  if (env_ok && !a.reset) H = chan[L.env] & hmask;
+  for (int i = threadIdx.x; i < L.envs_per_block * 34; i += blockDim.x) cnt_all[i] = 0;
+  __syncthreads();
+
+  bool succ = false;
+  int nsucc = 0;
+  uint32_t H_new = H, attempted = 0;
+  if (!a.reset) {
+    // attempts = actions * has_a_packet (124-125); unique ids + counts (127-128)
+    const uint32_t att = (L.active && row_any<DW>(b) && act <= (uint32_t)C) ? act : 0u;
+    for (int j = 1; j <= C; ++j) {
+      const int n = __popcll(__ballot(att == (uint32_t)j) & L.segmask);
+      if (!LARGE) {
+        if (L.k == 0) cnt[j] = n;
+      } else if (L.lane == 0) {
+        atomicAdd(&cnt[j], n);
+      }
+    }
+    __syncthreads();
+    for (int j = 1; j <= C; ++j) attempted |= (uint32_t)(cnt[j] > 0) << j;
+    // successful users: their channel has exactly one attempt and is good (140-142)
+    succ = att != 0 && cnt[att] == 1 && ((H >> att) & 1u);
+    nsucc = env_count<LARGE>(succ, L, cnt + 33);
+    if (succ) row_remove_first<DW>(b);
+    dc += row_expire_shift<DW>(b);  // (154-155)
+    // evolve_channel: C+1 scalar Bernoulli flips, channel 0 included (104-107, 156)
+    uint32_t f = 0;
+    if (env_ok) {
+      if (a.flips) {
+        f = reinterpret_cast<const uint32_t*>(a.flips)[L.env];
+      } else {
+        for (int blk = 0; blk * 4 < C + 1; ++blk) {
+          const u32x4 r = philox((uint32_t)genv, kPerEnv, a.rng_step, (kStreamFlip << 24) | (uint32_t)blk, a.seed);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int j = blk * 4 + i;
+            if (j <= C) f |= (uint32_t)((uint64_t)pick(r, i) < a.flip_thr[j]) << j;
+          }
+        }
+      }
+    }
+    H_new = (H ^ f) & hmask;
+  }
+  // arrivals (reset 54-71, step 159-177)
+  const bool drew = L.active && draws_now(a, L.k);
+  if (drew) {
+    const uint32_t x = arrival_value(a, ag, row, L.k, genv);
+    row_set<DW>(b, (int)ag.deadline - 1, x);
+    rc = (a.reset ? 0u : rc) + x;
+  }
+  if (a.reset) {
+    rc = drew ? rc : 0u;
+    dc = 0;
+  }
+  if (L.active) {
+    store_row<DW>(b, a.buf + row * DW);
+    a.recv[row] = rc;
+    a.disc[row] = dc;
+    if (a.success) a.success[row] = succ ? 1 : 0;
+  }
+  if (env_ok && L.k == 0) {
+    chan[L.env] = H_new;
+    if (!a.reset) {
+      if (a.reward) a.reward[L.env] = nsucc;    // (188)
+      a.selq[L.env] += __popc(attempted & H);  // (acknack > 0).sum()  (132)
+      a.seln[L.env] += __popc(attempted);      // (acknack != 0).sum() (133)
+      if (a.ack) {
+        double* ak = reinterpret_cast<double*>(a.ack) + (size_t)L.env * (C + 1);
+        ak[0] = 0.0;
+        for (int j = 1; j <= C; ++j) {
+          const int n = cnt[j];
+          ak[j] = n == 0 ? 0.0 : (((H >> j) & 1u) ? 1.0 / (double)n : -1.0);
+        }
+      }
+    } else {
+      a.selq[L.env] = 0;
+      a.seln[L.env] = 0;
+    }
+  }
+  // obs_k = [B'[k,:d_k], acknack] (180-184); acknack[idx] = 2H-1, good -> 1/count
+  // (129-137), rounded to float once from the double value like the reference's cast
+  const int env0 = LARGE ? blockIdx.x : blockIdx.x * L.envs_per_block;
+  const int nenv = min(L.envs_per_block, a.E - env0);
+  if (a.obs && L.active) {
+    float* o = lds_obs + (L.local_env * N + L.k) * F;
+    const int w = ag.obs_width;
+#pragma unroll
+    for (int j = 0; j < DW * 4; ++j)
+      if (j < w) o[j] = row_byte<DW>(b, j);
+    o[w] = 0.f;
+    for (int j = 1; j <= C; ++j) {
+      const int n = a.reset ? 0 : cnt[j];
+      o[w + j] = n == 0 ? 0.f : (((H >> j) & 1u) ? (float)(1.0 / (double)n) : -1.f);
+    }
+    for (int j = w + C + 1; j < F; ++j) o[j] = 0.f;
+  }
+  // state = [concat_k B'[k,:d_k], channel_state (post-evolve)] (185-186)
+  if (a.state && L.active) {
+    float* s = lds_state + L.local_env * a.S;
+    const int off = ag.state_offset, d = ag.deadline;
+#pragma unroll
+    for (int j = 0; j < DW * 4; ++j)
+      if (j < d) s[off + j] = row_byte<DW>(b, j);
+    const int sb = a.S - (C + 1);
+    if (L.k == 0)
+      for (int j = 0; j <= C; ++j) s[sb + j] = (float)((H_new >> j) & 1u);
+  }
+  if (a.obs || a.state) {
+    __syncthreads();
+    if (a.obs && nenv > 0) flush_contig(a.obs + (size_t)env0 * N * F, lds_obs, nenv * N * F);
+    if (a.state && nenv > 0) flush_rows(a.state + (size_t)env0 * a.state_stride, a.state_stride, lds_state, nenv, a.S);
+  }
+}
+
+
+// =====================================================================
+// synthetic actions (env-only benchmark / baseline policies)
+// =====================================================================
+template <typename MaskT>
+__global__ __launch_bounds__(256) void sample_actions_kernel(int E, int N, int C, int chsel, uint64_t env_base,
+                                                             uint64_t seed, uint32_t rng_step, uint64_t thr,
+                                                             void* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)E * N) return;
+  const int env = (int)(i / N), k = (int)(i - (int64_t)env * N);
+  const uint32_t genv = (uint32_t)(env_base + (uint64_t)env);
+  if (chsel) {
+    const u32x4 r = philox(genv, (uint32_t)k, rng_step, kStreamAction << 24, seed);
+    reinterpret_cast<uint8_t*>(out)[i] = (uint8_t)(((uint64_t)r.x * (uint64_t)(C + 1)) >> 32);
+    return;
+  }
+  uint32_t m = 0;
+  for (int blk = 0; blk * 4 < C; ++blk) {
+    const u32x4 r = philox(genv, (uint32_t)k, rng_step, (kStreamAction << 24) | (uint32_t)blk, seed);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = blk * 4 + j;
+      if (c < C) m |= (uint32_t)((uint64_t)pick(r, j) < thr) << c;
+    }
+  }
+  reinterpret_cast<MaskT*>(out)[i] = (MaskT)m;
+}
+
+}  // namespace d2d
+
+// =====================================================================
+// C ABI launchers
+// =====================================================================
+using namespace d2d;
+
+namespace {
+
+int buffer_words(int D) { return D <= 4 ? 1 : D <= 8 ? 2 : D <= 12 ? 3 : D <= 16 ? 4 : 8; }
+
+int check_desc(const d2d_env_desc* d) {
+  if (!d) { d2d_set_error("desc is NULL"); return D2D_EINVAL; }
+  const bool comb = d->env_kind == D2D_ENV_COMBINATORIAL;
+  if (!comb && d->env_kind != D2D_ENV_CHANNEL_SELECTION) { d2d_set_error("unknown env_kind %d", d->env_kind); return D2D_EINVAL; }
+  if (d->n_agents < 1 || d->n_agents > kMaxAgents) { d2d_set_error("n_agents=%d outside [1,%d]", d->n_agents, kMaxAgents); return D2D_EUNSUPPORTED; }
+  if (d->n_channels < 1 || d->n_channels > (comb ? 32 : 31)) { d2d_set_error("n_channels=%d unsupported", d->n_channels); return D2D_EUNSUPPORTED; }
+  if (d->max_deadline < 1 || d->max_deadline > 32) { d2d_set_error("max_deadline=%d outside [1,32]", d->max_deadline); return D2D_EUNSUPPORTED; }
+  if (d->n_envs < 0) { d2d_set_error("n_envs < 0"); return D2D_EINVAL; }
+  const int F = comb ? d->max_deadline + 2 * d->n_channels : d->max_deadline + d->n_channels + 1;
+  if (d->obs_dim != F) { d2d_set_error("obs_dim=%d, expected %d", d->obs_dim, F); return D2D_EINVAL; }
+  if (d->state_stride < d->state_dim) { d2d_set_error("state_stride < state_dim"); return D2D_EINVAL; }
+  if (!d->agents || !d->flip_thr || !d->arrival_kind_host || !d->period_host || !d->offset_host) {
+    d2d_set_error("desc tables must be non-NULL"); return D2D_EINVAL;
+  }
+  return D2D_OK;
+}
+
+// which agents draw an arrival at timestep t: numpy float semantics of
+// `timestep % period == offsets` (combinatorial_env.py:183,194), t = 0 at reset
+void draw_mask(const d2d_env_desc* d, int t, uint64_t* mask) {
+  memset(mask, 0, sizeof(uint64_t) * (kMaxAgents / 64));
+  for (int k = 0; k < d->n_agents; ++k) {
+    const int kind = d->arrival_kind_host[k];
+    bool dr = kind == D2D_ARRIVAL_POISSON;
+    if (kind == D2D_ARRIVAL_SCHEDULED_BERNOULLI) dr = std::fmod((double)t, d->period_host[k]) == d->offset_host[k];
+    if (dr) mask[k >> 6] |= 1ull << (k & 63);
+  }
+}
+
+template <typename K>
+int set_lds(K kernel, size_t bytes) {
+  if (bytes > 163840) { d2d_set_error("LDS requirement %zu B exceeds 160 KiB (N*obs_dim too large)", bytes); return D2D_EUNSUPPORTED; }
+  if (bytes > 65536)
+    D2D_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  return D2D_OK;
+}
+
+template <typename K>
+int launch(K kernel, const EnvArgs& a, int block, hipStream_t s) {
+  const bool large = a.N > kWave;
+  const int epb = large ? 1 : block / a.seg;
+  const int grid = (a.E + epb - 1) / epb;
+  if (grid == 0) return D2D_OK;
+  const int obs_words = a.obs ? ((epb * a.N * a.F + 3) & ~3) : 0;
+  const size_t lds = sizeof(float) * ((size_t)a.cnt_words + (size_t)(a.obs || a.state ? ((epb * a.N * a.F + 3) & ~3) : 0) +
+                                      (a.state ? (size_t)epb * a.S : 0));
+  (void)obs_words;
+  int rc = set_lds(kernel, lds);
+  if (rc) return rc;
+  hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), lds, s, a);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
+template <typename MaskT, int DW>
+int dispatch_comb(const EnvArgs& a, int block, hipStream_t s) {
+  if (a.N > kWave) return launch(comb_kernel<MaskT, DW, true>, a, block, s);
+  return launch(comb_kernel<MaskT, DW, false>, a, block, s);
+}
+
+template <int DW>
+int dispatch_dw(const EnvArgs& a, int block, bool comb, int C, hipStream_t s) {
+  if (!comb) {
+    if (a.N > kWave) return launch(chsel_kernel<DW, true>, a, block, s);
+    return launch(chsel_kernel<DW, false>, a, block, s);
+  }
+  if (C <= 8) return dispatch_comb<uint8_t, DW>(a, block, s);
+  if (C <= 16) return dispatch_comb<uint16_t, DW>(a, block, s);
+  return dispatch_comb<uint32_t, DW>(a, block, s);
+}
+
+int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions, const d2d_env_replay* rp,
+            const d2d_env_out* out, int reset, int t, uint32_t rng_step, void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (!st || !st->buffers || !st->channels || !st->received || !st->discarded) {
+    d2d_set_error("state buffers must be non-NULL"); return D2D_EINVAL;
+  }
+  const bool comb = d->env_kind == D2D_ENV_COMBINATORIAL;
+  if (!comb && (!st->sel_quality || !st->sel_count)) { d2d_set_error("chsel needs sel_quality/sel_count"); return D2D_EINVAL; }
+  if (!reset && !actions) { d2d_set_error("actions is NULL"); return D2D_EINVAL; }
+  EnvArgs a;
+  memset(&a, 0, sizeof(a));
+  a.E = d->n_envs; a.N = d->n_agents; a.C = d->n_channels; a.D = d->max_deadline; a.F = d->obs_dim;
+  a.S = d->state_dim; a.state_stride = d->state_stride; a.reset = reset; a.rng_step = rng_step;
+  a.env_base = d->env_base; a.seed = d->seed; a.agents = d->agents; a.flip_thr = d->flip_thr;
+  a.buf = st->buffers; a.chan = st->channels; a.recv = st->received; a.disc = st->discarded;
+  a.selq = st->sel_quality; a.seln = st->sel_count; a.actions = actions;
+  if (rp) { a.flips = rp->flips; a.arrivals = rp->arrivals; }
+  if (out) { a.obs = out->obs; a.state = out->state; a.reward = out->reward; a.ack = out->ack; a.success = out->success; }
+  draw_mask(d, reset ? 0 : t, a.draw);
+  const bool large = a.N > kWave;
+  int seg = 1;
+  while (seg < a.N) seg <<= 1;
+  a.seg = large ? ((a.N + kWave - 1) / kWave) * kWave : seg;
+  // block: 256 lanes (4 waves) unless the LDS staging of that many envs would
+  // exceed 64 KiB (keep >= 2 workgroups per CU); LARGE: one env per block
+  auto cnt_words = [&](int epb) { return comb ? (large ? 80 : 0) : (((epb * 34) + 3) & ~3); };
+  auto lds_bytes = [&](int blk) {
+    const int epb = large ? 1 : blk / a.seg;
+    return sizeof(float) * ((size_t)cnt_words(epb) + (size_t)((epb * a.N * a.F + 3) & ~3) +
+                            (a.state ? (size_t)epb * a.S : 0));
+  };
+  int block = large ? a.seg : 256;
+  while (!large && block > kWave && block > a.seg && lds_bytes(block) > 65536) block >>= 1;
+  a.cnt_words = cnt_words(large ? 1 : block / a.seg);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (buffer_words(a.D)) {
+    case 1: return dispatch_dw<1>(a, block, comb, a.C, s);
+    case 2: return dispatch_dw<2>(a, block, comb, a.C, s);
+    case 3: return dispatch_dw<3>(a, block, comb, a.C, s);
+    case 4: return dispatch_dw<4>(a, block, comb, a.C, s);
+    default: return dispatch_dw<8>(a, block, comb, a.C, s);
+  }
+}
+
+}  // namespace
+
+extern "C" int d2d_buffer_words(int32_t max_deadline) { return buffer_words(max_deadline); }
+
+extern "C" int d2d_mask_bytes(int32_t n_channels) { return n_channels <= 8 ? 1 : n_channels <= 16 ? 2 : 4; }
+
+extern "C" int d2d_env_reset(const d2d_env_desc* desc, const d2d_env_state* st, const d2d_env_replay* replay,
+                             const d2d_env_out* out, uint32_t rng_step, void* stream) {
+  return run_env(desc, st, nullptr, replay, out, 1, 0, rng_step, stream);
+}
+
+extern "C" int d2d_env_step(const d2d_env_desc* desc, const d2d_env_state* st, const void* actions,
+                            const d2d_env_replay* replay, const d2d_env_out* out, int32_t timestep, uint32_t rng_step,
+                            void* stream) {
+  return run_env(desc, st, actions, replay, out, 0, timestep, rng_step, stream);
+}
+
+extern "C" int d2d_sample_actions(const d2d_env_desc* d, void* actions, uint64_t threshold, uint32_t rng_step,
+                                  void* stream) {
+  int rc = check_desc(d);
+  if (rc) return rc;
+  if (!actions) { d2d_set_error("actions is NULL"); return D2D_EINVAL; }
+  const int64_t n = (int64_t)d->n_envs * d->n_agents;
+  if (n == 0) return D2D_OK;
+  const int grid = (int)((n + 255) / 256);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int chsel = d->env_kind == D2D_ENV_CHANNEL_SELECTION;
+  const int C = d->n_channels;
+  if (chsel || C <= 8)
+    hipLaunchKernelGGL(sample_actions_kernel<uint8_t>, dim3(grid), dim3(256), 0, s, d->n_envs, d->n_agents, C, chsel,
+                       d->env_base, d->seed, rng_step, threshold, actions);
+  else if (C <= 16)
+    hipLaunchKernelGGL(sample_actions_kernel<uint16_t>, dim3(grid), dim3(256), 0, s, d->n_envs, d->n_agents, C, 0,
+                       d->env_base, d->seed, rng_step, threshold, actions);
+  else
+    hipLaunchKernelGGL(sample_actions_kernel<uint32_t>, dim3(grid), dim3(256), 0, s, d->n_envs, d->n_agents, C, 0,
+                       d->env_base, d->seed, rng_step, threshold, actions);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}

@@ -1,0 +1,186 @@
+// GAE / discounted-return scan and column normalisation for gfx950.
+//
+// Replaces compute_gae + discount_rewards (/root/reference/algorithms/ippo.py:92-116,
+// identical to algorithms/d2d_ppo.py:100-124).  The reference builds the
+// sequence with list.insert(0, .) (O(T^2)) in float64 and normalises per
+// column (adv: numpy std ddof=0, returns: torch std ddof=1; each gated on ALL
+// columns having std > 0, quirk Q2).
+//
+// Layout [T][E][cols]: for a fixed t, the (env, column) pairs are contiguous,
+// so one thread per (env, column) walking t backwards reads and writes fully
+// coalesced rows; the recursion state (gae, R) lives in f64 registers.
+// Normalisation = deterministic two-level column sums (block partials in a
+// fixed order), so results do not depend on atomics ordering and the stats can
+// be all-reduced across ranks between the passes.
+#include <cmath>
+
+#include "common.h"
+
+namespace d2d {
+
+__global__ __launch_bounds__(256) void gae_scan_kernel(int T, int E, int cols, int rcols, const float* __restrict__ rew,
+                                                       const float* __restrict__ val, const uint8_t* __restrict__ done,
+                                                       double gamma, double lam, int last_shard, float* __restrict__ adv,
+                                                       float* __restrict__ ret) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t width = (int64_t)E * cols;
+  if (i >= width) return;
+  const int e = (int)(i / cols);
+  const bool global_last = last_shard && (e == E - 1);
+  double gae = 0.0, R = 0.0, v_next = 0.0;
+  for (int t = T - 1; t >= 0; --t) {
+    const int64_t o = (int64_t)t * width + i;
+    const double r = (double)rew[rcols == 1 ? (int64_t)t * E + e : o];
+    const double v = (double)val[o];
+    const double nd = done[t] ? 0.0 : 1.0;
+    // discount_rewards: R = r + R * gamma * (1 - done)   (ippo.py:107-109)
+    R = r + R * gamma * nd;
+    double a;
+    if (t == T - 1 && global_last) {
+      a = r - v;  // adv = [rewards[-1] - values[-1]]  (ippo.py:94)
+      gae = 0.0;  // the reference's running gae starts at 0 for step T-2 (ippo.py:93)
+    } else {
+      // delta = r + gamma V' (1-done) - V ; gae = delta + gamma lam (1-done) gae ; adv = gae + V (96-98)
+      const double delta = r + gamma * v_next * nd - v;
+      gae = delta + gamma * lam * nd * gae;
+      a = gae + v;
+    }
+    adv[o] = (float)a;
+    ret[o] = (float)R;
+    v_next = v;
+  }
+}
+
+constexpr int kStatRowBlocks = 1024;
+
+// partial[y][c] = sum over this block's rows of (x - center)^p
+__global__ __launch_bounds__(256) void colstats_partial_kernel(int64_t rows, int cols, int ct, const float* __restrict__ x,
+                                                               const double* __restrict__ center,
+                                                               double* __restrict__ partial) {
+  __shared__ double acc[256];
+  const int cl = threadIdx.x % ct, rl = threadIdx.x / ct, rlanes = blockDim.x / ct;
+  const int c = blockIdx.x * ct + cl;
+  double s = 0.0;
+  if (c < cols) {
+    const double m = center ? center[c] : 0.0;
+    for (int64_t r = (int64_t)blockIdx.y * rlanes + rl; r < rows; r += (int64_t)gridDim.y * rlanes) {
+      const double v = (double)x[r * cols + c] - m;
+      s += center ? v * v : v;
+    }
+  }
+  acc[threadIdx.x] = s;
+  __syncthreads();
+  if (rl == 0 && c < cols) {
+    double t = 0.0;
+    for (int j = 0; j < rlanes; ++j) t += acc[j * ct + cl];
+    partial[(int64_t)blockIdx.y * cols + c] = t;
+  }
+}
+
+__global__ void colstats_reduce_kernel(int nb, int cols, const double* __restrict__ partial, double* __restrict__ out) {
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < cols; c += gridDim.x * blockDim.x) {
+    double t = 0.0;
+    for (int y = 0; y < nb; ++y) t += partial[(int64_t)y * cols + c];
+    out[c] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void colstats_finalize_kernel(int cols, const double* sum, const double* m2, double n,
+                                                                int ddof, double* mean, double* scale, int32_t* gate) {
+  int ok = 1;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    mean[c] = sum[c] / n;
+    if (m2) {
+      const double sd = sqrt(m2[c] / (n - (double)ddof));
+      ok &= sd > 0.0;
+      scale[c] = 1.0 / sd;
+    }
+  }
+  if (m2) {
+    ok = __syncthreads_and(ok);
+    if (threadIdx.x == 0) *gate = ok;
+  }
+}
+
+__global__ __launch_bounds__(256) void normalize_kernel(int64_t n, int cols, float* __restrict__ x,
+                                                        const double* __restrict__ mean,
+                                                        const double* __restrict__ scale, const int32_t* __restrict__ gate) {
+  if (!*gate) return;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % cols);
+    x[i] = (float)(((double)x[i] - mean[c]) * scale[c]);
+  }
+}
+
+}  // namespace d2d
+
+using namespace d2d;
+
+extern "C" int d2d_gae_scan(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards, const float* values,
+                            const uint8_t* dones, double gamma, double lam, int32_t last_shard, float* adv, float* ret,
+                            void* stream) {
+  if (T < 0 || E < 0 || cols < 1 || (reward_cols != 1 && reward_cols != cols) || !rewards || !values || !dones || !adv || !ret) {
+    d2d_set_error("d2d_gae_scan: bad arguments");
+    return D2D_EINVAL;
+  }
+  const int64_t width = (int64_t)E * cols;
+  if (T == 0 || width == 0) return D2D_OK;
+  hipLaunchKernelGGL(gae_scan_kernel, dim3((unsigned)((width + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), T, E, cols, reward_cols, rewards, values, dones, gamma, lam, last_shard,
+                     adv, ret);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
+extern "C" int64_t d2d_colstats_workspace(int64_t rows, int32_t cols) {
+  (void)rows;
+  return (int64_t)kStatRowBlocks * cols;
+}
+
+extern "C" int d2d_colstats(int64_t rows, int32_t cols, const float* x, const double* center, double* partial,
+                            double* out, void* stream) {
+  if (rows < 0 || cols < 1 || !x || !partial || !out) {
+    d2d_set_error("d2d_colstats: bad arguments");
+    return D2D_EINVAL;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  int ct = 1;
+  while (ct < cols && ct < 64) ct <<= 1;
+  const int rlanes = 256 / ct;
+  int64_t nb = (rows + (int64_t)rlanes * 16 - 1) / ((int64_t)rlanes * 16);
+  nb = nb < 1 ? 1 : (nb > kStatRowBlocks ? kStatRowBlocks : nb);
+  hipLaunchKernelGGL(colstats_partial_kernel, dim3((cols + ct - 1) / ct, (unsigned)nb), dim3(256), 0, s, rows, cols, ct,
+                     x, center, partial);
+  D2D_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(colstats_reduce_kernel, dim3((cols + 255) / 256), dim3(256), 0, s, (int)nb, cols, partial, out);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
+extern "C" int d2d_colstats_finalize(int32_t cols, const double* sum, const double* m2, double n, int32_t ddof,
+                                     double* mean, double* scale, int32_t* gate, void* stream) {
+  if (cols < 1 || !sum || !mean || (m2 && (!scale || !gate))) {
+    d2d_set_error("d2d_colstats_finalize: bad arguments");
+    return D2D_EINVAL;
+  }
+  hipLaunchKernelGGL(colstats_finalize_kernel, dim3(1), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), cols, sum,
+                     m2, n, ddof, mean, scale, gate);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
+extern "C" int d2d_normalize_columns(int64_t rows, int32_t cols, float* x, const double* mean, const double* scale,
+                                     const int32_t* gate, void* stream) {
+  if (rows < 0 || cols < 1 || !x || !mean || !scale || !gate) {
+    d2d_set_error("d2d_normalize_columns: bad arguments");
+    return D2D_EINVAL;
+  }
+  const int64_t n = rows * cols;
+  if (n == 0) return D2D_OK;
+  int64_t grid = (n + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(normalize_kernel, dim3((unsigned)grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), n, cols,
+                     x, mean, scale, gate);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}

@@ -1,0 +1,127 @@
+"""ctypes binding of libd2dhip.so (the C ABI declared in include/d2d_hip.h).
+
+The library is built in-tree (`python __graft_entry__.py build` or
+`make -C d2d-ppo_amd`) for gfx950 and loaded AFTER torch, so that it binds to
+the HIP runtime torch already mapped (same SONAME libamdhip64.so.7): device
+pointers and streams are then shared with torch.  There is no CPU fallback:
+every entry point raises if the library cannot be loaded or no GPU is present.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported before the HIP library is loaded)
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libd2dhip.so")
+
+D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION = 0, 1
+D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
+ABI_VERSION = 1
+
+_p = ctypes.c_void_p
+
+
+class EnvDesc(ctypes.Structure):
+    _fields_ = [("env_kind", ctypes.c_int32), ("n_agents", ctypes.c_int32), ("n_channels", ctypes.c_int32),
+                ("max_deadline", ctypes.c_int32), ("obs_dim", ctypes.c_int32), ("state_dim", ctypes.c_int32),
+                ("state_stride", ctypes.c_int32), ("n_envs", ctypes.c_int32), ("env_base", ctypes.c_uint64),
+                ("seed", ctypes.c_uint64), ("agents", _p), ("flip_thr", _p), ("arrival_kind_host", _p),
+                ("period_host", _p), ("offset_host", _p)]
+
+
+class EnvState(ctypes.Structure):
+    _fields_ = [("buffers", _p), ("channels", _p), ("received", _p), ("discarded", _p), ("sel_quality", _p),
+                ("sel_count", _p)]
+
+
+class EnvOut(ctypes.Structure):
+    _fields_ = [("obs", _p), ("state", _p), ("reward", _p), ("ack", _p), ("success", _p)]
+
+
+class EnvReplay(ctypes.Structure):
+    _fields_ = [("flips", _p), ("arrivals", _p)]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "d2d_env_reset": (ctypes.c_int, [ctypes.POINTER(EnvDesc), ctypes.POINTER(EnvState), ctypes.POINTER(EnvReplay),
+                                      ctypes.POINTER(EnvOut), ctypes.c_uint32, _p]),
+    "d2d_env_step": (ctypes.c_int, [ctypes.POINTER(EnvDesc), ctypes.POINTER(EnvState), _p, ctypes.POINTER(EnvReplay),
+                                     ctypes.POINTER(EnvOut), ctypes.c_int32, ctypes.c_uint32, _p]),
+    "d2d_sample_actions": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _p, ctypes.c_uint64, ctypes.c_uint32, _p]),
+    "d2d_mask_bytes": (ctypes.c_int, [ctypes.c_int32]),
+    "d2d_buffer_words": (ctypes.c_int, [ctypes.c_int32]),
+    "d2d_gae_scan": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p, ctypes.c_double,
+                                     ctypes.c_double, ctypes.c_int32, _p, _p, _p]),
+    "d2d_colstats_workspace": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
+    "d2d_colstats": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, _p, _p, _p, _p, _p]),
+    "d2d_colstats_finalize": (ctypes.c_int, [ctypes.c_int32, _p, _p, ctypes.c_double, ctypes.c_int32, _p, _p, _p,
+                                              _p]),
+    "d2d_normalize_columns": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, _p, _p, _p, _p, _p]),
+    "d2d_last_error": (ctypes.c_char_p, []),
+    "d2d_abi_version": (ctypes.c_int, []),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+class D2DHipError(RuntimeError):
+    pass
+
+
+def _hip_runtimes_mapped():
+    try:
+        with open("/proc/self/maps") as fh:
+            return sorted({ln.split()[-1] for ln in fh if "libamdhip64" in ln})
+    except OSError:
+        return []
+
+
+def load(check_single_runtime=True):
+    """Load libd2dhip.so (no GPU needed just to load and inspect the exports)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise D2DHipError(f"HIP extension not built: {LIB_PATH} is missing (run `python __graft_entry__.py build`)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    if lib.d2d_abi_version() != ABI_VERSION:
+        raise D2DHipError(f"libd2dhip ABI {lib.d2d_abi_version()} != {ABI_VERSION}")
+    if check_single_runtime:
+        rts = _hip_runtimes_mapped()
+        if len(rts) > 1:
+            raise D2DHipError(f"two HIP runtimes mapped in this process: {rts}")
+    _lib = lib
+    return lib
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise D2DHipError("the D2D-PPO HIP path needs a ROCm GPU (torch.cuda.is_available() is False); "
+                          "there is no CPU fallback")
+    return load()
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = _lib.d2d_last_error().decode() if _lib is not None else ""
+        if rc == -1:
+            raise ValueError(f"{what}: {msg}")
+        if rc == -2:
+            raise NotImplementedError(f"{what}: {msg}")
+        raise D2DHipError(f"{what} failed ({rc}): {msg}")
+
+
+def ptr(t):
+    """Raw device pointer of a torch tensor (or None)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)

@@ -1,0 +1,165 @@
+/* d2d_hip.h — C ABI of the MI355X (gfx950) D2D-PPO hot path.
+ *
+ * The reference (benrobaglia/D2D-PPO) is pure Python with no FFI; its
+ * "plugin interface" is the duck-typed env/learner API.  These
+ * entry points are what that API's hot methods bind to (ctypes, see
+ * INTEGRATION.md); each cites the reference code it replaces.
+ *
+ * Conventions
+ *   - every buffer is caller-allocated device memory (plain pointers);
+ *   - the `stream` argument is a hipStream_t passed as void*;
+ *   - calls are stream-ordered, never allocate, never synchronise the host,
+ *     and are therefore graph-capturable;
+ *   - return 0 (D2D_OK) or a negative code; d2d_last_error() describes it
+ *     (thread-local string).
+ *   - one stream per env batch; not re-entrant for the same state buffers.
+ *
+ * Env batch = E independent environments with identical parameters (one
+ * rank's shard).  Device layouts, N agents, C channels,
+ * D = max deadline, DW = d2d_buffer_words(D) (1,2,3,4 or 8 uint32 per row):
+ *   buffers   uint32 [E][N][DW]  byte j of agent k's row = packets with j
+ *                                slots to deadline (byte 0 expires next)
+ *   channels  comb : mask [E][N] (uint8 if C<=8, uint16 if C<=16, uint32 if
+ *                    C<=32); bit c = 1 <=> channel c is good for agent k
+ *             chsel: uint32 [E], bit j = state of channel j (0..C)
+ *   actions   comb : mask [E][N] (same width as channels), bit c = attempt on c
+ *             chsel: uint8 [E][N], channel id 0..C (0 = idle)
+ *   obs       float [E][N][obs_dim], agent k's row is prefix-compact:
+ *               comb  [B[k,:w_k], channel_row_k (pre-evolve), ack(C), 0 ...]
+ *               chsel [B[k,:d_k], ack(C+1), 0 ...]
+ *             (w_k = D when homogeneous_size else d_k)
+ *   state     float [E][state_stride], the reference's np.concatenate(state)
+ */
+#ifndef D2D_HIP_H
+#define D2D_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define D2D_ABI_VERSION 1
+
+enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1 };
+enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
+enum { D2D_OK = 0, D2D_EINVAL = -1, D2D_EUNSUPPORTED = -2, D2D_EHIP = -3 };
+
+/* Per-agent parameters, device table [N] (32 bytes each). */
+typedef struct d2d_agent_entry {
+    uint8_t deadline;      /* d_k  (deadlines[k], combinatorial_env.py:9) */
+    uint8_t obs_width;     /* w_k  buffer columns in obs (D if homogeneous_size, :104-107) */
+    uint8_t arrival_kind;  /* D2D_ARRIVAL_*  (traffic model split, :66-85) */
+    uint8_t reserved;
+    int32_t state_offset;  /* sum_{j<k} d_j  (all_buffers concat, :207) */
+    double lam;            /* Poisson mean lbdas[k] */
+    double pois_p0;        /* exp(-lam) */
+    uint64_t arrival_thr;  /* Bernoulli(arrival_probs[k]) threshold floor(q * 2^32) */
+} d2d_agent_entry;
+
+typedef struct d2d_env_desc {
+    int32_t env_kind;       /* D2D_ENV_* */
+    int32_t n_agents;       /* N <= 1024 */
+    int32_t n_channels;     /* C <= 32 (comb), C <= 31 (chsel) */
+    int32_t max_deadline;   /* D <= 32 */
+    int32_t obs_dim;        /* D + 2C (comb) / D + C + 1 (chsel) */
+    int32_t state_dim;      /* sum d + C(N+1) (comb) / sum d + C + 1 (chsel) */
+    int32_t state_stride;   /* >= state_dim, multiple of 4 */
+    int32_t n_envs;         /* E, envs in this batch */
+    uint64_t env_base;      /* global index of env 0 (Philox counter; rank shard offset) */
+    uint64_t seed;          /* Philox key */
+    const d2d_agent_entry* agents;  /* device [N] */
+    const uint64_t* flip_thr;       /* device: comb [N][C], chsel [C+1]; floor(p * 2^32) */
+    /* host-side arrival schedule (evaluated per call, numpy float semantics):
+     * agent k draws at timestep t iff kind==POISSON or
+     * (kind==SCHEDULED_BERNOULLI and fmod(t, period[k]) == offset[k]) */
+    const uint8_t* arrival_kind_host;  /* host [N] */
+    const double* period_host;         /* host [N] */
+    const double* offset_host;         /* host [N] */
+} d2d_env_desc;
+
+typedef struct d2d_env_state {
+    uint32_t* buffers;
+    void* channels;
+    uint32_t* received;     /* [E][N] packets received this episode (received_packets) */
+    uint32_t* discarded;    /* [E][N] packets expired (discarded_packets) */
+    uint32_t* sel_quality;  /* chsel [E] selected_channel_qualities; NULL for comb */
+    uint32_t* sel_count;    /* chsel [E] number_selected_channel; NULL for comb */
+} d2d_env_state;
+
+typedef struct d2d_env_out {  /* any field may be NULL */
+    float* obs;         /* [E][N][obs_dim] */
+    float* state;       /* [E][state_stride] */
+    int32_t* reward;    /* [E]  |successful users| (broadcast to all agents by the host) */
+    void* ack;          /* comb int8 [E][C] in {-1,0,1}; chsel double [E][C+1] */
+    uint8_t* success;   /* [E][N] 1 if agent k delivered a packet this slot */
+} d2d_env_out;
+
+typedef struct d2d_env_replay {  /* parity mode; both NULL = Philox production stream */
+    const void* flips;        /* comb mask [E][N]; chsel uint32 [E] */
+    const uint8_t* arrivals;  /* [E][N] arrival value for agents that draw at this call */
+} d2d_env_replay;
+
+/* Replaces CombinatorialEnv.reset (envs/combinatorial_env.py:61-114) and
+ * ChannelSelectionEnv.reset (envs/channel_selection_env.py:49-98). */
+int d2d_env_reset(const d2d_env_desc* desc, const d2d_env_state* st, const d2d_env_replay* replay,
+                  const d2d_env_out* out, uint32_t rng_step, void* stream);
+
+/* Replaces CombinatorialEnv.step (envs/combinatorial_env.py:127-242, with
+ * evolve_channel 116-118 and evolve_buffer 120-124) and
+ * ChannelSelectionEnv.step (envs/channel_selection_env.py:116-214).
+ * `timestep` is the value after the increment (t = 1, 2, ...). */
+int d2d_env_step(const d2d_env_desc* desc, const d2d_env_state* st, const void* actions,
+                 const d2d_env_replay* replay, const d2d_env_out* out, int32_t timestep, uint32_t rng_step,
+                 void* stream);
+
+/* Synthetic actions (env-only benchmark; replaces the per-agent
+ * np.random.binomial of baselines.CombinatorialRandomAccess.act,
+ * algorithms/baselines.py:181-183): comb mask bit c ~ Bernoulli(thr/2^32);
+ * chsel uniform channel id in 0..C. */
+int d2d_sample_actions(const d2d_env_desc* desc, void* actions, uint64_t threshold, uint32_t rng_step,
+                       void* stream);
+
+/* Bytes of one comb channel/action mask for C channels (1, 2 or 4). */
+int d2d_mask_bytes(int32_t n_channels);
+
+/* uint32 words per agent buffer row for max deadline D (D<=4:1, <=8:2, <=12:3, <=16:4, <=32:8). */
+int d2d_buffer_words(int32_t max_deadline);
+
+/* ---- GAE / discounted returns (algorithms/ippo.py:92-116 == d2d_ppo.py:100-124) ----
+ * Sequence semantics: the batch is the reference's sequential rollout of the
+ * E envs' episodes in env-major order, so row (t, e) of column c follows
+ *   R = r + gamma * R' * (1 - done_t),  delta = r + gamma V' (1-done_t) - V,
+ *   gae = delta + gamma*lam*(1-done_t)*gae,  adv = gae + V  (quirk Q1),
+ * except the globally last element (e = E-1, t = T-1 on the last shard),
+ * whose adv is r - V (ippo.py:94).
+ *   rewards [T][E][reward_cols] (reward_cols 1 = broadcast over columns, or cols),
+ *   values [T][E][cols], dones [T] (every env's sequence ends at t = T-1)
+ *   adv, ret [T][E][cols] float (raw, un-normalised)                     */
+int d2d_gae_scan(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards, const float* values,
+                 const uint8_t* dones, double gamma, double lam, int32_t last_shard, float* adv, float* ret,
+                 void* stream);
+
+/* Column sums over rows of x [rows][cols]: out[c] = sum_r (x[r][c] - center[c])^p,
+ * p = 1 when center == NULL else 2.  Deterministic two-level reduction in
+ * double; `partial` is a workspace of d2d_colstats_workspace(rows, cols) doubles. */
+int64_t d2d_colstats_workspace(int64_t rows, int32_t cols);
+int d2d_colstats(int64_t rows, int32_t cols, const float* x, const double* center, double* partial,
+                 double* out, void* stream);
+
+/* mean = sum / n ; when m2 != NULL: std = sqrt(m2 / (n - ddof)), scale = 1/std and
+ * *gate = all columns std > 0 (ippo.py:100-101, 114-115); when m2 == NULL only mean. */
+int d2d_colstats_finalize(int32_t cols, const double* sum, const double* m2, double n, int32_t ddof,
+                          double* mean, double* scale, int32_t* gate, void* stream);
+
+/* x = gate ? (x - mean) * scale : x  (per column) */
+int d2d_normalize_columns(int64_t rows, int32_t cols, float* x, const double* mean, const double* scale,
+                          const int32_t* gate, void* stream);
+
+const char* d2d_last_error(void);
+int d2d_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* D2D_HIP_H */

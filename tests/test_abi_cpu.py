@@ -1,0 +1,119 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads and exports
+every symbol include/d2d_hip.h declares (no compute calls without a GPU), the
+ctypes structs match the header layout, and the host logic (spec derivation,
+mask packing, reference-API attributes) behaves like the reference."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "d2d_hip.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(d2d_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    import d2dhip
+    lib = d2dhip.load()
+    fns = header_functions()
+    assert len(fns) >= 12
+    for fn in fns:
+        assert hasattr(lib, fn), fn
+        assert fn in d2dhip.EXPORTED, f"{fn} has no ctypes signature"
+    assert lib.d2d_abi_version() == 1
+    assert [lib.d2d_mask_bytes(c) for c in (1, 8, 9, 16, 17, 32)] == [1, 1, 2, 2, 4, 4]
+    assert [lib.d2d_buffer_words(d) for d in (1, 4, 5, 8, 12, 14, 16, 17, 32)] == [1, 1, 2, 2, 3, 4, 4, 8, 8]
+    assert lib.d2d_colstats_workspace(1000, 64) >= 64
+
+
+def test_ctypes_structs_match_header_layout():
+    from d2dhip import _lib
+    from d2dhip.spec import AGENT_DTYPE
+    assert AGENT_DTYPE.itemsize == 32
+    assert ctypes.sizeof(_lib.EnvDesc) == 8 * 4 + 8 * 2 + 8 * 5
+    assert ctypes.sizeof(_lib.EnvState) == 6 * 8 and ctypes.sizeof(_lib.EnvOut) == 5 * 8
+    assert ctypes.sizeof(_lib.EnvReplay) == 2 * 8
+
+
+def test_library_validates_arguments_without_gpu():
+    """Argument checks run before any HIP call, so they work on a GPU-less host."""
+    import d2dhip
+    from d2dhip import _lib
+    lib = d2dhip.load()
+    rc = lib.d2d_env_step(None, None, None, None, None, 1, 0, None)
+    assert rc == -1 and b"desc" in lib.d2d_last_error()
+    desc = _lib.EnvDesc(0, 2000, 8, 7, 23, 0, 0, 1, 0, 0, None, None, None, None, None)
+    assert lib.d2d_env_reset(ctypes.byref(desc), None, None, None, 0, None) == -2
+    assert lib.d2d_gae_scan(10, 1, 0, 1, None, None, None, 0.9, 0.97, 1, None, None, None) == -1
+
+
+def test_gpu_required_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("host has a GPU")
+    from envs.combinatorial_env import CombinatorialEnv
+    import d2dhip
+    e = CombinatorialEnv(2, 2, np.array([3, 3]), np.ones(2))
+    with pytest.raises(d2dhip.D2DHipError, match="no CPU fallback"):
+        e.reset()
+
+
+def test_spec_matches_reference_spaces():
+    from envs.channel_selection_env import ChannelSelectionEnv
+    from envs.combinatorial_env import CombinatorialEnv
+    d = np.array([7, 14] * 3)
+    e = CombinatorialEnv(6, 8, d, np.ones(6) * 0.5, homogeneous_size=True)
+    assert [s.shape[0] for s in e.observation_space] == [30] * 6            # combinatorial_env.py:52-53
+    assert e.state_space.shape == (int(d.sum()) + 8 * 7,)                   # :57-58
+    assert [s.n for s in e.action_space] == [8] * 6
+    e2 = CombinatorialEnv(6, 8, d, np.ones(6) * 0.5)
+    assert [s.shape[0] for s in e2.observation_space] == list(d + 16)       # :49-50
+    assert np.array_equal(e2.spec.obs_len, d + 16) and e2.spec.F == 30
+    c = ChannelSelectionEnv(5, 16, np.array([7] * 5), np.ones(5), channel_switch=np.full(17, 0.8))
+    assert [s.n for s in c.action_space] == [17] * 5                         # channel_selection_env.py:43
+    assert c.state_space.shape == (35 + 17,)
+    assert c.spec.F == 7 + 17
+
+
+def test_spec_traffic_models_and_errors():
+    from d2dhip.spec import EnvSpec, POISSON, SCHEDULED
+    mk = lambda tm, pdev=(): EnvSpec("comb", 4, 2, [3, 3, 3, 3], [0.5] * 4, 2, [1] * 4, [0] * 4, 10, tm, pdev,  # noqa
+                                     False, None)
+    assert list(mk("aperiodic").arrival_kinds()) == [POISSON] * 4
+    assert list(mk("periodic").arrival_kinds()) == [SCHEDULED] * 4
+    assert list(mk("heterogeneous", np.array([1, 3])).arrival_kinds()) == [POISSON, SCHEDULED, POISSON, SCHEDULED]
+    with pytest.raises(ValueError, match="traffic model not supported"):
+        mk("bursty").arrival_kinds()
+    with pytest.raises(AssertionError):
+        mk("heterogeneous", []).arrival_kinds()
+    # 1-D channel_switch broadcasts over agents (run_ippo_combinatorial.py:34)
+    s = EnvSpec("comb", 3, 4, [2, 2, 2], [1] * 3, 5, None, None, 10, "aperiodic", [], False, np.array([.1, .2, .3, .4]))
+    assert s.switch.shape == (3, 4) and np.all(s.switch[2] == [.1, .2, .3, .4])
+    # chsel needs C+1 switch probabilities (channel_selection_env.py:105)
+    with pytest.raises(IndexError):
+        EnvSpec("chsel", 3, 4, [2, 2, 2], [1] * 3, 5, None, None, 10, "aperiodic", [], False, np.array([.1] * 4))
+
+
+def test_mask_packing_roundtrip():
+    from d2dhip.envbatch import pack_masks
+    rng = np.random.default_rng(0)
+    for C in (1, 5, 8, 12, 16, 23, 32):
+        bits = rng.integers(0, 2, size=(7, 3, C))
+        m = pack_masks(bits, C)
+        raw = np.ascontiguousarray(m).view(np.uint8).reshape(7, 3, -1)
+        back = np.unpackbits(raw, axis=2, bitorder="little")[:, :, :C]
+        assert np.array_equal(back, bits)
+
+
+def test_bernoulli_threshold_edges():
+    from d2dhip.spec import bernoulli_threshold
+    t = bernoulli_threshold([0.0, 1.0, 0.5, 0.2])
+    assert list(t) == [0, 2 ** 32, 2 ** 31, int(np.floor(0.2 * 2 ** 32))]
