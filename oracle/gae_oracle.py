@@ -26,8 +26,10 @@ def compute_gae_seq(rewards, dones, values, gamma, lbda):
     return adv.astype(np.float32)
 
 
-def discount_rewards_seq(rewards, gamma, dones, normalize=True):
-    """Reference semantics (ippo.py:104-116): float64 recursion, float32 cast, ddof=1 normalisation."""
+def discount_rewards_seq(rewards, gamma, dones, normalize=True, exact_stats=False):
+    """Reference semantics (ippo.py:104-116): float64 recursion, float32 cast, ddof=1 normalisation.
+    exact_stats: take mean/std in float64 instead of the reference's float32 (at 1e5+ rows the
+    reference's own float32 reduction noise exceeds 1e-5; the batched checks compare exact values)."""
     r = np.asarray(rewards, dtype=np.float64)
     d = np.asarray(dones, dtype=np.float64)
     out = np.zeros_like(r)
@@ -37,9 +39,10 @@ def discount_rewards_seq(rewards, gamma, dones, normalize=True):
         out[i] = R
     out = out.astype(np.float32)
     if normalize:
-        sd = out.std(0, ddof=1)
+        x = out.astype(np.float64) if exact_stats else out
+        sd = x.std(0, ddof=1)
         if (sd > 0).all():
-            out = (out - out.mean(0)) / sd
+            out = ((x - x.mean(0)) / sd).astype(np.float32)
     return out
 
 
@@ -54,6 +57,6 @@ def gae_returns_batched(rewards, values, dones, gamma, lbda):
     seq = lambda x: np.transpose(x, (1, 0, 2)).reshape(E * T, cols)  # noqa: E731
     d = np.tile(np.asarray(dones, dtype=np.float64), E)
     adv = compute_gae_seq(seq(r), d, seq(v), gamma, lbda)
-    ret = discount_rewards_seq(seq(r), gamma, d, True)
+    ret = discount_rewards_seq(seq(r), gamma, d, True, exact_stats=True)
     back = lambda x: np.transpose(x.reshape(E, T, cols), (1, 0, 2))  # noqa: E731
     return back(adv), back(ret)
