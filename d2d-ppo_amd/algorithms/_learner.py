@@ -1,0 +1,268 @@
+"""Device-resident rollout collection / evaluation shared by iPPO and D2DPPO.
+
+Reference loops replaced (all per agent, per step, batch-1, host<->device
+round trips):
+  create_rollouts  /root/reference/algorithms/ippo.py:277-343, d2d_ppo.py:279-339
+  test             ippo.py:345-388, d2d_ppo.py:341-383
+  preprocess_input_for_rnn  ippo.py:390-403, d2d_ppo.py:385-398
+
+Here one slot for all agents of all `env.n_envs` envs is:
+  policy forward for all agents (agent-stacked bmm) -> sample -> pack the
+  actions into channel masks -> one env-step kernel writing the next obs /
+  state straight into the rollout buffers.
+Nothing leaves the GPU until an episode ends (scores).
+
+Sequence order: a rollout of E envs x W waves of full episodes is the
+reference's sequential rollout of E*W episodes in env-major order
+(env 0's episodes, then env 1's, ...); GAE, normalisation and the update
+all use that order.
+"""
+import math
+
+import numpy as np
+import torch
+
+from d2dhip.envbatch import pack_masks_torch
+from d2dhip.gae import gae_returns
+
+from ._core import make_dist, rnn_windows, unpack_actions
+
+
+class Rollout:
+    """Device tensors of one rollout ([T][E]... time-major as produced)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+class BatchedLearnerBase:
+    combinatorial = False
+    useRNN = False
+
+    # ------------------------------------------------------------- setup
+    def _resolve_device(self, device):
+        if device is None:
+            dev = torch.device('cuda' if torch.cuda.is_available() else "cpu")
+        else:
+            dev = torch.device(device)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        return dev
+
+    def _bind_env(self):
+        env = self.env
+        if getattr(env, "_batch", None) is None:
+            env.device = self.device
+        elif env._batch.device != self.device:
+            raise ValueError(f"env lives on {env._batch.device}, learner on {self.device}")
+        return env.batch()
+
+    @property
+    def kind(self):
+        return self.env.kind
+
+    def _policy_act(self):
+        if self.useRNN:
+            return "sigmoid" if self.combinatorial else "softmax"
+        return "softmax"  # Policy always ends in softmax (ippo.py:73), Bernoulli of softmax probs (quirk Q6)
+
+    # -------------------------------------------------------- obs plumbing
+    def _agent_major(self, obs_t):
+        """[E][N][F] -> [N][E][F]"""
+        return obs_t.transpose(0, 1)
+
+    def _window(self, obs_buf, ep_start, i):
+        """RNN input at step i: last <= history_len obs of the current episode, unpadded
+        (ippo.py:302-304), as [N][E][w][F]."""
+        lo = max(ep_start, i - self.history_len + 1)
+        return obs_buf[lo: i + 1].permute(2, 1, 0, 3)
+
+    def _policy_input(self, obs_buf, ep_start, i):
+        if self.useRNN:
+            return self._window(obs_buf, ep_start, i)
+        return self._agent_major(obs_buf[i])
+
+    def _actions_from_probs(self, probs, train):
+        if self.combinatorial:
+            if train:
+                a = torch.bernoulli(probs)
+            else:
+                a = (probs > 0.5).to(probs.dtype)
+            dist = make_dist(probs, True)
+            return a, dist.log_prob(a).mean(-1)
+        if train:
+            a = torch.multinomial(probs.reshape(-1, probs.shape[-1]), 1).view(probs.shape[:-1])
+        else:
+            a = probs.argmax(dim=-1)
+        dist = make_dist(probs, False)
+        return a, dist.log_prob(a)
+
+    def _env_actions(self, a):
+        """agent-major sampled actions -> env action buffer [E][N]"""
+        if self.kind == "comb":
+            return pack_masks_torch(a.transpose(0, 1))
+        return a.transpose(0, 1).to(torch.uint8).contiguous()
+
+    # ------------------------------------------------------------ rollout
+    def _collect(self, num_episodes, train=True, want_values=False, want_state=False, teacher=None):
+        """teacher (parity testing, n_envs == 1): recorded reference actions and env draws,
+        dict(actions [T][N][C|1], reset_arrivals [W][N], flips [T][..], arrivals [T][N]);
+        the policy still computes probs/log-probs/values, of the forced actions."""
+        b = self._bind_env()
+        env = self.env
+        s = b.spec
+        E, L, N, Fd = b.E, env.episode_length, s.N, s.F
+        waves = max(1, math.ceil(num_episodes / E))
+        T = waves * L
+        dev = self.device
+        obs_buf = torch.empty((T, E, N, Fd), dtype=torch.float32, device=dev)
+        act_buf = torch.empty((T, E, N), dtype=b.action_buffer().dtype, device=dev)
+        logp_buf = torch.empty((T, N, E), dtype=torch.float32, device=dev)
+        rew_i32 = torch.empty((T, E), dtype=torch.int32, device=dev)
+        val_buf = torch.empty((T, N, E), dtype=torch.float32, device=dev) if want_values else None
+        state_buf = torch.empty((T, E, s.state_stride), dtype=torch.float32, device=dev) if want_state else None
+        scores, ep_rewards, jains = [], [], []
+        tf = self._teacher_tensors(teacher, b, T) if teacher is not None else None
+        with torch.no_grad():
+            for w in range(waves):
+                t0 = w * L
+                env.reset_batched(want_obs=True, want_state=want_state, out_obs=obs_buf[t0],
+                                  out_state=state_buf[t0] if want_state else None,
+                                  replay_arrivals=None if tf is None else tf["reset_arrivals"][w])
+                for t in range(L):
+                    i = t0 + t
+                    x = self._policy_input(obs_buf, t0, i)
+                    probs = self.policy.forward(x)
+                    if tf is None:
+                        a, logp = self._actions_from_probs(probs, train)
+                    else:
+                        a = tf["actions"][i]
+                        dist = make_dist(probs, self.combinatorial)
+                        logp = dist.log_prob(a).mean(-1) if self.combinatorial else dist.log_prob(a)
+                    logp_buf[i] = logp
+                    if want_values:
+                        val_buf[i] = self.value.forward(x)[..., 0]
+                    act = self._env_actions(a)
+                    act_buf[i] = act
+                    last = t + 1 == L
+                    env.step_batched(act, want_obs=not last, want_state=want_state and not last,
+                                     out_obs=None if last else obs_buf[i + 1],
+                                     out_state=None if (last or not want_state) else state_buf[i + 1],
+                                     out_reward=rew_i32[i], replay=None if tf is None else tf["replay"][i])
+                recv = b.received.sum(1).double()
+                disc = b.discarded.sum(1).double()
+                scores.extend((1 - disc / recv).cpu().tolist())
+                ep_rewards.extend(rew_i32[t0:t0 + L].double().sum(0).cpu().tolist())
+                if not train:
+                    jains.extend(self._jains(b))
+        dones = torch.zeros(T, dtype=torch.uint8, device=dev)
+        dones[L - 1::L] = 1
+        return Rollout(obs=obs_buf, actions=act_buf, logp=logp_buf, rewards=rew_i32.float(), values=val_buf,
+                       states=state_buf, dones=dones, scores=scores, ep_rewards=ep_rewards, jains=jains, T=T, E=E,
+                       waves=waves, L=L)
+
+    def _teacher_tensors(self, teacher, b, T):
+        from d2dhip.envbatch import pack_masks
+        if b.E != 1:
+            raise ValueError("teacher forcing needs n_envs == 1")
+        s, dev = b.spec, b.device
+        acts = np.asarray(teacher["actions"], dtype=np.float64)[:T]
+        if self.combinatorial:
+            a = torch.from_numpy(acts.reshape(T, s.N, 1, -1).astype(np.float32)).to(dev)       # [T][N][1][C]
+        else:
+            a = torch.from_numpy(acts.reshape(T, s.N, 1).astype(np.int64)).to(dev)             # [T][N][1]
+        fl = np.asarray(teacher["flips"])[:T]
+        arr = np.asarray(teacher["arrivals"])[:T].astype(np.uint8)
+        replay = []
+        for i in range(T):
+            if s.kind == "comb":
+                f = torch.from_numpy(np.ascontiguousarray(pack_masks(fl[i][None], s.C))).to(dev)
+            else:
+                word = int((fl[i].astype(np.int64) << np.arange(fl[i].shape[-1])).sum())
+                f = torch.tensor([word], dtype=torch.int32, device=dev)
+            replay.append((f, torch.from_numpy(arr[i][None].copy()).to(dev)))
+        ra = [torch.from_numpy(np.asarray(r, dtype=np.uint8)[None].copy()).to(dev) for r in teacher["reset_arrivals"]]
+        return {"actions": a, "replay": replay, "reset_arrivals": ra}
+
+    @staticmethod
+    def _jains(b):
+        recv = b.received.double()
+        disc = b.discarded.double()
+        u = torch.where(recv > 0, 1 - disc / recv.clamp(min=1), torch.ones_like(recv))
+        j = u.sum(1) ** 2 / recv.shape[1] / (u ** 2).sum(1)
+        return j.cpu().tolist()
+
+    # ------------------------------------------------------ update inputs
+    def _seq(self, x_tne):
+        """[T][N][E] -> [N][E*T] (env-major sample order)"""
+        return x_tne.permute(1, 2, 0).reshape(x_tne.shape[1], -1)
+
+    def _update_inputs(self, ro):
+        """Agent-major update tensors from a rollout."""
+        s = self.env.batch().spec
+        N = s.N
+        if self.useRNN:
+            seq = ro.obs.permute(1, 2, 0, 3).reshape(ro.E * N, ro.T, -1)          # [E*N][T][F]
+            win = rnn_windows(seq, self.history_len, ro.L)                        # [E*N][T][L][F]
+            x = win.view(ro.E, N, ro.T, self.history_len, -1).transpose(0, 1).reshape(N, ro.E * ro.T,
+                                                                                       self.history_len, -1)
+        else:
+            x = ro.obs.permute(2, 1, 0, 3).reshape(N, ro.E * ro.T, -1)
+        acts = ro.actions.permute(2, 1, 0).reshape(N, -1)                        # [N][E*T]
+        if self.kind == "comb":
+            acts = unpack_actions(acts, s.C)                                      # [N][B][C]
+        else:
+            acts = acts.long()
+        return x, acts, self._seq(ro.logp)
+
+    def _evaluate(self, x, acts):
+        probs = self.policy.forward(x)
+        dist = make_dist(probs, self.combinatorial)
+        if self.combinatorial:
+            return dist.log_prob(acts).mean(-1), dist.entropy().mean(-1)
+        return dist.log_prob(acts), dist.entropy()
+
+    # ------------------------------------------------------------- test
+    def test(self, num_episodes):
+        ro = self._collect(num_episodes, train=False)
+        n = num_episodes
+        sc = np.array(ro.scores[:n], dtype=np.float64)
+        ja = np.array(ro.jains[:n], dtype=np.float64)
+        rw = np.array(ro.ep_rewards[:n], dtype=np.float64)
+        ch = 0  # channel_errors is never incremented by these envs (combinatorial_env.py:97)
+        return np.mean(sc), np.mean(ja), np.sum([ch] * n), np.mean(rw)
+
+    # --------------------------------------------------------- save/load
+    def save(self, checkpoint_path):
+        for i, agent in enumerate(self.agents):
+            sd = {k: v.detach().clone().cpu() for k, v in agent.policy_network.state_dict().items()}
+            torch.save(sd, f"{checkpoint_path}/agent_{i}.pth")
+        print("Models saved!")
+
+    def load(self, checkpoint_path):
+        for i, agent in enumerate(self.agents):
+            sd = torch.load(f"{checkpoint_path}/agent_{i}.pth", map_location=self.device, weights_only=True)
+            agent.policy_network.load_state_dict(sd)
+        print("Models loaded!")
+
+    def preprocess_input_for_rnn(self, obs_agent):
+        """(T, in) -> (T, history_len, in), front-zero-padded per episode (ippo.py:390-403)."""
+        return rnn_windows(obs_agent.unsqueeze(0), self.history_len, self.env.episode_length)[0]
+
+    # ----------------------------------------------------- GAE wrapper
+    def _gae(self, rewards_te, values_tec, dones, normalize_adv=True, normalize_ret=True):
+        return gae_returns(rewards_te, values_tec, dones, self.gamma, 0.97, normalize_adv=normalize_adv,
+                           normalize_ret=normalize_ret, group=self.process_group,
+                           last_shard=self._last_shard(), n_envs_total=self._n_envs_total())
+
+    # data-parallel hooks (algorithms/data_parallel.py); single process: identity
+    process_group = None
+
+    def _reduce_grads(self, params):
+        pass
+
+    def _last_shard(self):
+        return True
+
+    def _n_envs_total(self):
+        return None

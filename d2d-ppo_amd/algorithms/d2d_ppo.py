@@ -1,0 +1,228 @@
+"""D2D-PPO — drop-in for /root/reference/algorithms/d2d_ppo.py (HAPPO-style:
+per-agent actors, one centralized critic on the global state at the BS,
+random agent permutation per epoch, compound ratio M passed agent to agent).
+
+The sequential chain (d2d_ppo.py:429-436) feeds agent sigma_j the advantage
+times the ratios of the agents before it, each computed from that agent's
+parameters BEFORE its own optimizer step — and no agent's parameters change
+until its own turn.  So M_{sigma_j} = A * r_{sigma_0} * ... * r_{sigma_{j-1}}
+with every r from the epoch-start parameters: an exclusive prefix product
+along the permutation.  All N actor updates of an epoch therefore
+run as ONE agent-stacked forward/backward; the prefix is N elementwise
+multiplies over [B] in sigma order, left to right exactly like the
+reference's loop.  Per-agent clip_grad_norm_(20) and Adam are kept.
+"""
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ._core import Policy, RNN, StackedNets, Value, init_weights, make_dist  # noqa: F401
+from ._learner import BatchedLearnerBase
+from .ippo import compute_gae, discount_rewards  # noqa: F401  (identical in both reference modules)
+
+
+class PPO:
+    """Per-agent actor (d2d_ppo.py:128-216)."""
+
+    def __init__(self, num_inputs, n_actions, hidden_size=128, gamma=0.99, policy_lr=1e-3, beta_entropy=0.01,
+                 useRNN=False, combinatorial=False, device='cpu', history_len=5, early_stopping=True):
+        self.history_len = history_len
+        self.useRNN = useRNN
+        self.combinatorial = combinatorial
+        self.early_stopping = early_stopping
+        self.device = torch.device(device)
+        self.n_actions = n_actions
+        self.beta_entropy = beta_entropy
+        if not self.useRNN:
+            self.policy_network = Policy(num_inputs, n_actions, hidden_size)
+        else:
+            self.policy_network = RNN(num_inputs, n_actions, hidden_size, combinatorial=combinatorial)
+        self.gamma = gamma
+        self.policy_lr = policy_lr
+        self.policy_optimizer = None
+
+    def select_action(self, state, train=True):
+        probs = self.policy_network(state.to(self.device))
+        dist = make_dist(probs, self.combinatorial)
+        if self.combinatorial:
+            action = dist.sample().squeeze() if train else (dist.probs.squeeze() > 0.5) * 1.
+            return action.cpu().detach().numpy(), dist.log_prob(action).mean(-1), dist.entropy().mean(-1)
+        action = dist.sample() if train else probs.argmax(dim=1)
+        return action.cpu().detach().numpy(), dist.log_prob(action), dist.entropy()
+
+    def evaluate(self, states, actions):
+        probs = self.policy_network(states.to(self.device).squeeze())
+        dist = make_dist(probs, self.combinatorial)
+        a = torch.as_tensor(actions).to(self.device)
+        if self.combinatorial:
+            return dist.log_prob(a).mean(-1), dist.entropy().mean(-1)
+        return dist.log_prob(a), dist.entropy()
+
+    def train_step(self, states, actions, log_probs_old, M, cliprange=0.1):
+        if self.policy_optimizer is None:
+            self.policy_optimizer = torch.optim.Adam(self.policy_network.parameters(), lr=self.policy_lr)
+        M = M.to(self.device)
+        log_probs, entropy = self.evaluate(states, actions)
+        entropy = entropy.mean()
+        ratio = torch.exp(log_probs - log_probs_old.to(self.device))
+        policy_loss = -torch.min(ratio * M, torch.clamp(ratio, 1.0 - cliprange, 1.0 + cliprange) * M).mean() \
+            - self.beta_entropy * entropy
+        self.policy_optimizer.zero_grad()
+        policy_loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.policy_network.parameters(), 20)
+        self.policy_optimizer.step()
+        return policy_loss.item(), ratio * M
+
+
+def happo_chain(adv, ratio, perm):
+    """M for every agent: adv [B], ratio [N][B] (detached), perm = sigma (np array of agent ids).
+    M[sigma_j] = (((adv * r_sigma0) * r_sigma1) ... * r_sigma_{j-1}), multiplied left to right in
+    float32 exactly like the reference's loop (torch.cumprod may accumulate in double on CPU)."""
+    N = ratio.shape[0]
+    perm = [int(i) for i in np.asarray(perm)]
+    M = torch.empty_like(ratio)
+    cur = adv
+    for j, i in enumerate(perm):
+        M[i] = cur
+        if j + 1 < N:
+            cur = ratio[i] * cur
+    return M
+
+
+class D2DPPO(BatchedLearnerBase):
+    def __init__(self,
+                 env,
+                 hidden_size=128,
+                 gamma=0.99,
+                 policy_lr=1e-3,
+                 value_lr=1e-3,
+                 beta_entropy=0.01,
+                 device=None,
+                 useRNN=False,
+                 save_path=None,
+                 combinatorial=False,
+                 history_len=10,
+                 early_stopping=True):
+        self.env = env
+        self.history_len = history_len
+        self.n_agents = env.n_agents
+        self.hidden_size = hidden_size
+        self.gamma = gamma
+        self.policy_lr = policy_lr,   # tuples, as in the reference (d2d_ppo.py:239-240)
+        self.value_lr = value_lr,
+        self.beta_entropy = beta_entropy
+        self.early_stopping = early_stopping
+        self.useRNN = useRNN
+        self.save_path = save_path
+        self.combinatorial = combinatorial
+        self.device = self._resolve_device(device)
+        if self.device.type != "cuda":
+            import d2dhip
+            d2dhip.require_gpu()
+        self.agents = [PPO(num_inputs=self.env.observation_space[k].shape[0],
+                           n_actions=self.env.action_space[k].n,
+                           hidden_size=hidden_size,
+                           gamma=gamma,
+                           policy_lr=policy_lr,
+                           beta_entropy=beta_entropy,
+                           useRNN=useRNN,
+                           combinatorial=combinatorial,
+                           history_len=history_len,
+                           device=self.device,
+                           early_stopping=early_stopping) for k in range(self.n_agents)]
+        # The value network is at the BS (d2d_ppo.py:264-267)
+        self.value_network = Value(self.env.state_space.shape[0], hidden_size)
+        self.value_network = self.value_network.to(self.device)
+        self.value_optimizer = torch.optim.Adam(self.value_network.parameters(), lr=value_lr)
+        in_dims = [env.observation_space[k].shape[0] for k in range(self.n_agents)]
+        self.policy = StackedNets([a.policy_network for a in self.agents], in_dims,
+                                  "rnn" if useRNN else "mlp", self.device, act=self._policy_act())
+        self.policy_optimizer = torch.optim.Adam(self.policy.parameters(), lr=policy_lr)
+
+    # ------------------------------------------------------------ rollouts
+    def _rollout(self, num_episodes, teacher=None):
+        ro = self._collect(num_episodes, train=True, want_state=True, teacher=teacher)
+        S = self.env.state_space.shape[0]
+        ro.state_seq = ro.states[:, :, :S].transpose(0, 1).reshape(ro.E * ro.T, S)     # [E*T][S]
+        # returns = discount_rewards(rewards (T,N)).mean(1) (d2d_ppo.py:333,339): every agent has the
+        # same reward, so all N normalised columns are identical and their mean is that column
+        zero_v = torch.zeros((ro.T, ro.E, 1), dtype=torch.float32, device=self.device)
+        _, ret = self._gae(ro.rewards, zero_v, ro.dones, normalize_adv=False, normalize_ret=True)
+        ro.ret_mean = ret[:, :, 0].t().reshape(-1)                                     # [E*T]
+        return ro
+
+    def create_rollouts(self, num_episodes=4):
+        """Reference return structure (d2d_ppo.py:339): obs list, states (T,S), actions, log_probs (T,N),
+        rewards.mean(1), returns.mean(1), scores, dones (env-major sample axis when n_envs > 1)."""
+        ro = self._rollout(num_episodes)
+        s = self.env.batch().spec
+        N = s.N
+        obs = ro.obs.permute(2, 1, 0, 3).reshape(N, ro.E * ro.T, -1)
+        obs_list = [obs[k, :, : s.obs_len[k]] for k in range(N)]
+        acts = ro.actions.permute(1, 0, 2).reshape(ro.E * ro.T, N)
+        if self.kind == "comb":
+            from ._core import unpack_actions
+            acts = unpack_actions(acts, s.C)
+        rewards = ro.rewards.t().reshape(-1).double().cpu().numpy()
+        dones = [bool(d) for d in ro.dones.cpu().tolist()] * ro.E
+        return (obs_list, ro.state_seq, acts.cpu().numpy(), self._seq(ro.logp).t().cpu(), rewards,
+                ro.ret_mean.cpu(), ro.scores, dones)
+
+    # -------------------------------------------------------------- update
+    def _epoch(self, ro, x, acts, logp_old, cliprange=0.1):
+        """One reference epoch (d2d_ppo.py:413-448) for all agents at once."""
+        # 1) Sample a cycle of agents — the global numpy stream, exactly like the reference
+        cycle = np.arange(self.n_agents)
+        np.random.shuffle(cycle)
+        # 2) global advantage at the BS
+        values = self.value_network(ro.state_seq).squeeze()
+        v_te = values.detach().view(ro.E, ro.T).t().unsqueeze(2).contiguous()
+        adv, _ = self._gae(ro.rewards, v_te, ro.dones, normalize_adv=True, normalize_ret=False)
+        A = adv[:, :, 0].t().reshape(-1)                                                # [E*T]
+        # 3) the agents' chain as one batched update
+        log_probs, entropy = self._evaluate(x, acts)
+        ratio = torch.exp(log_probs - logp_old)                                          # [N][B]
+        M = happo_chain(A, ratio.detach(), cycle)
+        surr1 = ratio * M
+        surr2 = torch.clamp(ratio, 1.0 - cliprange, 1.0 + cliprange) * M
+        ploss = -torch.min(surr1, surr2).mean(1) - self.beta_entropy * entropy.mean(1)    # [N]
+        self.policy_optimizer.zero_grad()
+        ploss.sum().backward()
+        self._reduce_grads(self.policy.parameters())
+        self.policy.grad_norm_clip_(20)
+        self.policy_optimizer.step()
+        # 4) critic update (d2d_ppo.py:440-446)
+        value_loss = F.mse_loss(values, ro.ret_mean, reduction='mean')
+        self.value_optimizer.zero_grad()
+        value_loss.backward()
+        self._reduce_grads(list(self.value_network.parameters()))
+        torch.nn.utils.clip_grad_norm_(self.value_network.parameters(), 20)
+        self.value_optimizer.step()
+        pl = ploss.detach().cpu().numpy()
+        return [float(pl[i]) for i in cycle], value_loss.detach()
+
+    def train(self, num_iter, num_episodes=4, n_epoch=4, test_freq=100):
+        scores_episode = []
+        score_test_list = []
+        policy_loss_list = []
+        value_loss_list = []
+        for iter in range(num_iter):
+            ro = self._rollout(num_episodes)
+            scores = ro.scores
+            scores_episode += scores
+            x, acts, logp_old = self._update_inputs(ro)
+            for epoch in range(n_epoch):
+                ploss_agents, value_loss = self._epoch(ro, x, acts, logp_old)
+                policy_loss_list.append(ploss_agents)
+                value_loss_list.append(value_loss)
+                if iter % test_freq == 0:
+                    score_test, jains, channel_loss, avg_rewards = self.test(50)
+                    score_test_list.append(score_test)
+                    print(f"Iteration: {iter}, Epoch: {epoch}, score rollout: {np.mean(scores)} "
+                          f"Score test: {(score_test, jains, channel_loss, avg_rewards)}")
+                    if np.max(score_test_list) == score_test:
+                        if self.save_path is not None:
+                            self.save(self.save_path)
+                    if (score_test == 1) & (self.early_stopping):
+                        return scores_episode, score_test_list, policy_loss_list, value_loss_list
+        return scores_episode, score_test_list, policy_loss_list, value_loss_list

@@ -1,0 +1,163 @@
+"""GPU parity of the batched learners against the reference (pytest -m gpu).
+
+For each golden learner fixture (tools/gen_fixtures.py gen_learner: iPPO and
+D2D-PPO x {MLP, GRU} x {Bernoulli/combinatorial, Categorical/channel
+selection}) the reference was run on CPU with fixed seeds:
+  1. create_rollouts(2) on its env, recording the actions it sampled and the
+     env's random draws;
+  2. one train() iteration (2 epochs) on exactly that rollout.
+Here the same initial weights are loaded into our learner; the rollout is
+re-run on the GPU with the recorded actions/draws (teacher forcing + env
+replay) and must reproduce the reference's obs/states (exact), log-probs,
+values, advantages and returns (1e-5); the training iteration must reproduce
+the reference's per-epoch losses and the final weights of every agent and
+critic.  Tolerances: 1e-5 absolute for rollout quantities and losses
+(BASELINE.json north_star); final weights 1e-4 absolute (two Adam steps at
+lr 3e-3..1e-2 amplify last-bit gradient differences in near-zero
+components: |dw| <= 2*lr*|g_err|/sqrt(v)).
+"""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def names():
+    return sorted(os.path.basename(p)[8:-4] for p in glob.glob(os.path.join(GOLDEN, "learner_*.npz")))
+
+
+def _params(z):
+    raw = json.loads(str(z["params_json"]))
+    return {k: (np.array(v["__nd__"], dtype=v["dtype"]) if isinstance(v, dict) else v) for k, v in raw.items()}
+
+
+def _sd(z, prefix):
+    out = {}
+    for k in z.files:
+        if k.startswith(prefix + "/"):
+            out[k[len(prefix) + 1:]] = torch.from_numpy(z[k].copy())
+    return out
+
+
+def build(z):
+    from algorithms.d2d_ppo import D2DPPO
+    from algorithms.ippo import iPPO
+    from envs.channel_selection_env import ChannelSelectionEnv
+    from envs.combinatorial_env import CombinatorialEnv
+    kind = str(z["kind"])
+    params = _params(z)
+    env = (CombinatorialEnv if kind == "comb" else ChannelSelectionEnv)(**params, n_envs=1, device="cuda", seed=0)
+    common = dict(hidden_size=int(z["hidden"]), gamma=float(z["gamma"]), policy_lr=3e-3, value_lr=1e-2,
+                  device="cuda", useRNN=bool(z["useRNN"]), combinatorial=bool(z["combinatorial"]),
+                  history_len=int(z["history_len"]), early_stopping=False)
+    return env, kind, common, iPPO, D2DPPO
+
+
+@pytest.mark.parametrize("name", names())
+def test_learner_matches_reference(name):
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm GPU")
+    z = np.load(os.path.join(GOLDEN, f"learner_{name}.npz"))
+    algo = name.split("_")[0]
+    env, kind, common, iPPO, D2DPPO = build(z)
+    lr = iPPO(env, **common) if algo == "ippo" else D2DPPO(env, beta_entropy=0.02, **common)
+    N = env.n_agents
+    for i, ag in enumerate(lr.agents):
+        ag.policy_network.load_state_dict(_sd(z, f"init/agent{i}/policy"))
+        if algo == "ippo":
+            ag.value_network.load_state_dict(_sd(z, f"init/agent{i}/value"))
+    if algo == "d2d":
+        lr.value_network.load_state_dict(_sd(z, "init/critic"))
+    teacher = dict(actions=z["ro/actions"], reset_arrivals=z["draws/reset_arrivals"], flips=z["draws/flips"],
+                   arrivals=z["draws/arrivals"])
+    ro = lr._rollout(2, teacher=teacher)
+    s = env.spec
+    T = ro.T
+    obs = ro.obs[:, 0].cpu().numpy()                                            # [T][N][F]
+    for k in range(N):
+        assert np.array_equal(obs[:, k, : s.obs_len[k]], z[f"ro/obs{k}"]), k
+    logp = lr._seq(ro.logp).t().cpu().numpy()
+    np.testing.assert_allclose(logp, z["ro/log_probs"], rtol=0, atol=1e-5)
+    np.testing.assert_allclose(np.array(ro.scores), z["ro/scores"], rtol=0, atol=1e-12)
+    if algo == "ippo":
+        np.testing.assert_allclose(lr._seq(ro.values).t().cpu().numpy(), z["ro/values"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(ro.adv.t().cpu().numpy(), z["ro/advantages"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(ro.ret.t().cpu().numpy(), z["ro/returns"], rtol=0, atol=1e-5)
+    else:
+        assert np.array_equal(ro.state_seq.cpu().numpy(), z["ro/states"])
+        assert np.array_equal(ro.rewards[:, 0].double().cpu().numpy(), z["ro/rewards_mean"])
+        np.testing.assert_allclose(ro.ret_mean.cpu().numpy(), z["ro/returns"], rtol=0, atol=1e-5)
+    if bool(z["useRNN"]):
+        win = lr.preprocess_input_for_rnn(torch.from_numpy(z["ro/obs0"]).cuda()).cpu().numpy()
+        assert np.array_equal(win, z["rnnwin/agent0"])
+
+    # --- one training iteration on the same rollout
+    lr._rollout = lambda num_episodes, teacher=None, _ro=ro: _ro
+    lr.test = lambda num_episodes: (0.5, 1.0, 0, 0.0)
+    np.random.seed(21)
+    if algo == "ippo":
+        res = lr.train(1, n_epoch=2, num_episodes=2, test_freq=10 ** 9)
+        np.testing.assert_allclose(res[2], z["train/policy_loss"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose(res[3], z["train/value_loss"], rtol=0, atol=1e-5)
+    else:
+        res = lr.train(1, num_episodes=2, n_epoch=2, test_freq=10 ** 9)
+        np.testing.assert_allclose(np.array(res[2]), z["train/policy_loss"], rtol=0, atol=1e-5)
+        np.testing.assert_allclose([float(v) for v in res[3]], z["train/value_loss"], rtol=0, atol=1e-5)
+    for i, ag in enumerate(lr.agents):
+        for k, v in ag.policy_network.state_dict().items():
+            np.testing.assert_allclose(v.cpu().numpy(), z[f"final/agent{i}/policy/{k}"], rtol=0, atol=1e-4,
+                                       err_msg=f"agent {i} policy {k}")
+        if algo == "ippo":
+            for k, v in ag.value_network.state_dict().items():
+                np.testing.assert_allclose(v.cpu().numpy(), z[f"final/agent{i}/value/{k}"], rtol=0, atol=1e-4,
+                                           err_msg=f"agent {i} value {k}")
+    if algo == "d2d":
+        for k, v in lr.value_network.state_dict().items():
+            np.testing.assert_allclose(v.cpu().numpy(), z[f"final/critic/{k}"], rtol=0, atol=1e-4, err_msg=k)
+
+
+def test_save_load_roundtrip(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm GPU")
+    z = np.load(os.path.join(GOLDEN, "learner_d2d_rnn_comb.npz"))
+    env, kind, common, iPPO, D2DPPO = build(z)
+    lr = D2DPPO(env, **common)
+    lr.save(str(tmp_path))
+    before = [{k: v.clone() for k, v in a.policy_network.state_dict().items()} for a in lr.agents]
+    sd0 = torch.load(tmp_path / "agent_0.pth", weights_only=True)
+    assert set(sd0) == {"lstm.weight_ih_l0", "lstm.weight_hh_l0", "lstm.bias_ih_l0", "lstm.bias_hh_l0",
+                        "layers.0.weight", "layers.0.bias", "layers.2.weight", "layers.2.bias"}
+    assert sd0["lstm.weight_ih_l0"].shape[1] == env.observation_space[0].shape[0]
+    with torch.no_grad():
+        for p in lr.policy.parameters():
+            p.add_(1.0)
+    lr.load(str(tmp_path))
+    for a, b in zip(lr.agents, before):
+        for k, v in a.policy_network.state_dict().items():
+            assert torch.equal(v, b[k])
+
+
+def test_batched_train_and_test_run_at_scale():
+    """A real (non-teacher) iPPO iteration + test() on 256 parallel envs of the 64x8 env."""
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm GPU")
+    from algorithms.ippo import iPPO
+    from envs.combinatorial_env import CombinatorialEnv
+    N = 16
+    env = CombinatorialEnv(N, 8, np.array([7, 14] * (N // 2)), np.full(N, 0.3), episode_length=30,
+                           channel_switch=np.full((N, 8), 0.3), homogeneous_size=True, n_envs=256, device="cuda",
+                           seed=5)
+    lr = iPPO(env, hidden_size=32, gamma=0.6, policy_lr=3e-4, device="cuda", combinatorial=True)
+    res = lr.train(2, n_epoch=2, num_episodes=256, test_freq=1)
+    scores, tests, pl, vl = res
+    assert len(scores) == 512 and len(tests) == 4 and len(pl) == 4
+    assert all(np.isfinite(pl)) and all(np.isfinite(vl))
+    sc, ja, ch, rw = lr.test(300)
+    assert 0 <= sc <= 1 and 0 < ja <= 1 and ch == 0 and rw >= 0

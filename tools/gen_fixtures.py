@@ -264,8 +264,162 @@ def gen_data():
     print("data json written to", dst)
 
 
+
+
+# ----------------------------------------------------------------- learners
+def _sd_np(module):
+    return {k: v.detach().cpu().numpy().copy() for k, v in module.state_dict().items()}
+
+
+def _put(out, prefix, sd):
+    for k, v in sd.items():
+        out[f"{prefix}/{k}"] = v
+
+
+class RecordingEnv:
+    """Forwards to a reference env and records the actions it is given and the
+    random draws it makes (flip masks / arrivals recovered from state diffs)."""
+
+    def __init__(self, env):
+        self.__dict__["_env"] = env
+        self.__dict__["rec"] = {"reset_arrivals": [], "actions": [], "flips": [], "arrivals": []}
+
+    def __getattr__(self, k):
+        return getattr(self._env, k)
+
+    def __setattr__(self, k, v):
+        setattr(self._env, k, v)
+
+    def reset(self):
+        out = self._env.reset()
+        d = np.asarray(self._env.deadlines)
+        self.rec["reset_arrivals"].append([self._env.current_buffers[k, d[k] - 1] for k in range(self._env.n_agents)])
+        return out
+
+    def step(self, actions):
+        if not hasattr(self._env, "homogeneous_size"):
+            # ChannelSelectionEnv: the reference learners pass (N, 1) categorical actions, which the env
+            # broadcasts to (N, N) (SURVEY Q4, a crash/miscount bug); parity is defined on (N,) actions
+            actions = np.asarray(actions).reshape(-1)
+        H0 = np.array(self._env.channel_state, dtype=np.float64).copy()
+        out = self._env.step(actions)
+        H1 = np.array(self._env.channel_state, dtype=np.float64)
+        d = np.asarray(self._env.deadlines)
+        self.rec["actions"].append(np.array(actions, dtype=np.float64))
+        self.rec["flips"].append(np.abs(H1 - H0).astype(np.uint8))
+        self.rec["arrivals"].append([self._env.current_buffers[k, d[k] - 1] for k in range(self._env.n_agents)])
+        return out
+
+
+LEARNER_VARIANTS = {
+    # name: (env kind, useRNN, combinatorial, history_len)
+    "mlp_comb": ("comb", False, True, 4),
+    "rnn_comb": ("comb", True, True, 4),
+    "mlp_cat": ("chsel", False, False, 3),
+    "rnn_cat": ("chsel", True, False, 3),
+}
+
+
+def _learner_env(kind, episode_length=20):
+    if kind == "comb":
+        mod = ref_module("envs.combinatorial_env")
+        setup8 = safe_pickle.load(f"{DATA}/setup_8_channels.p")
+        return mod.CombinatorialEnv(
+            n_agents=6, n_channels=8, deadlines=setup8["deadlines"], lbdas=np.array([0.5] * 6),
+            period=np.array([2] * 6), arrival_probs=setup8["arrival_probs"], offsets=setup8["offsets"],
+            episode_length=episode_length, traffic_model="heterogeneous", homogeneous_size=False,
+            periodic_devices=[0, 1, 2], channel_switch=setup8["channel_switch"]), dict(
+            n_agents=6, n_channels=8, deadlines=setup8["deadlines"], lbdas=np.array([0.5] * 6),
+            period=np.array([2] * 6), arrival_probs=setup8["arrival_probs"], offsets=setup8["offsets"],
+            episode_length=episode_length, traffic_model="heterogeneous", homogeneous_size=False,
+            periodic_devices=[0, 1, 2], channel_switch=setup8["channel_switch"])
+    mod = ref_module("envs.channel_selection_env")
+    p = dict(n_agents=4, n_channels=3, deadlines=np.array([4, 6, 4, 5]), lbdas=np.array([0.6] * 4),
+             episode_length=episode_length, traffic_model="aperiodic", channel_switch=np.array([0.5, 0.3, 0.7, 0.2]))
+    return mod.ChannelSelectionEnv(**p), p
+
+
+def gen_learner():
+    import torch
+    ippo = ref_module("algorithms.ippo")
+    d2d = ref_module("algorithms.d2d_ppo")
+    for vname, (kind, useRNN, comb, hl) in LEARNER_VARIANTS.items():
+        for algo in ("ippo", "d2d"):
+            out = {"kind": kind, "useRNN": useRNN, "combinatorial": comb, "history_len": hl, "hidden": 16,
+                   "gamma": 0.6, "episode_length": 20}
+            env, params = _learner_env(kind)
+            out["params_json"] = json.dumps({k: _jsonable(v) for k, v in params.items()})
+            torch.manual_seed(3)
+            np.random.seed(5)
+            if algo == "ippo":
+                lr = ippo.iPPO(env, hidden_size=16, gamma=0.6, policy_lr=3e-3, value_lr=1e-2, device="cpu",
+                               useRNN=useRNN, combinatorial=comb, history_len=hl, early_stopping=False)
+            else:
+                lr = d2d.D2DPPO(env, hidden_size=16, gamma=0.6, policy_lr=3e-3, value_lr=1e-2, beta_entropy=0.02,
+                                device="cpu", useRNN=useRNN, combinatorial=comb, history_len=hl,
+                                early_stopping=False)
+                _put(out, "init/critic", _sd_np(lr.value_network))
+            for i, ag in enumerate(lr.agents):
+                _put(out, f"init/agent{i}/policy", _sd_np(ag.policy_network))
+                if algo == "ippo":
+                    _put(out, f"init/agent{i}/value", _sd_np(ag.value_network))
+            # --- teacher-forced rollout: record actions + env draws of a real create_rollouts
+            rec_env = RecordingEnv(env)
+            lr.env = rec_env
+            torch.manual_seed(11)
+            ro = lr.create_rollouts(2)
+            lr.env = env
+            for k, v in rec_env.rec.items():
+                out[f"draws/{k}"] = np.array(v)
+            if algo == "ippo":
+                obs_t, acts, logp, rets, vals, advs, scores, dones = ro
+                out["ro/values"] = np.asarray(vals)
+                out["ro/advantages"] = advs.numpy()
+            else:
+                obs_t, states, acts, logp, rew_mean, rets, scores, dones = ro
+                out["ro/states"] = states.numpy()
+                out["ro/rewards_mean"] = np.asarray(rew_mean)
+            for i, o in enumerate(obs_t):
+                out[f"ro/obs{i}"] = o.numpy()
+            out["ro/actions"] = np.asarray(acts, dtype=np.float64)
+            out["ro/log_probs"] = logp.numpy()
+            out["ro/returns"] = rets.numpy()
+            out["ro/scores"] = np.array(scores)
+            out["ro/dones"] = np.array(dones)
+            # --- one training iteration on exactly that rollout (create_rollouts patched; the
+            # iteration-0 evaluation is stubbed: it only reads the env, it does not change weights)
+            lr.create_rollouts = lambda num_episodes=4, _ro=ro: _ro
+            lr.test = lambda num_episodes: (0.5, 1.0, 0, 0.0)
+            np.random.seed(21)  # D2D agent permutation stream (d2d_ppo.py:421-422)
+            if algo == "ippo":
+                res = lr.train(1, n_epoch=2, num_episodes=2, test_freq=10 ** 9)
+                out["train/policy_loss"] = np.array(res[2])
+                out["train/value_loss"] = np.array(res[3])
+            else:
+                res = lr.train(1, num_episodes=2, n_epoch=2, test_freq=10 ** 9)
+                out["train/policy_loss"] = np.array(res[2])          # [epoch][agent in sigma order]
+                out["train/value_loss"] = np.array([float(v) for v in res[3]])
+                np.random.seed(21)
+                perms = []
+                for _ in range(2):
+                    c = np.arange(env.n_agents)
+                    np.random.shuffle(c)
+                    perms.append(c)
+                out["train/perms"] = np.array(perms)
+                _put(out, "final/critic", _sd_np(lr.value_network))
+            for i, ag in enumerate(lr.agents):
+                _put(out, f"final/agent{i}/policy", _sd_np(ag.policy_network))
+                if algo == "ippo":
+                    _put(out, f"final/agent{i}/value", _sd_np(ag.value_network))
+            # preprocess_input_for_rnn on agent 0's obs (ippo.py:390-403)
+            if useRNN:
+                out["rnnwin/agent0"] = lr.preprocess_input_for_rnn(obs_t[0]).numpy()
+            np.savez_compressed(os.path.join(OUT, f"learner_{algo}_{vname}.npz"), **out)
+            print(f"learner_{algo}_{vname}: T={len(dones)} scores={np.round(scores, 3)}")
+
+
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    which = sys.argv[1:] or ["data", "env", "gae"]
+    which = sys.argv[1:] or ["data", "env", "gae", "learner"]
     for w in which:
-        {"data": gen_data, "env": gen_env, "gae": gen_gae}[w]()
+        {"data": gen_data, "env": gen_env, "gae": gen_gae, "learner": gen_learner}[w]()
