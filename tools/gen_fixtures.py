@@ -388,6 +388,14 @@ def gen_learner():
             out["ro/dones"] = np.array(dones)
             # --- one training iteration on exactly that rollout (create_rollouts patched; the
             # iteration-0 evaluation is stubbed: it only reads the env, it does not change weights)
+            if not comb:
+                # Categorical actions come back as (T, N, 1) (ippo.py:318); actions[:, i] is then (T, 1)
+                # and Categorical.log_prob broadcasts it against (T,) to (T, T) inside train_step
+                # (SURVEY Q4).  Parity is defined on the flattened (T,) actions, so train on those.
+                ro = list(ro)
+                ai = 1 if algo == "ippo" else 2
+                ro[ai] = np.asarray(ro[ai]).reshape(len(dones), env.n_agents)
+                ro = tuple(ro)
             lr.create_rollouts = lambda num_episodes=4, _ro=ro: _ro
             lr.test = lambda num_episodes: (0.5, 1.0, 0, 0.0)
             np.random.seed(21)  # D2D agent permutation stream (d2d_ppo.py:421-422)
