@@ -11,6 +11,15 @@ collective).  One step = one slot for every env: synthetic actions (Philox
 Bernoulli(0.1) per agent-channel) + the env-step kernel, fp32 obs emitted to
 HBM; every episode_length slots the envs reset (inside the timed loop).
 Inputs are HBM-resident before timing starts.
+
+Two more legs are reported in the same JSON line (they do not change `value`):
+  rollout : the iPPO behaviour-policy slot at the same 65,536 envs — agent-stacked
+            actor + critic forward (H=64), Bernoulli sampling, log-probs, action
+            packing and the env kernel (ippo.py:293-330 batched);
+  ppo     : PPO updates/s — one update = one epoch of the iPPO clipped-surrogate
+            + value update for all 64 actors and 64 critics (ippo.py:194-217,
+            418-426) over a full-episode rollout of --ppo-envs envs per GPU
+            (200 slots), incl. the RCCL gradient all-reduce when N > 1.
 """
 import argparse
 import json
@@ -109,6 +118,71 @@ def load_pmc_traffic():
         return None
 
 
+def rollout_leg(env, args, world):
+    """iPPO behaviour-policy slots at the full env batch (policy in the loop)."""
+    from algorithms.ippo import iPPO
+    torch.manual_seed(0)
+    lr = iPPO(env, hidden_size=64, gamma=0.6, policy_lr=3e-4, value_lr=1e-3, device=env.batch().device,
+              useRNN=False, combinatorial=True)
+    b = env.batch()
+    ring = torch.empty((2,) + tuple(b.obs.shape), dtype=torch.float32, device=b.device)
+    rew = torch.empty((b.E,), dtype=torch.int32, device=b.device)
+    b.reset(want_obs=True, out_obs=ring[0])
+
+    def slot(k):
+        if b.timestep >= env.episode_length:
+            b.reset(want_obs=True, out_obs=ring[k % 2])
+        with torch.no_grad():
+            a, logp, v = lr._act(ring[k % 2].transpose(0, 1), True, True)
+            b.step(lr._env_actions(a), want_obs=True, out_obs=ring[(k + 1) % 2], out_reward=rew)
+
+    for k in range(10):
+        slot(k)
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    K = args.rollout_steps
+    for k in range(K):
+        slot(k)
+    torch.cuda.synchronize()
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world)
+    v = b.E * world * K / el
+    return {"env_steps_per_s": v, "agent_steps_per_s": v * b.spec.N, "ms_per_step": el / K * 1e3, "steps": K,
+            "policy": "iPPO MLP H=64 actor+critic (64 agents, agent-stacked bmm), Bernoulli sampling, fp32"}
+
+
+def ppo_leg(args, rank, world, local):
+    """PPO updates/s of iPPO on a full-episode rollout of --ppo-envs envs per GPU."""
+    from algorithms.ippo import iPPO
+    from envs.combinatorial_env import CombinatorialEnv
+    params = config3_params(args.episode_length)
+    E2 = args.ppo_envs
+    env2 = CombinatorialEnv(**params, n_envs=E2, device=f"cuda:{local}", seed=7)
+    torch.manual_seed(1)
+    lr = iPPO(env2, hidden_size=64, gamma=0.6, policy_lr=3e-4, value_lr=1e-3, device=f"cuda:{local}",
+              useRNN=False, combinatorial=True)
+    ro = lr._rollout(E2)
+    x, acts, logp_old = lr._update_inputs(ro)
+    lr._epoch(x, acts, logp_old, ro.adv, ro.ret)  # warm-up (allocator, hipBLASLt heuristics)
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    P = args.ppo_epochs
+    for _ in range(P):
+        lr._epoch(x, acts, logp_old, ro.adv, ro.ret)
+    torch.cuda.synchronize()
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world)
+    N = params["n_agents"]
+    samples = ro.T * E2 * world
+    flop = 6.0 * N * samples * (30 * 64 + 64 * 8 + 30 * 64 + 64)  # fwd+bwd ~ 3x fwd, 2 flop/mac
+    return {"updates_per_s": P / el, "ms_per_update": el / P * 1e3, "epochs": P,
+            "batch": f"{E2} envs/GPU x {ro.T} slots x {N} agents (actor+critic, one Adam step each)",
+            "agent_samples_per_update": samples * N, "agent_samples_per_s": samples * N * P / el,
+            "gemm_tflops": flop * P / el / 1e12}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -118,6 +192,10 @@ def main():
     ap.add_argument("--episode-length", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--legs", default="env,rollout,ppo")
+    ap.add_argument("--rollout-steps", type=int, default=60)
+    ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
+    ap.add_argument("--ppo-epochs", type=int, default=6)
     args = ap.parse_args()
 
     rank, world, local = setup_dist(args.gpus)
@@ -172,6 +250,13 @@ def main():
     if pmc and pmc.get("kernel_prefix") and pmc.get("envs") == E and pmc.get("agents") == N:
         traffic = pmc.get("bytes_per_launch")
 
+    legs = set(args.legs.split(","))
+    rollout = ppo = None
+    if "rollout" in legs:
+        rollout = rollout_leg(env, args, world)
+    if "ppo" in legs:
+        ppo = ppo_leg(args, rank, world, local)
+
     if rank == 0:
         res = {
             "metric": METRIC,
@@ -198,6 +283,10 @@ def main():
                          "bytes_per_launch": bytes_per_launch,
                          "bytes_per_agent_step": BYTES_PER_AGENT_STEP},
         }
+        if rollout is not None:
+            res["rollout"] = rollout
+        if ppo is not None:
+            res["ppo"] = ppo
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(params, seconds=args.cpu_seconds)
         print(json.dumps(res))

@@ -26,6 +26,7 @@ from d2dhip.envbatch import pack_masks_torch
 from d2dhip.gae import gae_returns
 
 from ._core import make_dist, rnn_windows, unpack_actions
+from .data_parallel import DataParallelMixin, allreduce_mean_scalar
 
 
 class Rollout:
@@ -35,7 +36,7 @@ class Rollout:
         self.__dict__.update(kw)
 
 
-class BatchedLearnerBase:
+class BatchedLearnerBase(DataParallelMixin):
     combinatorial = False
     useRNN = False
 
@@ -97,6 +98,19 @@ class BatchedLearnerBase:
         dist = make_dist(probs, False)
         return a, dist.log_prob(a)
 
+    def _act(self, x, train=True, want_values=False, forced=None):
+        """One slot of the behaviour policy for all agents and envs: probs -> actions,
+        log-probs (ippo.py:154-176 batched) and, for iPPO, the critic values."""
+        probs = self.policy.forward(x)
+        if forced is None:
+            a, logp = self._actions_from_probs(probs, train)
+        else:
+            a = forced
+            dist = make_dist(probs, self.combinatorial)
+            logp = dist.log_prob(a).mean(-1) if self.combinatorial else dist.log_prob(a)
+        v = self.value.forward(x)[..., 0] if want_values else None
+        return a, logp, v
+
     def _env_actions(self, a):
         """agent-major sampled actions -> env action buffer [E][N]"""
         if self.kind == "comb":
@@ -132,16 +146,10 @@ class BatchedLearnerBase:
                 for t in range(L):
                     i = t0 + t
                     x = self._policy_input(obs_buf, t0, i)
-                    probs = self.policy.forward(x)
-                    if tf is None:
-                        a, logp = self._actions_from_probs(probs, train)
-                    else:
-                        a = tf["actions"][i]
-                        dist = make_dist(probs, self.combinatorial)
-                        logp = dist.log_prob(a).mean(-1) if self.combinatorial else dist.log_prob(a)
+                    a, logp, v = self._act(x, train, want_values, None if tf is None else tf["actions"][i])
                     logp_buf[i] = logp
                     if want_values:
-                        val_buf[i] = self.value.forward(x)[..., 0]
+                        val_buf[i] = v
                     act = self._env_actions(a)
                     act_buf[i] = act
                     last = t + 1 == L
@@ -230,10 +238,16 @@ class BatchedLearnerBase:
         ja = np.array(ro.jains[:n], dtype=np.float64)
         rw = np.array(ro.ep_rewards[:n], dtype=np.float64)
         ch = 0  # channel_errors is never incremented by these envs (combinatorial_env.py:97)
-        return np.mean(sc), np.mean(ja), np.sum([ch] * n), np.mean(rw)
+        out = [np.mean(sc), np.mean(ja), np.sum([ch] * n), np.mean(rw)]
+        if getattr(self, "world_size", 1) > 1:  # every rank must take the same save / early-stop branch
+            out = [allreduce_mean_scalar(v, self.device, self.process_group) for v in out]
+            out[2] = 0
+        return tuple(out)
 
     # --------------------------------------------------------- save/load
     def save(self, checkpoint_path):
+        if getattr(self, "rank", 0) != 0:
+            return
         for i, agent in enumerate(self.agents):
             sd = {k: v.detach().clone().cpu() for k, v in agent.policy_network.state_dict().items()}
             torch.save(sd, f"{checkpoint_path}/agent_{i}.pth")
@@ -255,14 +269,4 @@ class BatchedLearnerBase:
                            normalize_ret=normalize_ret, group=self.process_group,
                            last_shard=self._last_shard(), n_envs_total=self._n_envs_total())
 
-    # data-parallel hooks (algorithms/data_parallel.py); single process: identity
-    process_group = None
-
-    def _reduce_grads(self, params):
-        pass
-
-    def _last_shard(self):
-        return True
-
-    def _n_envs_total(self):
-        return None
+    process_group = None  # set by DataParallelMixin._setup_data_parallel when world_size > 1

@@ -138,6 +138,7 @@ class D2DPPO(BatchedLearnerBase):
         self.policy = StackedNets([a.policy_network for a in self.agents], in_dims,
                                   "rnn" if useRNN else "mlp", self.device, act=self._policy_act())
         self.policy_optimizer = torch.optim.Adam(self.policy.parameters(), lr=policy_lr)
+        self._setup_data_parallel(self.policy.parameters() + list(self.value_network.parameters()))
 
     # ------------------------------------------------------------ rollouts
     def _rollout(self, num_episodes, teacher=None):
@@ -174,6 +175,7 @@ class D2DPPO(BatchedLearnerBase):
         # 1) Sample a cycle of agents — the global numpy stream, exactly like the reference
         cycle = np.arange(self.n_agents)
         np.random.shuffle(cycle)
+        cycle = self._sync_perm(cycle)
         # 2) global advantage at the BS
         values = self.value_network(ro.state_seq).squeeze()
         v_te = values.detach().view(ro.E, ro.T).t().unsqueeze(2).contiguous()

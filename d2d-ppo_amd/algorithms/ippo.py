@@ -161,6 +161,7 @@ class iPPO(BatchedLearnerBase):
         self.value = StackedNets([a.value_network for a in self.agents], in_dims, kind, self.device, act=None)
         self.policy_optimizer = torch.optim.Adam(self.policy.parameters(), lr=policy_lr)
         self.value_optimizer = torch.optim.Adam(self.value.parameters(), lr=value_lr)
+        self._setup_data_parallel(self.policy.parameters() + self.value.parameters())
 
     # ------------------------------------------------------------ rollouts
     def _rollout(self, num_episodes, teacher=None):
