@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.h"
@@ -29,6 +30,7 @@ constexpr int kMaxAgents = 1024;
 
 struct EnvArgs {
   int E, N, C, D, F, S, state_stride, seg, reset, cnt_words;
+  uint32_t flags;  // bit 0: non-temporal (streaming) stores for the obs/state flush
   uint32_t rng_step;
   uint64_t env_base, seed;
   const d2d_agent_entry* agents;
@@ -157,28 +159,56 @@ __device__ __forceinline__ uint32_t arrival_value(const EnvArgs& a, const d2d_ag
 // ------------------------------------------------------ LDS -> HBM flushing
 // Copy `count` floats from LDS to a contiguous global range with float4 stores
 // when both ends allow it (every obs/state row group of a block is contiguous).
-__device__ __forceinline__ void flush_contig(float* __restrict__ dst, const float* src, int count) {
+template <typename T>
+__device__ __forceinline__ void st_stream(T* p, const T& v, bool nt) {
+  if (nt)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
+__device__ __forceinline__ void flush_contig(float* __restrict__ dst, const float* src, int count, bool nt) {
   const bool vec = ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) && ((count & 3) == 0);
   if (vec) {
     float4* d4 = reinterpret_cast<float4*>(dst);
     const float4* s4 = reinterpret_cast<const float4*>(src);
-    for (int i = threadIdx.x; i < (count >> 2); i += blockDim.x) d4[i] = s4[i];
+    for (int i = threadIdx.x; i < (count >> 2); i += blockDim.x) {
+      const float4 v = s4[i];
+      if (nt) {
+        __builtin_nontemporal_store(v.x, &d4[i].x);
+        __builtin_nontemporal_store(v.y, &d4[i].y);
+        __builtin_nontemporal_store(v.z, &d4[i].z);
+        __builtin_nontemporal_store(v.w, &d4[i].w);
+      } else {
+        d4[i] = v;
+      }
+    }
   } else {
-    for (int i = threadIdx.x; i < count; i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < count; i += blockDim.x) st_stream(dst + i, src[i], nt);
   }
 }
 
-__device__ __forceinline__ void flush_rows(float* __restrict__ dst, int stride, const float* src, int rows, int S) {
+__device__ __forceinline__ void flush_rows(float* __restrict__ dst, int stride, const float* src, int rows, int S,
+                                           bool nt) {
   if ((S & 3) == 0 && (stride & 3) == 0 && ((reinterpret_cast<uintptr_t>(dst) & 15) == 0)) {
     const int q = S >> 2;
     for (int i = threadIdx.x; i < rows * q; i += blockDim.x) {
       const int r = i / q, j = i - r * q;
-      reinterpret_cast<float4*>(dst + (size_t)r * stride)[j] = reinterpret_cast<const float4*>(src + r * S)[j];
+      float4* d4 = reinterpret_cast<float4*>(dst + (size_t)r * stride) + j;
+      const float4 v = reinterpret_cast<const float4*>(src + r * S)[j];
+      if (nt) {
+        __builtin_nontemporal_store(v.x, &d4->x);
+        __builtin_nontemporal_store(v.y, &d4->y);
+        __builtin_nontemporal_store(v.z, &d4->z);
+        __builtin_nontemporal_store(v.w, &d4->w);
+      } else {
+        *d4 = v;
+      }
     }
   } else {
     for (int i = threadIdx.x; i < rows * S; i += blockDim.x) {
       const int r = i / S, j = i - r * S;
-      dst[(size_t)r * stride + j] = src[r * S + j];
+      st_stream(dst + (size_t)r * stride + j, src[r * S + j], nt);
     }
   }
 }
@@ -223,39 +253,77 @@ __device__ __forceinline__ int env_count(bool v, const Lane& L, int* lds_acc) {
   return tot;
 }
 
+// Wave-local LDS hand-off: every lane's LDS writes are complete (lgkmcnt(0)) before
+// any lane of the same wave reads them; no workgroup barrier needed.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Copy `count` floats of this wave's LDS slot to a contiguous global range.
+__device__ __forceinline__ void wave_flush(float* __restrict__ dst, const float* src, int count, bool nt) {
+  const int lane = threadIdx.x & (kWave - 1);
+  if (((reinterpret_cast<uintptr_t>(dst) & 15) == 0) && ((reinterpret_cast<uintptr_t>(src) & 15) == 0) &&
+      ((count & 3) == 0)) {
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    for (int i = lane; i < (count >> 2); i += kWave) {
+      const float4 v = s4[i];
+      if (nt) {
+        __builtin_nontemporal_store(v.x, &d4[i].x);
+        __builtin_nontemporal_store(v.y, &d4[i].y);
+        __builtin_nontemporal_store(v.z, &d4[i].z);
+        __builtin_nontemporal_store(v.w, &d4[i].w);
+      } else {
+        d4[i] = v;
+      }
+    }
+  } else {
+    for (int i = lane; i < count; i += kWave) st_stream(dst + i, src[i], nt);
+  }
+}
+
 // =====================================================================
 // Combinatorial env: action = binary N x C matrix, per-(agent, channel)
 // Markov channel, ACK vector in {-1, 0, 1}.
+//   CT    : compile-time channel count (0 = runtime a.C)
+//   RESET : reset instead of step (combinatorial_env.py:61-114)
+// LDS: [cnt_words][per-wave obs slots: 64*F floats each][state]
+//   N <= 64 : state staged per wave (the wave's envs), flushed by the wave;
+//   N  > 64 : state of the block's single env staged per block.
 // =====================================================================
-template <typename MaskT, int DW, bool LARGE>
+template <typename MaskT, int DW, bool LARGE, int CT, bool RESET>
 __global__ __launch_bounds__(kMaxAgents) void comb_kernel(EnvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Lane L = lane_geometry<LARGE>(a);
-  // LDS carve: [64 int counters][obs rows][state rows]
+  const int N = a.N, F = a.F;
+  const int C = CT ? CT : a.C;
+  const int wave = threadIdx.x >> 6;
+  const int nwaves = blockDim.x >> 6;
   int* cnt = reinterpret_cast<int*>(lds);  // LARGE: n[32], g[32]; reward at [64]
-  float* lds_obs = lds + a.cnt_words;
-  float* lds_state = lds_obs + ((L.envs_per_block * a.N * a.F + 3) & ~3);
-  const int N = a.N, C = a.C, F = a.F;
+  const int slot = (kWave * F + 3) & ~3;
+  float* lds_obs = lds + a.cnt_words + wave * slot;
+  const int epw = LARGE ? 1 : kWave / a.seg;  // envs per wave
+  float* lds_state = LARGE ? lds + a.cnt_words + nwaves * slot
+                           : lds + a.cnt_words + nwaves * slot + wave * ((epw * a.S + 3) & ~3);
   const size_t row = (size_t)L.env * N + L.k;
   const uint64_t genv = a.env_base + (uint64_t)L.env;
   const uint32_t cmask = (C >= 32) ? 0xFFFFFFFFu : ((1u << C) - 1u);
-  const MaskT* chan_in = reinterpret_cast<const MaskT*>(a.chan);
 
   Row<DW> b;
 #pragma unroll
   for (int i = 0; i < DW; ++i) b.w[i] = 0;
-  uint32_t h_pre = 0, act = 0, rc = 0, dc = 0;
+  uint32_t h_pre = cmask, act = 0, rc = 0, dc = 0;
   d2d_agent_entry ag{};
   if (L.active) {
     ag = a.agents[L.k];
-    if (!a.reset) {
+    if (!RESET) {
       load_row<DW>(b, a.buf + row * DW);
-      h_pre = (uint32_t)chan_in[row] & cmask;
+      h_pre = (uint32_t)reinterpret_cast<const MaskT*>(a.chan)[row] & cmask;
       act = (uint32_t)reinterpret_cast<const MaskT*>(a.actions)[row] & cmask;
       rc = a.recv[row];
       dc = a.disc[row];
-    } else {
-      h_pre = cmask;
     }
   }
   if (LARGE) {
@@ -263,15 +331,16 @@ __global__ __launch_bounds__(kMaxAgents) void comb_kernel(EnvArgs a) {
     __syncthreads();
   }
 
-  uint32_t ack_one = 0, ack_zero = 0, h_new = h_pre;
+  uint32_t ack_one = cmask, ack_zero = 0, h_new = h_pre;
   bool succ = false;
   int nsucc = 0;
-  if (!a.reset) {
+  if (!RESET) {
+    ack_one = 0;
     // attempts = actions * has_a_packet; attempts_good_channels = attempts * channel_state (135-138)
     const uint32_t att = row_any<DW>(b) ? act : 0u;
     const uint32_t good = att & h_pre;
-    // n_users_per_channel, good-attempt count, acknack (148, 155-157): ballots per channel
-    for (int c = 0; c < C; ++c) {
+    // n_users_per_channel, good-attempt count, acknack (148, 155-157): two ballots per channel
+    auto count_channel = [&](int c) {
       const uint64_t m = __ballot((att >> c) & 1u) & L.segmask;
       const uint64_t g = __ballot((good >> c) & 1u) & L.segmask;
       if (!LARGE) {
@@ -282,6 +351,12 @@ __global__ __launch_bounds__(kMaxAgents) void comb_kernel(EnvArgs a) {
         atomicAdd(&cnt[c], __popcll(m));
         atomicAdd(&cnt[32 + c], __popcll(g));
       }
+    };
+    if constexpr (CT != 0) {
+#pragma unroll
+      for (int c = 0; c < CT; ++c) count_channel(c);
+    } else {
+      for (int c = 0; c < C; ++c) count_channel(c);
     }
     if (LARGE) {
       __syncthreads();
@@ -302,80 +377,107 @@ __global__ __launch_bounds__(kMaxAgents) void comb_kernel(EnvArgs a) {
       if (a.flips) {
         f = (uint32_t)reinterpret_cast<const MaskT*>(a.flips)[row];
       } else {
-        for (int blk = 0; blk * 4 < C; ++blk) {
+        const uint64_t* thr = a.flip_thr + (size_t)L.k * C;
+        auto flip_block = [&](int blk) {
           const u32x4 r = philox((uint32_t)genv, (uint32_t)L.k, a.rng_step, (kStreamFlip << 24) | (uint32_t)blk, a.seed);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int c = blk * 4 + i;
-            if (c < C) f |= (uint32_t)((uint64_t)pick(r, i) < a.flip_thr[(size_t)L.k * C + c]) << c;
+            if (c < C) f |= (uint32_t)((uint64_t)pick(r, i) < thr[c]) << c;
           }
+        };
+        if constexpr (CT != 0) {
+#pragma unroll
+          for (int blk = 0; blk < (CT + 3) / 4; ++blk) flip_block(blk);
+        } else {
+          for (int blk = 0; blk * 4 < C; ++blk) flip_block(blk);
         }
       }
     }
     h_new = (h_pre ^ f) & cmask;
   }
-  // arrivals (reset 66-85, step 178-196)
-  if (L.active && draws_now(a, L.k)) {
+  // arrivals (reset 66-85, step 178-196); N <= 64 keeps the draw mask in one word
+  const bool drew = L.active && (LARGE ? draws_now(a, L.k) : ((a.draw[0] >> L.k) & 1ull));
+  if (drew) {
     const uint32_t x = arrival_value(a, ag, row, L.k, genv);
     row_set<DW>(b, (int)ag.deadline - 1, x);
-    rc = (a.reset ? 0u : rc) + x;
+    rc = (RESET ? 0u : rc) + x;
+  } else if (RESET) {
+    rc = 0;
   }
-  if (a.reset) {
-    rc = L.active && draws_now(a, L.k) ? rc : 0u;
-    dc = 0;
-    ack_one = cmask;  // reset obs/state carry ones(C) in the feedback slot (108-112)
-  }
+  if (RESET) dc = 0;
   // ---- state update
   if (L.active) {
     store_row<DW>(b, a.buf + row * DW);
     reinterpret_cast<MaskT*>(a.chan)[row] = (MaskT)h_new;
     a.recv[row] = rc;
     a.disc[row] = dc;
-    if (a.success) a.success[row] = succ ? 1 : 0;
-    if (L.k == 0 && !a.reset) {
-      if (a.reward) a.reward[L.env] = nsucc;  // rewards = len(successful_users) (211)
-      if (a.ack) {
-        int8_t* ak = reinterpret_cast<int8_t*>(a.ack) + (size_t)L.env * C;
-        for (int c = 0; c < C; ++c) ak[c] = ((ack_one >> c) & 1) ? 1 : (((ack_zero >> c) & 1) ? 0 : -1);
+    if (!RESET) {
+      if (a.success) a.success[row] = succ ? 1 : 0;
+      if (L.k == 0) {
+        if (a.reward) a.reward[L.env] = nsucc;  // rewards = len(successful_users) (211)
+        if (a.ack) {
+          int8_t* ak = reinterpret_cast<int8_t*>(a.ack) + (size_t)L.env * C;
+          for (int c = 0; c < C; ++c) ak[c] = ((ack_one >> c) & 1) ? 1 : (((ack_zero >> c) & 1) ? 0 : -1);
+        }
       }
     }
   }
-  // ---- emission: obs_k = [B'[k,:w_k], channel_obs[k] (pre-evolve), acknack] (199-206)
-  const int env0 = LARGE ? blockIdx.x : blockIdx.x * L.envs_per_block;
-  const int nenv = min(L.envs_per_block, a.E - env0);
+  // reset obs/state carry ones(C) in the channel and feedback slots (108-112)
+  // ---- obs_k = [B'[k,:w_k], channel_obs[k] (pre-evolve), acknack] (199-206)
+  const int wave_env0 = LARGE ? blockIdx.x : (blockIdx.x * L.envs_per_block + wave * epw);
+  const int wave_nenv = LARGE ? 1 : max(0, min(epw, a.E - wave_env0));
   if (a.obs) {
     if (L.active) {
-      float* o = lds_obs + (L.local_env * N + L.k) * F;
+      const int lrow = LARGE ? (L.k - wave * kWave) : ((L.local_env - wave * epw) * N + L.k);
+      float* o = lds_obs + lrow * F;
       const int w = ag.obs_width;
 #pragma unroll
       for (int j = 0; j < DW * 4; ++j)
         if (j < w) o[j] = row_byte<DW>(b, j);
-      for (int c = 0; c < C; ++c) {
+      auto obs_channel = [&](int c) {
         o[w + c] = (float)((h_pre >> c) & 1u);
         o[w + C + c] = ((ack_one >> c) & 1u) ? 1.f : (((ack_zero >> c) & 1u) ? 0.f : -1.f);
+      };
+      if constexpr (CT != 0) {
+#pragma unroll
+        for (int c = 0; c < CT; ++c) obs_channel(c);
+      } else {
+        for (int c = 0; c < C; ++c) obs_channel(c);
       }
       for (int j = w + 2 * C; j < F; ++j) o[j] = 0.f;
+    }
+    wave_lds_sync();
+    if (LARGE) {
+      const int k0 = wave * kWave;
+      const int nrows = max(0, min(kWave, N - k0));
+      if (nrows > 0) wave_flush(a.obs + ((size_t)blockIdx.x * N + k0) * F, lds_obs, nrows * F, a.flags & 1u);
+    } else if (wave_nenv > 0) {
+      wave_flush(a.obs + (size_t)wave_env0 * N * F, lds_obs, wave_nenv * N * F, a.flags & 1u);
     }
   }
   // state = [concat_k B'[k,:d_k], channel_state (post-evolve).flatten(), acknack] (207-209)
   if (a.state) {
     if (L.active) {
-      float* s = lds_state + L.local_env * a.S;
+      float* st = lds_state + (LARGE ? 0 : (L.local_env - wave * epw) * a.S);
       const int off = ag.state_offset, d = ag.deadline;
 #pragma unroll
       for (int j = 0; j < DW * 4; ++j)
-        if (j < d) s[off + j] = row_byte<DW>(b, j);
+        if (j < d) st[off + j] = row_byte<DW>(b, j);
       const int sb = a.S - C * (N + 1);
-      for (int c = 0; c < C; ++c) s[sb + L.k * C + c] = (float)((h_new >> c) & 1u);
+      for (int c = 0; c < C; ++c) st[sb + L.k * C + c] = (float)((h_new >> c) & 1u);
       if (L.k == 0)
         for (int c = 0; c < C; ++c)
-          s[sb + N * C + c] = ((ack_one >> c) & 1u) ? 1.f : (((ack_zero >> c) & 1u) ? 0.f : -1.f);
+          st[sb + N * C + c] = ((ack_one >> c) & 1u) ? 1.f : (((ack_zero >> c) & 1u) ? 0.f : -1.f);
     }
-  }
-  if (a.obs || a.state) {
-    __syncthreads();
-    if (a.obs && nenv > 0) flush_contig(a.obs + (size_t)env0 * N * F, lds_obs, nenv * N * F);
-    if (a.state && nenv > 0) flush_rows(a.state + (size_t)env0 * a.state_stride, a.state_stride, lds_state, nenv, a.S);
+    if (LARGE) {
+      __syncthreads();
+      flush_rows(a.state + (size_t)blockIdx.x * a.state_stride, a.state_stride, lds_state, 1, a.S, a.flags & 1u);
+    } else {
+      wave_lds_sync();
+      for (int r = 0; r < wave_nenv; ++r)
+        wave_flush(a.state + (size_t)(wave_env0 + r) * a.state_stride, lds_state + r * a.S, a.S, a.flags & 1u);
+    }
   }
 }
 
@@ -522,8 +624,8 @@ __global__ __launch_bounds__(kMaxAgents) void chsel_kernel(EnvArgs a) {
   }
   if (a.obs || a.state) {
     __syncthreads();
-    if (a.obs && nenv > 0) flush_contig(a.obs + (size_t)env0 * N * F, lds_obs, nenv * N * F);
-    if (a.state && nenv > 0) flush_rows(a.state + (size_t)env0 * a.state_stride, a.state_stride, lds_state, nenv, a.S);
+    if (a.obs && nenv > 0) flush_contig(a.obs + (size_t)env0 * N * F, lds_obs, nenv * N * F, a.flags & 1u);
+    if (a.state && nenv > 0) flush_rows(a.state + (size_t)env0 * a.state_stride, a.state_stride, lds_state, nenv, a.S, a.flags & 1u);
   }
 }
 
@@ -565,6 +667,17 @@ using namespace d2d;
 
 namespace {
 
+// streaming (non-temporal) stores for the obs/state flush: d2d_set_option(D2D_OPT_NT_STORES, v),
+// initial value from the environment variable D2D_NT_STORES
+int g_nt_stores = -1;
+uint32_t store_flags() {
+  if (g_nt_stores < 0) {
+    const char* e = getenv("D2D_NT_STORES");
+    g_nt_stores = (e && e[0] == '1') ? 1 : 0;
+  }
+  return (uint32_t)g_nt_stores;
+}
+
 int buffer_words(int D) { return D <= 4 ? 1 : D <= 8 ? 2 : D <= 12 ? 3 : D <= 16 ? 4 : 8; }
 
 int check_desc(const d2d_env_desc* d) {
@@ -604,16 +717,30 @@ int set_lds(K kernel, size_t bytes) {
   return D2D_OK;
 }
 
+// dynamic LDS of one workgroup (must match the carve in the kernels)
+size_t lds_need(const EnvArgs& a, int block, bool comb) {
+  const bool large = a.N > kWave;
+  const bool stage = a.obs || a.state;
+  if (comb) {
+    const int nwaves = block / kWave;
+    const int epw = large ? 1 : kWave / a.seg;
+    const size_t slot = (size_t)((kWave * a.F + 3) & ~3);
+    size_t w = (size_t)a.cnt_words + (stage ? nwaves * slot : 0);
+    if (a.state) w += large ? (size_t)a.S : (size_t)nwaves * ((epw * a.S + 3) & ~3);
+    return sizeof(float) * w;
+  }
+  const int epb = large ? 1 : block / a.seg;
+  return sizeof(float) * ((size_t)a.cnt_words + (size_t)(stage ? ((epb * a.N * a.F + 3) & ~3) : 0) +
+                          (a.state ? (size_t)epb * a.S : 0));
+}
+
 template <typename K>
-int launch(K kernel, const EnvArgs& a, int block, hipStream_t s) {
+int launch(K kernel, const EnvArgs& a, int block, hipStream_t s, bool comb) {
   const bool large = a.N > kWave;
   const int epb = large ? 1 : block / a.seg;
   const int grid = (a.E + epb - 1) / epb;
   if (grid == 0) return D2D_OK;
-  const int obs_words = a.obs ? ((epb * a.N * a.F + 3) & ~3) : 0;
-  const size_t lds = sizeof(float) * ((size_t)a.cnt_words + (size_t)(a.obs || a.state ? ((epb * a.N * a.F + 3) & ~3) : 0) +
-                                      (a.state ? (size_t)epb * a.S : 0));
-  (void)obs_words;
+  const size_t lds = lds_need(a, block, comb);
   int rc = set_lds(kernel, lds);
   if (rc) return rc;
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), lds, s, a);
@@ -621,21 +748,36 @@ int launch(K kernel, const EnvArgs& a, int block, hipStream_t s) {
   return D2D_OK;
 }
 
-template <typename MaskT, int DW>
+template <typename MaskT, int DW, int CT, bool RESET>
+int dispatch_comb_ct(const EnvArgs& a, int block, hipStream_t s) {
+  if (a.N > kWave) return launch(comb_kernel<MaskT, DW, true, CT, RESET>, a, block, s, true);
+  return launch(comb_kernel<MaskT, DW, false, CT, RESET>, a, block, s, true);
+}
+
+template <int DW>
 int dispatch_comb(const EnvArgs& a, int block, hipStream_t s) {
-  if (a.N > kWave) return launch(comb_kernel<MaskT, DW, true>, a, block, s);
-  return launch(comb_kernel<MaskT, DW, false>, a, block, s);
+  const int C = a.C;
+  if (a.reset) {
+    if (C <= 8) return dispatch_comb_ct<uint8_t, DW, 0, true>(a, block, s);
+    if (C <= 16) return dispatch_comb_ct<uint16_t, DW, 0, true>(a, block, s);
+    return dispatch_comb_ct<uint32_t, DW, 0, true>(a, block, s);
+  }
+  if (C == 8) return dispatch_comb_ct<uint8_t, DW, 8, false>(a, block, s);
+  if (C == 4) return dispatch_comb_ct<uint8_t, DW, 4, false>(a, block, s);
+  if (C == 16) return dispatch_comb_ct<uint16_t, DW, 16, false>(a, block, s);
+  if (C <= 8) return dispatch_comb_ct<uint8_t, DW, 0, false>(a, block, s);
+  if (C <= 16) return dispatch_comb_ct<uint16_t, DW, 0, false>(a, block, s);
+  return dispatch_comb_ct<uint32_t, DW, 0, false>(a, block, s);
 }
 
 template <int DW>
 int dispatch_dw(const EnvArgs& a, int block, bool comb, int C, hipStream_t s) {
+  (void)C;
   if (!comb) {
-    if (a.N > kWave) return launch(chsel_kernel<DW, true>, a, block, s);
-    return launch(chsel_kernel<DW, false>, a, block, s);
+    if (a.N > kWave) return launch(chsel_kernel<DW, true>, a, block, s, false);
+    return launch(chsel_kernel<DW, false>, a, block, s, false);
   }
-  if (C <= 8) return dispatch_comb<uint8_t, DW>(a, block, s);
-  if (C <= 16) return dispatch_comb<uint16_t, DW>(a, block, s);
-  return dispatch_comb<uint32_t, DW>(a, block, s);
+  return dispatch_comb<DW>(a, block, s);
 }
 
 int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions, const d2d_env_replay* rp,
@@ -658,6 +800,7 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
   if (rp) { a.flips = rp->flips; a.arrivals = rp->arrivals; }
   if (out) { a.obs = out->obs; a.state = out->state; a.reward = out->reward; a.ack = out->ack; a.success = out->success; }
   draw_mask(d, reset ? 0 : t, a.draw);
+  a.flags = store_flags();
   const bool large = a.N > kWave;
   int seg = 1;
   while (seg < a.N) seg <<= 1;
@@ -665,14 +808,12 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
   // block: 256 lanes (4 waves) unless the LDS staging of that many envs would
   // exceed 64 KiB (keep >= 2 workgroups per CU); LARGE: one env per block
   auto cnt_words = [&](int epb) { return comb ? (large ? 80 : 0) : (((epb * 34) + 3) & ~3); };
-  auto lds_bytes = [&](int blk) {
-    const int epb = large ? 1 : blk / a.seg;
-    return sizeof(float) * ((size_t)cnt_words(epb) + (size_t)((epb * a.N * a.F + 3) & ~3) +
-                            (a.state ? (size_t)epb * a.S : 0));
-  };
   int block = large ? a.seg : 256;
-  while (!large && block > kWave && block > a.seg && lds_bytes(block) > 65536) block >>= 1;
   a.cnt_words = cnt_words(large ? 1 : block / a.seg);
+  while (!large && block > kWave && block > a.seg && lds_need(a, block, comb) > 65536) {
+    block >>= 1;
+    a.cnt_words = cnt_words(block / a.seg);
+  }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (buffer_words(a.D)) {
     case 1: return dispatch_dw<1>(a, block, comb, a.C, s);
@@ -684,6 +825,15 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
 }
 
 }  // namespace
+
+extern "C" int d2d_set_option(int32_t option, int32_t value) {
+  if (option == D2D_OPT_NT_STORES) {
+    g_nt_stores = value ? 1 : 0;
+    return D2D_OK;
+  }
+  d2d_set_error("unknown option %d", option);
+  return D2D_EINVAL;
+}
 
 extern "C" int d2d_buffer_words(int32_t max_deadline) { return buffer_words(max_deadline); }
 

@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libd2dhip.so")
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION = 0, 1
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
 ABI_VERSION = 1
+D2D_OPT_NT_STORES = 1
 
 _p = ctypes.c_void_p
 
@@ -58,6 +59,7 @@ _SIGS = {
     "d2d_colstats_finalize": (ctypes.c_int, [ctypes.c_int32, _p, _p, ctypes.c_double, ctypes.c_int32, _p, _p, _p,
                                               _p]),
     "d2d_normalize_columns": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, _p, _p, _p, _p, _p]),
+    "d2d_set_option": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),
     "d2d_last_error": (ctypes.c_char_p, []),
     "d2d_abi_version": (ctypes.c_int, []),
 }

@@ -156,6 +156,11 @@ int d2d_colstats_finalize(int32_t cols, const double* sum, const double* m2, dou
 int d2d_normalize_columns(int64_t rows, int32_t cols, float* x, const double* mean, const double* scale,
                           const int32_t* gate, void* stream);
 
+/* Process-wide tuning options (not part of the reference interface).
+ * D2D_OPT_NT_STORES: 1 = write obs/state with non-temporal (streaming) stores. */
+enum { D2D_OPT_NT_STORES = 1 };
+int d2d_set_option(int32_t option, int32_t value);
+
 const char* d2d_last_error(void);
 int d2d_abi_version(void);
 
