@@ -127,14 +127,17 @@ def rollout_leg(env, args, world):
     b = env.batch()
     ring = torch.empty((2,) + tuple(b.obs.shape), dtype=torch.float32, device=b.device)
     rew = torch.empty((b.E,), dtype=torch.int32, device=b.device)
+    act = b.action_buffer()
+    logp = torch.empty((b.spec.N, b.E), dtype=torch.float32, device=b.device)
+    val = torch.empty_like(logp)
     b.reset(want_obs=True, out_obs=ring[0])
 
     def slot(k):
         if b.timestep >= env.episode_length:
             b.reset(want_obs=True, out_obs=ring[k % 2])
         with torch.no_grad():
-            a, logp, v = lr._act(ring[k % 2].transpose(0, 1), True, True)
-            b.step(lr._env_actions(a), want_obs=True, out_obs=ring[(k + 1) % 2], out_reward=rew)
+            lr._policy_slot(ring, 0, k % 2, True, act, logp, val, None, b)
+            b.step(act, want_obs=True, out_obs=ring[(k + 1) % 2], out_reward=rew)
 
     for k in range(10):
         slot(k)
@@ -148,8 +151,9 @@ def rollout_leg(env, args, world):
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world)
     v = b.E * world * K / el
+    path = "fused HIP policy kernel (fp32 MFMA)" if lr._fused_ok() else "torch agent-stacked bmm"
     return {"env_steps_per_s": v, "agent_steps_per_s": v * b.spec.N, "ms_per_step": el / K * 1e3, "steps": K,
-            "policy": "iPPO MLP H=64 actor+critic (64 agents, agent-stacked bmm), Bernoulli sampling, fp32"}
+            "policy": f"iPPO MLP H=64 actor+critic, 64 agents, Bernoulli sampling, fp32; {path}"}
 
 
 def ppo_leg(args, rank, world, local):

@@ -18,6 +18,7 @@ reference's sequential rollout of E*W episodes in env-major order
 all use that order.
 """
 import math
+import os
 
 import numpy as np
 import torch
@@ -98,6 +99,60 @@ class BatchedLearnerBase(DataParallelMixin):
         dist = make_dist(probs, False)
         return a, dist.log_prob(a)
 
+    # ------------------------------------------------ behaviour policy slot
+    def _fused_ok(self):
+        """The fused HIP policy kernel covers the MLP policies (H <= 64, A <= 16, F <= 64)."""
+        if getattr(self, "_fused", None) is None:
+            p = self.policy
+            self._fused = (not self.useRNN and p.kind == "mlp" and p.H <= 64 and p.A <= 16 and p.F <= 64
+                           and os.environ.get("D2D_FUSED_POLICY", "1") != "0")
+        return self._fused
+
+    def _policy_seed(self):
+        if getattr(self, "_pseed", None) is None:
+            # drawn from torch's global RNG, so torch.manual_seed makes rollouts reproducible,
+            # as with the reference's torch.distributions sampling
+            self._pseed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        return self._pseed
+
+    def _mlp_desc(self, E, env_base):
+        from d2dhip import _lib
+        p = self.policy.params
+        crit = getattr(self, "value", None)
+        cp = crit.params if (crit is not None and getattr(crit, "kind", None) == "mlp") else None
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        return _lib.MlpDesc(self.policy.N, E, self.policy.F, self.policy.H, self.policy.A,
+                            0 if self.combinatorial else 1, ptr(p["w1"]), ptr(p["b1"]), ptr(p["w2"]), ptr(p["b2"]),
+                            ptr(cp["w1"]) if cp else None, ptr(cp["b1"]) if cp else None,
+                            ptr(cp["w2"]) if cp else None, ptr(cp["b2"]) if cp else None,
+                            self._policy_seed(), int(env_base))
+
+    def _policy_slot(self, obs_buf, t0, i, train, act_out, logp_out, val_out, tf, b):
+        """Actions for slot i of every env (written to act_out [E][N]), log-probs [N][E], values [N][E]."""
+        forced = None if tf is None else tf["actions"][i]
+        if self._fused_ok() and (self.kind == "comb") == bool(self.combinatorial):
+            from d2dhip import _lib
+            lib = _lib.require_gpu()
+            desc = self._mlp_desc(b.E, b.desc.env_base)
+            fz = None
+            if forced is not None:
+                fz = self._env_actions(forced).contiguous()
+            rc = lib.d2d_policy_mlp_step(desc, obs_buf[i].data_ptr(), None if fz is None else fz.data_ptr(),
+                                         b.rng_step, 0 if train else 1, act_out.data_ptr(), logp_out.data_ptr(),
+                                         None if val_out is None else val_out.data_ptr(), _lib.stream_ptr())
+            _lib.check(rc, "d2d_policy_mlp_step")
+            if val_out is not None and desc.v1 is None:
+                raise RuntimeError("critic values requested without an MLP critic")
+            return act_out
+        x = self._policy_input(obs_buf, t0, i)
+        a, logp, v = self._act(x, train, val_out is not None, forced)
+        logp_out.copy_(logp)
+        if val_out is not None:
+            val_out.copy_(v)
+        act = self._env_actions(a)
+        act_out.copy_(act)
+        return act_out
+
     def _act(self, x, train=True, want_values=False, forced=None):
         """One slot of the behaviour policy for all agents and envs: probs -> actions,
         log-probs (ippo.py:154-176 batched) and, for iPPO, the critic values."""
@@ -145,13 +200,8 @@ class BatchedLearnerBase(DataParallelMixin):
                                   replay_arrivals=None if tf is None else tf["reset_arrivals"][w])
                 for t in range(L):
                     i = t0 + t
-                    x = self._policy_input(obs_buf, t0, i)
-                    a, logp, v = self._act(x, train, want_values, None if tf is None else tf["actions"][i])
-                    logp_buf[i] = logp
-                    if want_values:
-                        val_buf[i] = v
-                    act = self._env_actions(a)
-                    act_buf[i] = act
+                    act = self._policy_slot(obs_buf, t0, i, train, act_buf[i], logp_buf[i],
+                                            val_buf[i] if want_values else None, tf, b)
                     last = t + 1 == L
                     env.step_batched(act, want_obs=not last, want_state=want_state and not last,
                                      out_obs=None if last else obs_buf[i + 1],

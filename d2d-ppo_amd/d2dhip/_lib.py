@@ -43,6 +43,13 @@ class EnvReplay(ctypes.Structure):
     _fields_ = [("flips", _p), ("arrivals", _p)]
 
 
+class MlpDesc(ctypes.Structure):
+    _fields_ = [("n_agents", ctypes.c_int32), ("n_envs", ctypes.c_int32), ("obs_dim", ctypes.c_int32),
+                ("hidden", ctypes.c_int32), ("n_out", ctypes.c_int32), ("kind", ctypes.c_int32),
+                ("w1", _p), ("b1", _p), ("w2", _p), ("b2", _p), ("v1", _p), ("c1", _p), ("v2", _p), ("c2", _p),
+                ("seed", ctypes.c_uint64), ("env_base", ctypes.c_uint64)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "d2d_env_reset": (ctypes.c_int, [ctypes.POINTER(EnvDesc), ctypes.POINTER(EnvState), ctypes.POINTER(EnvReplay),
@@ -60,6 +67,8 @@ _SIGS = {
                                               _p]),
     "d2d_normalize_columns": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, _p, _p, _p, _p, _p]),
     "d2d_set_option": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),
+    "d2d_policy_mlp_step": (ctypes.c_int, [ctypes.POINTER(MlpDesc), _p, _p, ctypes.c_uint32, ctypes.c_int32, _p, _p,
+                                            _p, _p]),
     "d2d_last_error": (ctypes.c_char_p, []),
     "d2d_abi_version": (ctypes.c_int, []),
 }

@@ -156,6 +156,27 @@ int d2d_colstats_finalize(int32_t cols, const double* sum, const double* m2, dou
 int d2d_normalize_columns(int64_t rows, int32_t cols, float* x, const double* mean, const double* scale,
                           const int32_t* gate, void* stream);
 
+/* ---- fused behaviour-policy slot (MLP learners) ----
+ * Replaces Policy/Value.forward + PPO.select_action for every agent of every env
+ * (algorithms/ippo.py:54-90, 154-176; d2d_ppo.py:62-98, 159-181).  Weights are the
+ * agent-stacked nn.Linear tensors:  w1 [N][H][F], b1 [N][H], w2 [N][A][H], b2 [N][A];
+ * optional critic v1 [N][H][F], c1 [N][H], v2 [N][1][H], c2 [N][1] (NULL = no critic).
+ * kind 0: softmax -> Bernoulli per output (combinatorial, A = C channels), actions =
+ *         channel masks [E][N] (d2d_mask_bytes(A) bytes), logp = mean_c log_prob;
+ * kind 1: softmax -> Categorical over A = C+1 ids, actions = uint8 [E][N].
+ * obs [E][N][F] (the env kernel's layout); logp, value [N][E].  forced != NULL
+ * evaluates the given actions instead of sampling; deterministic = argmax / p > 0.5.
+ * Sampling uses Philox stream 3 at (env_base + env, agent, rng_step). */
+typedef struct d2d_mlp_desc {
+    int32_t n_agents, n_envs, obs_dim, hidden, n_out, kind;
+    const float *w1, *b1, *w2, *b2;
+    const float *v1, *c1, *v2, *c2;
+    uint64_t seed, env_base;
+} d2d_mlp_desc;
+
+int d2d_policy_mlp_step(const d2d_mlp_desc* desc, const float* obs, const void* forced, uint32_t rng_step,
+                        int32_t deterministic, void* actions, float* logp, float* value, void* stream);
+
 /* Process-wide tuning options (not part of the reference interface).
  * D2D_OPT_NT_STORES: 1 = write obs/state with non-temporal (streaming) stores. */
 enum { D2D_OPT_NT_STORES = 1 };
