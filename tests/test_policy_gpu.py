@@ -1,8 +1,12 @@
 """GPU parity of the fused behaviour-policy kernel (csrc/policy_kernels.hip) against a
 plain torch fp32 reference of the same op (the reference's Policy/Value forward +
-torch.distributions Bernoulli/Categorical, algorithms/ippo.py:54-90,154-176).
-Tolerance: 1e-5 absolute on log-probs and values; actions exact (sampled actions are
-compared with the same Philox uniforms, ties |u - p| < 1e-6 excluded)."""
+torch.distributions Bernoulli/Categorical, algorithms/ippo.py:54-90,154-176), with the
+reference's initialisation (orthogonal, gain 2) and env-like observations.
+Tolerance: values 1e-5 absolute; log-probs 1e-5 absolute wherever every probability of
+the (agent, env) lies in [1e-3, 1-1e-3]; elsewhere log(1-p) for p -> 1 is ill-conditioned
+in fp32 for BOTH implementations (a 1-ulp difference in p is a relative 6e-8/(1-p)
+difference in 1-p), so there 1e-3.  Actions exact (sampled actions are compared with the
+same Philox uniforms, ties |u - p| < 1e-6 excluded)."""
 import numpy as np
 import pytest
 
@@ -11,21 +15,21 @@ torch = pytest.importorskip("torch")
 
 
 def make(kind, N, E, F, H, A, in_dims=None, seed=0, critic=True):
-    g = torch.Generator().manual_seed(seed)
-    def lin(o, i, gain=0.3):
-        return (torch.randn(N, o, i, generator=g) * gain).float()
-    actor = {"w1": lin(H, F), "b1": lin(H, 1)[..., 0] * 0.1, "w2": lin(A, H, 0.5), "b2": lin(A, 1)[..., 0] * 0.1}
-    crit = {"w1": lin(H, F), "b1": lin(H, 1)[..., 0], "w2": lin(1, H), "b2": lin(1, 1)[..., 0]} if critic else None
-    obs = torch.randint(-1, 4, (E, N, F), generator=g).float()
-    if in_dims is not None:
-        for k, d in enumerate(in_dims):
-            actor["w1"][k, :, d:] = 0
-            if crit:
-                crit["w1"][k, :, d:] = 0
-            obs[:, k, d:] = 0
+    from algorithms._core import Policy, StackedNets, Value
+    torch.manual_seed(seed)
+    dims = in_dims or [F] * N
+    pol = StackedNets([Policy(d, A, H) for d in dims], dims, "mlp", "cpu", act="softmax")
+    val = StackedNets([Value(d, H) for d in dims], dims, "mlp", "cpu") if critic else None
+    g = torch.Generator().manual_seed(seed + 1)
+    obs = torch.zeros(E, N, F)
+    D = F // 3
+    obs[:, :, :D] = torch.randint(0, 3, (E, N, D), generator=g).float()            # buffer counts
+    obs[:, :, D:] = torch.randint(-1, 2, (E, N, F - D), generator=g).float()       # channel bits / ACK
+    for k, d in enumerate(dims):
+        obs[:, k, d:] = 0
     dev = "cuda"
-    to = lambda d: None if d is None else {k: v.to(dev).contiguous() for k, v in d.items()}  # noqa: E731
-    return to(actor), to(crit), obs.to(dev)
+    to = lambda st: None if st is None else {k: v.detach().to(dev).contiguous() for k, v in st.params.items()}  # noqa
+    return to(pol), to(val), obs.to(dev)
 
 
 def torch_ref(actor, crit, obs):
@@ -63,7 +67,9 @@ def test_forced_and_deterministic_match_torch(kind, F, H, A, in_dims):
         ref_lp = Categorical(probs=probs, validate_args=False).log_prob(ids)
     acts, lp, val = policy_mlp_step(actor, obs, kind, crit, forced=forced)
     assert torch.equal(acts, forced)
-    torch.testing.assert_close(lp, ref_lp, rtol=0, atol=1e-5)
+    well = ((probs > 1e-3) & (probs < 1 - 1e-3)).all(-1)
+    torch.testing.assert_close(lp[well], ref_lp[well], rtol=0, atol=1e-5)
+    torch.testing.assert_close(lp, ref_lp, rtol=0, atol=1e-3)
     torch.testing.assert_close(val, v, rtol=0, atol=1e-5)
     # deterministic evaluation actions (ippo.py:166 / 171)
     acts_d, lp_d, _ = policy_mlp_step(actor, obs, kind, None, deterministic=True)
