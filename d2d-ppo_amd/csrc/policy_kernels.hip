@@ -44,17 +44,50 @@ constexpr uint32_t kStreamPolicy = 3;
 
 __device__ __forceinline__ float shfl_xor_f(float v, int m) { return __shfl_xor(v, m, 64); }
 
-// torch.distributions.Bernoulli(probs).log_prob(t): logits = log(p) - log1p(-p) on p clamped
-// to [eps, 1-eps]; log_prob = -BCEWithLogits = log_sigmoid(x) - (1 - t) x
-__device__ __forceinline__ float bernoulli_logp(float p, float t) {
+// torch.distributions.Bernoulli(probs).log_prob(t) = -BCEWithLogits(logit(clamp(p)), t) with p
+// clamped to [eps, 1-eps]: mathematically log(pc) for t = 1 and log1p(-pc) for t = 0, which is
+// what is evaluated here (one transcendental instead of four; agrees to ~1e-7 relative).
+__device__ __forceinline__ float bernoulli_logp(float p, bool t) {
   const float eps = 1.1920928955078125e-07f;
   const float pc = fminf(fmaxf(p, eps), 1.f - eps);
-  const float x = logf(pc) - log1pf(-pc);
-  const float ls = fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
-  return ls - (1.f - t) * x;
+  return t ? logf(pc) : log1pf(-pc);
 }
 
-template <int KS, int HT>  // KS = input k-steps of 4 (F <= 4*KS), HT = hidden tiles of 16 (H <= 16*HT)
+// Input index carried by lane group g at MFMA k-step s.  The k order is permuted so that a
+// lane's KS inputs are KS/4 contiguous 4-float chunks of its obs row: [16q + 4g, 16q + 4g + 4).
+__device__ __forceinline__ int kidx(int s, int g) { return 16 * (s >> 2) + 4 * g + (s & 3); }
+
+// B operand of the obs tile: lane (g, i) <- X[env][kidx(s, g)], 0 past F / past E.
+// Branch-free: every load stays inside the row (indices clamped to F-1 / F-2), the
+// out-of-row values are zeroed by a select; even F uses 8-byte loads.
+template <int KS>
+__device__ __forceinline__ void load_obs_tile(float (&xf)[KS], const float* __restrict__ obs, int env, bool env_ok,
+                                              int N, int k, int F, int g) {
+  const float* row = obs + ((size_t)(env_ok ? env : 0) * N + k) * F;
+  if ((F & 1) == 0) {
+#pragma unroll
+    for (int q = 0; q < KS / 4; ++q) {
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int c = 16 * q + 4 * g + 2 * m;
+        const float2 v = *reinterpret_cast<const float2*>(row + min(c, F - 2));
+        xf[4 * q + 2 * m] = (env_ok && c < F) ? v.x : 0.f;
+        xf[4 * q + 2 * m + 1] = (env_ok && c + 1 < F) ? v.y : 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int c = kidx(s, g);
+      const float v = row[min(c, F - 1)];
+      xf[s] = (env_ok && c < F) ? v : 0.f;
+    }
+  }
+}
+
+// KS = input k-steps of 4 (F <= 4*KS), HT = hidden tiles of 16 (H <= 16*HT),
+// KIND 0 Bernoulli / 1 Categorical, CRITIC: iPPO per-agent critic present
+template <int KS, int HT, int KIND, bool CRITIC>
 __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;   // lane group: k-slot of A/B operands, row group of C/D
@@ -62,7 +95,7 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
   const int k = blockIdx.x;  // agent (fast grid axis: all agents of an env chunk run together)
   const int wave = threadIdx.x >> 6;
   const int N = a.N, F = a.F, H = a.H, A = a.A;
-  const bool critic = a.v1 != nullptr;
+  constexpr bool critic = CRITIC;
 
   // ---- register-resident weight fragments of agent k
   float w1f[HT][KS], v1f[HT][KS], w2f[HT][4], v2f[HT][4];
@@ -74,7 +107,7 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
     const int hrow = 16 * t + i;  // A row = hidden unit
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      const int kk = 4 * s + g;
+      const int kk = kidx(s, g);
       const bool ok = hrow < H && kk < F;
       w1f[t][s] = ok ? W1[(size_t)hrow * F + kk] : 0.f;
       v1f[t][s] = (ok && critic) ? V1[(size_t)hrow * F + kk] : 0.f;
@@ -100,19 +133,18 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
 
   const int tiles = a.envs_per_wave / 16;
   const int wave_env0 = (blockIdx.y * (blockDim.x >> 6) + wave) * a.envs_per_wave;
+  float xnext[KS];
+  load_obs_tile<KS>(xnext, a.obs, wave_env0 + i, wave_env0 + i < a.E, N, k, F, g);
   for (int tt = 0; tt < tiles; ++tt) {
     const int e0 = wave_env0 + tt * 16;
     if (e0 >= a.E) break;  // wave-uniform
     const int env = e0 + i;
     const bool env_ok = env < a.E;
-    // ---- obs tile as the B operand: lane (g, i) holds X[env][4s + g]
     float xf[KS];
-    const float* xrow = a.obs + ((size_t)(env_ok ? env : 0) * N + k) * F;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int kk = 4 * s + g;
-      xf[s] = (env_ok && kk < F) ? xrow[kk] : 0.f;
-    }
+    for (int s = 0; s < KS; ++s) xf[s] = xnext[s];
+    // prefetch the next tile's obs while this one computes
+    if (tt + 1 < tiles) load_obs_tile<KS>(xnext, a.obs, env + 16, env + 16 < a.E, N, k, F, g);
     // ---- layer 1 (actor, critic): H^T = W1 . X^T, bias as the initial accumulator
     f32x4 ha[HT], hv[HT];
 #pragma unroll
@@ -162,15 +194,16 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
     sum += shfl_xor_f(sum, 16);
     sum += shfl_xor_f(sum, 32);
     float p[4];
+    const float inv = 1.f / sum;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) p[r] = ex[r] / sum;
+    for (int r = 0; r < 4; ++r) p[r] = ex[r] * inv;
 
     const size_t cell = (size_t)env * N + k;
     const uint32_t genv = (uint32_t)(a.env_base + (uint64_t)(env_ok ? env : 0));
     float lp;
     uint32_t out_bits = 0;
     int out_id = 0;
-    if (a.kind == 0) {
+    if constexpr (KIND == 0) {
       // ---- Bernoulli per channel (combinatorial): u < p, one Philox block per lane group
       uint32_t forced_bits = 0;
       if (a.forced && env_ok) {
@@ -190,7 +223,7 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
           else if (a.deterministic) bit = p[r] > 0.5f;  // dist.probs > 0.5 (ippo.py:166)
           else bit = (float)(pick(rr, r) >> 8) * (1.f / 16777216.f) < p[r];
           out_bits |= (uint32_t)bit << act;
-          lsum += bernoulli_logp(p[r], bit ? 1.f : 0.f);
+          lsum += bernoulli_logp(p[r], bit);
         }
       }
       lsum += shfl_xor_f(lsum, 16);
@@ -257,7 +290,7 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
       out_id = chosen;
     }
     if (env_ok && g == 0) {
-      if (a.kind == 0) {
+      if constexpr (KIND == 0) {
         unsigned char* ob = reinterpret_cast<unsigned char*>(a.act_out) + cell * a.mask_bytes;
         for (int b = 0; b < a.mask_bytes; ++b) ob[b] = (unsigned char)(out_bits >> (8 * b));
       } else {
@@ -278,7 +311,11 @@ static int launch_policy(const MlpArgs& a, hipStream_t s) {
   const int waves = 4;
   const int envs_per_block = waves * a.envs_per_wave;
   dim3 grid(a.N, (a.E + envs_per_block - 1) / envs_per_block);
-  hipLaunchKernelGGL((policy_mlp_kernel<KS, HT>), grid, dim3(64 * waves), 0, s, a);
+  const bool critic = a.v1 != nullptr;
+  if (a.kind == 0 && critic) hipLaunchKernelGGL((policy_mlp_kernel<KS, HT, 0, true>), grid, dim3(64 * waves), 0, s, a);
+  else if (a.kind == 0) hipLaunchKernelGGL((policy_mlp_kernel<KS, HT, 0, false>), grid, dim3(64 * waves), 0, s, a);
+  else if (critic) hipLaunchKernelGGL((policy_mlp_kernel<KS, HT, 1, true>), grid, dim3(64 * waves), 0, s, a);
+  else hipLaunchKernelGGL((policy_mlp_kernel<KS, HT, 1, false>), grid, dim3(64 * waves), 0, s, a);
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
 }
@@ -298,7 +335,7 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const float* obs, cons
   MlpArgs a;
   a.E = d->n_envs; a.N = d->n_agents; a.F = d->obs_dim; a.H = d->hidden; a.A = d->n_out; a.kind = d->kind;
   a.deterministic = deterministic ? 1 : 0;
-  a.envs_per_wave = 64;
+  a.envs_per_wave = 256;
   a.rng_step = rng_step; a.seed = d->seed; a.env_base = d->env_base;
   a.w1 = d->w1; a.b1 = d->b1; a.w2 = d->w2; a.b2 = d->b2; a.v1 = d->v1; a.c1 = d->c1; a.v2 = d->v2; a.c2 = d->c2;
   a.obs = obs; a.forced = forced; a.act_out = actions; a.logp_out = logp; a.value_out = value;
