@@ -826,9 +826,15 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
 
 }  // namespace
 
+extern int g_policy_f32_mfma;  // policy_kernels.hip
+
 extern "C" int d2d_set_option(int32_t option, int32_t value) {
   if (option == D2D_OPT_NT_STORES) {
     g_nt_stores = value ? 1 : 0;
+    return D2D_OK;
+  }
+  if (option == D2D_OPT_POLICY_F32_MFMA) {
+    g_policy_f32_mfma = value ? 1 : 0;
     return D2D_OK;
   }
   d2d_set_error("unknown option %d", option);

@@ -29,6 +29,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 struct MlpArgs {
   int E, N, F, H, A, kind, deterministic, envs_per_wave;
+  float inv_A;
   uint32_t rng_step;
   uint64_t seed, env_base;
   const float *w1, *b1, *w2, *b2, *v1, *c1, *v2, *c2;
@@ -44,13 +45,19 @@ constexpr uint32_t kStreamPolicy = 3;
 
 __device__ __forceinline__ float shfl_xor_f(float v, int m) { return __shfl_xor(v, m, 64); }
 
+// relu as one v_max_i32 on the bit pattern (negative floats are negative ints, -0 -> +0);
+// fmaxf(x, 0) costs a NaN-quieting canonicalize plus the max under the IEEE mode
+__device__ __forceinline__ float relu(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+
 // torch.distributions.Bernoulli(probs).log_prob(t) = -BCEWithLogits(logit(clamp(p)), t) with p
-// clamped to [eps, 1-eps]: mathematically log(pc) for t = 1 and log1p(-pc) for t = 0, which is
-// what is evaluated here (one transcendental instead of four; agrees to ~1e-7 relative).
+// clamped to [eps, 1-eps]: mathematically log(pc) for t = 1 and log(1 - pc) for t = 0.  One
+// hardware log (v_log_f32, ~1 ulp in log2) of the selected argument: 1 - pc is exact for
+// pc >= 1/2 and within 2^-24 relative below, so the absolute error of the result is ~1e-7 (the
+// library logf/log1pf pair costs ~190 instructions per call; parity tolerance is 1e-5 absolute).
 __device__ __forceinline__ float bernoulli_logp(float p, bool t) {
   const float eps = 1.1920928955078125e-07f;
   const float pc = fminf(fmaxf(p, eps), 1.f - eps);
-  return t ? logf(pc) : log1pf(-pc);
+  return __logf(t ? pc : 1.f - pc);
 }
 
 // Input index carried by lane group g at MFMA k-step s.  The k order is permuted so that a
@@ -82,6 +89,144 @@ __device__ __forceinline__ void load_obs_tile(float (&xf)[KS], const float* __re
       const float v = row[min(c, F - 1)];
       xf[s] = (env_ok && c < F) ? v : 0.f;
     }
+  }
+}
+
+// channel masks of 1 / 2 / 4 bytes (d2d_mask_bytes): one typed access, no byte loop
+__device__ __forceinline__ uint32_t load_mask(const void* base, size_t cell, int mask_bytes) {
+  if (mask_bytes == 1) return reinterpret_cast<const uint8_t*>(base)[cell];
+  if (mask_bytes == 2) return reinterpret_cast<const uint16_t*>(base)[cell];
+  return reinterpret_cast<const uint32_t*>(base)[cell];
+}
+__device__ __forceinline__ void store_mask(void* base, size_t cell, int mask_bytes, uint32_t v) {
+  if (mask_bytes == 1) reinterpret_cast<uint8_t*>(base)[cell] = (uint8_t)v;
+  else if (mask_bytes == 2) reinterpret_cast<uint16_t*>(base)[cell] = (uint16_t)v;
+  else reinterpret_cast<uint32_t*>(base)[cell] = v;
+}
+
+// Softmax over the A action logits of env i (lane group g holds actions 4g..4g+3 in lg),
+// sampling / forced / deterministic actions, log-prob and the stores (ippo.py:154-176).
+template <int KIND, bool CRITIC>
+__device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, float value, int env, bool env_ok,
+                                                int k, int g) {
+  const int N = a.N, A = a.A;
+  constexpr bool critic = CRITIC;
+  // ---- softmax over the A actions of env i (lane group g holds actions 4g..4g+3)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (4 * g + r < A) mx = fmaxf(mx, lg[r]);
+  mx = fmaxf(mx, shfl_xor_f(mx, 16));
+  mx = fmaxf(mx, shfl_xor_f(mx, 32));
+  float ex[4], sum = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    ex[r] = (4 * g + r < A) ? expf(lg[r] - mx) : 0.f;
+    sum += ex[r];
+  }
+  sum += shfl_xor_f(sum, 16);
+  sum += shfl_xor_f(sum, 32);
+  float p[4];
+  const float inv = __builtin_amdgcn_rcpf(sum);  // 1 ulp
+#pragma unroll
+  for (int r = 0; r < 4; ++r) p[r] = ex[r] * inv;
+
+  const size_t cell = (size_t)env * N + k;
+  const uint32_t genv = (uint32_t)(a.env_base + (uint64_t)(env_ok ? env : 0));
+  float lp;
+  uint32_t out_bits = 0;
+  int out_id = 0;
+  if constexpr (KIND == 0) {
+    // ---- Bernoulli per channel (combinatorial): u < p, one Philox block per lane group
+    uint32_t forced_bits = 0;
+    if (a.forced) forced_bits = load_mask(a.forced, env_ok ? cell : 0, a.mask_bytes);
+    u32x4 rr = {0, 0, 0, 0};
+    if (!a.forced && !a.deterministic)
+      rr = philox(genv, (uint32_t)k, a.rng_step, (kStreamPolicy << 24) | (uint32_t)g, a.seed);
+    // selects, not branches: the mode tests are wave-uniform, the action index is per lane
+    float lsum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int act = 4 * g + r;
+      const bool b_forced = (forced_bits >> act) & 1u;
+      const bool b_det = p[r] > 0.5f;  // dist.probs > 0.5 (ippo.py:166)
+      const bool b_smp = (float)(pick(rr, r) >> 8) * (1.f / 16777216.f) < p[r];
+      const bool bit = act < A && (a.forced ? b_forced : (a.deterministic ? b_det : b_smp));
+      out_bits |= (uint32_t)bit << act;
+      const float l = bernoulli_logp(p[r], bit);
+      lsum += act < A ? l : 0.f;
+    }
+    lsum += shfl_xor_f(lsum, 16);
+    lsum += shfl_xor_f(lsum, 32);
+    lp = lsum * a.inv_A;  // log_prob(action).mean(-1)
+    out_bits |= (uint32_t)__shfl_xor((int)out_bits, 16, 64);
+    out_bits |= (uint32_t)__shfl_xor((int)out_bits, 32, 64);
+  } else {
+    // ---- Categorical over A ids (channel selection): Categorical(probs) renormalises, log of
+    // the clamped probability; sampling by inverse CDF of one Philox uniform; argmax when deterministic
+    const float eps = 1.1920928955078125e-07f;
+    float psum = p[0] + p[1] + p[2] + p[3];
+    float tot = psum;
+    tot += shfl_xor_f(tot, 16);
+    tot += shfl_xor_f(tot, 32);
+    int chosen = 0;
+    if (a.forced) {
+      chosen = env_ok ? reinterpret_cast<const unsigned char*>(a.forced)[cell] : 0;
+    } else if (a.deterministic) {
+      // first index of the maximum (torch.argmax)
+      float bv = -INFINITY;
+      int bi = A;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * g + r < A && p[r] > bv) { bv = p[r]; bi = 4 * g + r; }
+#pragma unroll
+      for (int m = 16; m <= 32; m <<= 1) {
+        const float ov = shfl_xor_f(bv, m);
+        const int oi = __shfl_xor(bi, m, 64);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      chosen = bi;
+    } else {
+      // prefix over lane groups: exclusive sum of psum for groups < g
+      const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step, (kStreamPolicy << 24), a.seed);
+      const float u = (float)(rr.x >> 8) * (1.f / 16777216.f) * tot;
+      const float s16 = __shfl_xor(psum, 16, 64);  // partner in pair (g ^ 1)
+      const float pair = psum + s16;
+      const float s32 = __shfl_xor(pair, 32, 64);
+      float before = 0.f;
+      if (g & 2) before += s32;
+      if (g & 1) before += s16;
+      int pick_id = A;  // A = "not in my group"
+      float c = before;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (4 * g + r < A && pick_id == A) {
+          c += p[r];
+          if (u < c) pick_id = 4 * g + r;
+        }
+      }
+      int best = pick_id;
+      best = min(best, __shfl_xor(best, 16, 64));
+      best = min(best, __shfl_xor(best, 32, 64));
+      chosen = best < A ? best : A - 1;  // rounding at the very top of the CDF
+    }
+    float lpv = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (4 * g + r == chosen) lpv = __logf(fminf(fmaxf(p[r] * __builtin_amdgcn_rcpf(tot), eps), 1.f - eps));
+    lpv += shfl_xor_f(lpv, 16);
+    lpv += shfl_xor_f(lpv, 32);
+    lp = lpv;
+    out_id = chosen;
+  }
+  if (env_ok && g == 0) {
+    if constexpr (KIND == 0) {
+      store_mask(a.act_out, cell, a.mask_bytes, out_bits);
+    } else {
+      reinterpret_cast<unsigned char*>(a.act_out)[cell] = (unsigned char)out_id;
+    }
+    a.logp_out[(size_t)k * a.E + env] = lp;
+    if (critic && a.value_out) a.value_out[(size_t)k * a.E + env] = value;
   }
 }
 
@@ -173,132 +318,256 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
 #pragma unroll
       for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pv += fmaxf(hv[t][r], 0.f) * v2f[t][r];
+        for (int r = 0; r < 4; ++r) pv = fmaf(relu(hv[t][r]), v2f[t][r], pv);
       pv += shfl_xor_f(pv, 16);
       pv += shfl_xor_f(pv, 32);
       value = pv + c2;
     }
-    // ---- softmax over the A actions of env i (lane group g holds actions 4g..4g+3)
-    float mx = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (4 * g + r < A) mx = fmaxf(mx, lg[r]);
-    mx = fmaxf(mx, shfl_xor_f(mx, 16));
-    mx = fmaxf(mx, shfl_xor_f(mx, 32));
-    float ex[4], sum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      ex[r] = (4 * g + r < A) ? expf(lg[r] - mx) : 0.f;
-      sum += ex[r];
-    }
-    sum += shfl_xor_f(sum, 16);
-    sum += shfl_xor_f(sum, 32);
-    float p[4];
-    const float inv = 1.f / sum;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) p[r] = ex[r] * inv;
+    policy_epilogue<KIND, CRITIC>(a, lg, value, env, env_ok, k, g);
+  }
+}
 
-    const size_t cell = (size_t)env * N + k;
-    const uint32_t genv = (uint32_t)(a.env_base + (uint64_t)(env_ok ? env : 0));
-    float lp;
-    uint32_t out_bits = 0;
-    int out_id = 0;
-    if constexpr (KIND == 0) {
-      // ---- Bernoulli per channel (combinatorial): u < p, one Philox block per lane group
-      uint32_t forced_bits = 0;
-      if (a.forced && env_ok) {
-        const unsigned char* fb = reinterpret_cast<const unsigned char*>(a.forced) + cell * a.mask_bytes;
-        for (int b = 0; b < a.mask_bytes; ++b) forced_bits |= (uint32_t)fb[b] << (8 * b);
+
+// ---------------------------------------------------------------------------------------------
+// Split-bf16 kernel (default).  Every fp32 operand v is written EXACTLY as v = vh + vm + vl with
+// three bf16 parts (8 + 8 + 8 significand bits, truncation split: vh = v with the low 16 bits
+// cleared, vm likewise of v - vh, vl = v - vh - vm).  A product w.x is then the sum of the nine
+// part products; the six with combined weight >= 2^-16 (hh, hm, mh, hl, mm, lh) are kept, so each
+// term is accurate to ~2^-24 relative, i.e. fp32 level, while each v_mfma_f32_16x16x32_bf16
+// (16 cycles/SIMD) does the K=32 work of eight v_mfma_f32_16x16x4_f32 (32 cycles each).
+// Observations are usually bf16-exact (integer buffer counts, channel / ACK bits): a tile whose
+// values all have zero low halves (one ballot) needs only the three weight parts against xh.
+// Layer-1 bias rides in the input column F (x = 1), so KC = ceil((F + 1) / 32) chunks.
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+struct Parts {
+  bf16x8 h, m, l;
+};
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float ffrom(uint32_t u) { return __uint_as_float(u); }
+// bf16 truncations (high halves) of a (low 16 bits of the result) and b (high 16 bits)
+__device__ __forceinline__ uint32_t pack_hi(float a, float b) {
+  return __builtin_amdgcn_perm(fbits(b), fbits(a), 0x07060302u);
+}
+__device__ __forceinline__ bf16x8 as_frag(const uint32_t (&u)[4]) {
+  u32x4v v = {u[0], u[1], u[2], u[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// exact three-way split of 8 floats into bf16 fragments
+__device__ __forceinline__ Parts split3(const float (&v)[8]) {
+  uint32_t H[4], M[4], L[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float a = v[2 * p], b = v[2 * p + 1];
+    const float ar = a - ffrom(fbits(a) & 0xFFFF0000u), br = b - ffrom(fbits(b) & 0xFFFF0000u);
+    const float al = ar - ffrom(fbits(ar) & 0xFFFF0000u), bl = br - ffrom(fbits(br) & 0xFFFF0000u);
+    H[p] = pack_hi(a, b);
+    M[p] = pack_hi(ar, br);
+    L[p] = pack_hi(al, bl);
+  }
+  return {as_frag(H), as_frag(M), as_frag(L)};
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// acc += W.X for split W and X: the six terms of weight >= 2^-16, smallest first.  X exact in
+// bf16 (xm = xl = 0) skips the three terms that would multiply zeros.
+__device__ __forceinline__ f32x4 mfma_split(const Parts& w, const Parts& x, bool x_exact, f32x4 acc) {
+  if (!x_exact) {
+    acc = mfma_bf16(w.h, x.l, acc);
+    acc = mfma_bf16(w.m, x.m, acc);
+    acc = mfma_bf16(w.h, x.m, acc);
+  }
+  acc = mfma_bf16(w.l, x.h, acc);
+  acc = mfma_bf16(w.m, x.h, acc);
+  acc = mfma_bf16(w.h, x.h, acc);
+  return acc;
+}
+
+// obs chunk c of env row: lane group g holds inputs 32c + 8g + j (j < 8); input F is the bias
+// input 1.0.  Every load is an in-row element (column clamped to the row), so the columns past F
+// hold duplicates of this agent's own (finite) inputs, which meet zero weight columns; only the
+// bias column is substituted.  Envs past E read env 0's row (their results are not stored).
+template <int KC>
+__device__ __forceinline__ void load_obs_chunks(float (&x)[KC][8], const float* __restrict__ obs, int env,
+                                                bool env_ok, int N, int k, int F, int g) {
+  const float* row = obs + ((size_t)(env_ok ? env : 0) * N + k) * F;
+  if ((F & 1) == 0) {
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int col = 32 * c + 8 * g + 2 * m;
+        const float2 v = *reinterpret_cast<const float2*>(row + min(col, F - 2));
+        x[c][2 * m] = col == F ? 1.f : v.x;
+        x[c][2 * m + 1] = col + 1 == F ? 1.f : v.y;
       }
-      u32x4 rr = {0, 0, 0, 0};
-      if (!a.forced && !a.deterministic)
-        rr = philox(genv, (uint32_t)k, a.rng_step, (kStreamPolicy << 24) | (uint32_t)g, a.seed);
-      float lsum = 0.f;
+  } else {
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int col = 32 * c + 8 * g + j;
+        const float v = row[min(col, F - 1)];
+        x[c][j] = col == F ? 1.f : v;
+      }
+  }
+}
+
+// KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even)
+template <int KC, int HT, int KIND, bool CRITIC>
+__global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpArgs a) {  // waves / SIMD
+  static_assert(HT % 2 == 0, "layer 2 consumes hidden tiles in pairs");
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const int i = lane & 15;
+  const int k = blockIdx.x;
+  const int wave = threadIdx.x >> 6;
+  const int N = a.N, F = a.F, H = a.H, A = a.A;
+
+  // ---- weight fragments of agent k, split once per workgroup
+  Parts w1p[HT][KC], v1p[CRITIC ? HT : 1][KC], w2p[HT / 2];
+  float v2f[HT][4];
+  f32x4 b2i;
+  {
+    const float* W1 = a.w1 + (size_t)k * H * F;
+    const float* V1 = CRITIC ? a.v1 + (size_t)k * H * F : nullptr;
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      const int hrow = 16 * t + i;
+      const bool hok = hrow < H;
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        float wv[8], vv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int col = 32 * c + 8 * g + j;
+          wv[j] = !hok ? 0.f : col < F ? W1[(size_t)hrow * F + col] : col == F ? a.b1[(size_t)k * H + hrow] : 0.f;
+          if constexpr (CRITIC)
+            vv[j] = !hok ? 0.f : col < F ? V1[(size_t)hrow * F + col] : col == F ? a.c1[(size_t)k * H + hrow] : 0.f;
+        }
+        w1p[t][c] = split3(wv);
+        if constexpr (CRITIC) v1p[t][c] = split3(vv);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int act = 4 * g + r;
-        if (act < A) {
-          bool bit;
-          if (a.forced) bit = (forced_bits >> act) & 1u;
-          else if (a.deterministic) bit = p[r] > 0.5f;  // dist.probs > 0.5 (ippo.py:166)
-          else bit = (float)(pick(rr, r) >> 8) * (1.f / 16777216.f) < p[r];
-          out_bits |= (uint32_t)bit << act;
-          lsum += bernoulli_logp(p[r], bit);
+        const int hid = 16 * t + 4 * g + r;
+        v2f[t][r] = (CRITIC && hid < H) ? a.v2[(size_t)k * H + hid] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int c2 = 0; c2 < HT / 2; ++c2) {
+      // element j of lane group g <-> hidden 16 * (2 c2 + (j >> 2)) + 4 g + (j & 3): the
+      // accumulator registers of layer-1 tiles 2 c2 and 2 c2 + 1
+      float wv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int hid = 16 * (2 * c2 + (j >> 2)) + 4 * g + (j & 3);
+        wv[j] = (i < A && hid < H) ? a.w2[((size_t)k * A + i) * H + hid] : 0.f;
+      }
+      w2p[c2] = split3(wv);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int act = 4 * g + r;
+      b2i[r] = act < A ? a.b2[(size_t)k * A + act] : 0.f;
+    }
+  }
+  const float c2 = CRITIC ? a.c2[k] : 0.f;
+
+  const int tiles = a.envs_per_wave / 16;
+  const int wave_env0 = (blockIdx.y * (blockDim.x >> 6) + wave) * a.envs_per_wave;
+  float xnext[KC][8];
+  load_obs_chunks<KC>(xnext, a.obs, wave_env0 + i, wave_env0 + i < a.E, N, k, F, g);
+  for (int tt = 0; tt < tiles; ++tt) {
+    const int e0 = wave_env0 + tt * 16;
+    if (e0 >= a.E) break;  // wave-uniform
+    const int env = e0 + i;
+    const bool env_ok = env < a.E;
+    // bf16 high parts of the inputs; the residual parts only when some input of the tile is
+    // not bf16-exact (wave-uniform branch, rare for env observations)
+    bf16x8 xh[KC];
+    uint32_t low = 0;
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      uint32_t u[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        low |= (fbits(xnext[c][2 * q]) | fbits(xnext[c][2 * q + 1])) & 0xFFFFu;
+        u[q] = pack_hi(xnext[c][2 * q], xnext[c][2 * q + 1]);
+      }
+      xh[c] = as_frag(u);
+    }
+    const bool x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;  // wave-uniform
+
+    // ---- layer 1 (actor, critic), transposed: H^T = W1' . [X | 1]^T; the three weight parts
+    // against the high parts of X, then (rarely) the residual terms of X
+    f32x4 ha[HT], hv[HT];
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        const f32x4 za = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ha[t];
+        ha[t] = mfma_bf16(w1p[t][c].l, xh[c], za);
+        ha[t] = mfma_bf16(w1p[t][c].m, xh[c], ha[t]);
+        ha[t] = mfma_bf16(w1p[t][c].h, xh[c], ha[t]);
+        if constexpr (CRITIC) {
+          const f32x4 zv = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : hv[t];
+          hv[t] = mfma_bf16(v1p[t][c].l, xh[c], zv);
+          hv[t] = mfma_bf16(v1p[t][c].m, xh[c], hv[t]);
+          hv[t] = mfma_bf16(v1p[t][c].h, xh[c], hv[t]);
         }
       }
-      lsum += shfl_xor_f(lsum, 16);
-      lsum += shfl_xor_f(lsum, 32);
-      lp = lsum / (float)A;  // log_prob(action).mean(-1)
-      out_bits |= (uint32_t)__shfl_xor((int)out_bits, 16, 64);
-      out_bits |= (uint32_t)__shfl_xor((int)out_bits, 32, 64);
-    } else {
-      // ---- Categorical over A ids (channel selection): Categorical(probs) renormalises, log of
-      // the clamped probability; sampling by inverse CDF of one Philox uniform; argmax when deterministic
-      const float eps = 1.1920928955078125e-07f;
-      float psum = p[0] + p[1] + p[2] + p[3];
-      float tot = psum;
-      tot += shfl_xor_f(tot, 16);
-      tot += shfl_xor_f(tot, 32);
-      int chosen = 0;
-      if (a.forced) {
-        chosen = env_ok ? reinterpret_cast<const unsigned char*>(a.forced)[cell] : 0;
-      } else if (a.deterministic) {
-        // first index of the maximum (torch.argmax)
-        float bv = -INFINITY;
-        int bi = A;
+    }
+    if (!x_exact) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (4 * g + r < A && p[r] > bv) { bv = p[r]; bi = 4 * g + r; }
+      for (int c = 0; c < KC; ++c) {
+        const Parts xp = split3(xnext[c]);
 #pragma unroll
-        for (int m = 16; m <= 32; m <<= 1) {
-          const float ov = shfl_xor_f(bv, m);
-          const int oi = __shfl_xor(bi, m, 64);
-          if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-        }
-        chosen = bi;
-      } else {
-        // prefix over lane groups: exclusive sum of psum for groups < g
-        const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step, (kStreamPolicy << 24), a.seed);
-        const float u = (float)(rr.x >> 8) * (1.f / 16777216.f) * tot;
-        const float s16 = __shfl_xor(psum, 16, 64);  // partner in pair (g ^ 1)
-        const float pair = psum + s16;
-        const float s32 = __shfl_xor(pair, 32, 64);
-        float before = 0.f;
-        if (g & 2) before += s32;
-        if (g & 1) before += s16;
-        int pick_id = A;  // A = "not in my group"
-        float c = before;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (4 * g + r < A && pick_id == A) {
-            c += p[r];
-            if (u < c) pick_id = 4 * g + r;
+        for (int t = 0; t < HT; ++t) {
+          ha[t] = mfma_bf16(w1p[t][c].h, xp.l, ha[t]);
+          ha[t] = mfma_bf16(w1p[t][c].m, xp.m, ha[t]);
+          ha[t] = mfma_bf16(w1p[t][c].h, xp.m, ha[t]);
+          if constexpr (CRITIC) {
+            hv[t] = mfma_bf16(v1p[t][c].h, xp.l, hv[t]);
+            hv[t] = mfma_bf16(v1p[t][c].m, xp.m, hv[t]);
+            hv[t] = mfma_bf16(v1p[t][c].h, xp.m, hv[t]);
           }
         }
-        int best = pick_id;
-        best = min(best, __shfl_xor(best, 16, 64));
-        best = min(best, __shfl_xor(best, 32, 64));
-        chosen = best < A ? best : A - 1;  // rounding at the very top of the CDF
       }
-      float lpv = 0.f;
+    }
+    if (tt + 1 < tiles) load_obs_chunks<KC>(xnext, a.obs, env + 16, env + 16 < a.E, N, k, F, g);
+
+    // ---- actor layer 2 on the accumulators of tile pairs (split, full six terms)
+    f32x4 lg = b2i;
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (4 * g + r == chosen) lpv = logf(fminf(fmaxf(p[r] / tot, eps), 1.f - eps));
-      lpv += shfl_xor_f(lpv, 16);
-      lpv += shfl_xor_f(lpv, 32);
-      lp = lpv;
-      out_id = chosen;
-    }
-    if (env_ok && g == 0) {
-      if constexpr (KIND == 0) {
-        unsigned char* ob = reinterpret_cast<unsigned char*>(a.act_out) + cell * a.mask_bytes;
-        for (int b = 0; b < a.mask_bytes; ++b) ob[b] = (unsigned char)(out_bits >> (8 * b));
-      } else {
-        reinterpret_cast<unsigned char*>(a.act_out)[cell] = (unsigned char)out_id;
+    for (int c2 = 0; c2 < HT / 2; ++c2) {
+      float hvals[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hvals[r] = relu(ha[2 * c2][r]);
+        hvals[4 + r] = relu(ha[2 * c2 + 1][r]);
       }
-      a.logp_out[(size_t)k * a.E + env] = lp;
-      if (critic && a.value_out) a.value_out[(size_t)k * a.E + env] = value;
+      lg = mfma_split(w2p[c2], split3(hvals), false, lg);
     }
+    // ---- critic layer 2 (64 -> 1) on VALU
+    float value = 0.f;
+    if constexpr (CRITIC) {
+      float pv = 0.f;
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pv = fmaf(relu(hv[t][r]), v2f[t][r], pv);
+      pv += shfl_xor_f(pv, 16);
+      pv += shfl_xor_f(pv, 32);
+      value = pv + c2;
+    }
+    policy_epilogue<KIND, CRITIC>(a, lg, value, env, env_ok, k, g);
   }
 }
 
@@ -306,8 +575,10 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
 
 using namespace d2d;
 
+int g_policy_f32_mfma = 0;  // d2d_set_option(D2D_OPT_POLICY_F32_MFMA, 1): fp32-MFMA kernel
+
 template <int KS, int HT>
-static int launch_policy(const MlpArgs& a, hipStream_t s) {
+static int launch_policy_f32(const MlpArgs& a, hipStream_t s) {
   const int waves = 4;
   const int envs_per_block = waves * a.envs_per_wave;
   dim3 grid(a.N, (a.E + envs_per_block - 1) / envs_per_block);
@@ -316,6 +587,20 @@ static int launch_policy(const MlpArgs& a, hipStream_t s) {
   else if (a.kind == 0) hipLaunchKernelGGL((policy_mlp_kernel<KS, HT, 0, false>), grid, dim3(64 * waves), 0, s, a);
   else if (critic) hipLaunchKernelGGL((policy_mlp_kernel<KS, HT, 1, true>), grid, dim3(64 * waves), 0, s, a);
   else hipLaunchKernelGGL((policy_mlp_kernel<KS, HT, 1, false>), grid, dim3(64 * waves), 0, s, a);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
+template <int KC, int HT>
+static int launch_policy_split(const MlpArgs& a, hipStream_t s) {
+  const int waves = 4;
+  const int envs_per_block = waves * a.envs_per_wave;
+  dim3 grid(a.N, (a.E + envs_per_block - 1) / envs_per_block);
+  const bool critic = a.v1 != nullptr;
+  if (a.kind == 0 && critic) hipLaunchKernelGGL((policy_split_kernel<KC, HT, 0, true>), grid, dim3(64 * waves), 0, s, a);
+  else if (a.kind == 0) hipLaunchKernelGGL((policy_split_kernel<KC, HT, 0, false>), grid, dim3(64 * waves), 0, s, a);
+  else if (critic) hipLaunchKernelGGL((policy_split_kernel<KC, HT, 1, true>), grid, dim3(64 * waves), 0, s, a);
+  else hipLaunchKernelGGL((policy_split_kernel<KC, HT, 1, false>), grid, dim3(64 * waves), 0, s, a);
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
 }
@@ -335,6 +620,7 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const float* obs, cons
   MlpArgs a;
   a.E = d->n_envs; a.N = d->n_agents; a.F = d->obs_dim; a.H = d->hidden; a.A = d->n_out; a.kind = d->kind;
   a.deterministic = deterministic ? 1 : 0;
+  a.inv_A = 1.f / (float)a.A;
   a.envs_per_wave = 256;
   a.rng_step = rng_step; a.seed = d->seed; a.env_base = d->env_base;
   a.w1 = d->w1; a.b1 = d->b1; a.w2 = d->w2; a.b2 = d->b2; a.v1 = d->v1; a.c1 = d->c1; a.v2 = d->v2; a.c2 = d->c2;
@@ -342,12 +628,12 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const float* obs, cons
   a.mask_bytes = d->n_out <= 8 ? 1 : d->n_out <= 16 ? 2 : 4;
   if (a.E == 0 || a.N == 0) return D2D_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int ks = (a.F + 3) / 4;
   const int ht = (a.H + 15) / 16;
-  if (ks <= 8) {
-    if (ht <= 2) return launch_policy<8, 2>(a, s);
-    return launch_policy<8, 4>(a, s);
+  if (g_policy_f32_mfma || a.F + 1 > 64) {
+    const int ks = (a.F + 3) / 4;
+    if (ks <= 8) return ht <= 2 ? launch_policy_f32<8, 2>(a, s) : launch_policy_f32<8, 4>(a, s);
+    return ht <= 2 ? launch_policy_f32<16, 2>(a, s) : launch_policy_f32<16, 4>(a, s);
   }
-  if (ht <= 2) return launch_policy<16, 2>(a, s);
-  return launch_policy<16, 4>(a, s);
+  if (a.F + 1 <= 32) return ht <= 2 ? launch_policy_split<1, 2>(a, s) : launch_policy_split<1, 4>(a, s);
+  return ht <= 2 ? launch_policy_split<2, 2>(a, s) : launch_policy_split<2, 4>(a, s);
 }

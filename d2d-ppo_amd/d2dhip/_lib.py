@@ -18,6 +18,7 @@ D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION = 0, 1
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
 ABI_VERSION = 1
 D2D_OPT_NT_STORES = 1
+D2D_OPT_POLICY_F32_MFMA = 2
 
 _p = ctypes.c_void_p
 

@@ -178,8 +178,10 @@ int d2d_policy_mlp_step(const d2d_mlp_desc* desc, const float* obs, const void* 
                         int32_t deterministic, void* actions, float* logp, float* value, void* stream);
 
 /* Process-wide tuning options (not part of the reference interface).
- * D2D_OPT_NT_STORES: 1 = write obs/state with non-temporal (streaming) stores. */
-enum { D2D_OPT_NT_STORES = 1 };
+ * D2D_OPT_NT_STORES: 1 = write obs/state with non-temporal (streaming) stores.
+ * D2D_OPT_POLICY_F32_MFMA: 1 = d2d_policy_mlp_step on v_mfma_f32_16x16x4_f32 instead of the
+ *   default exact-split bf16 MFMA kernel (both fp32-accurate; for A/B timing and tests). */
+enum { D2D_OPT_NT_STORES = 1, D2D_OPT_POLICY_F32_MFMA = 2 };
 int d2d_set_option(int32_t option, int32_t value);
 
 const char* d2d_last_error(void);

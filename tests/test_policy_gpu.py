@@ -6,7 +6,9 @@ Tolerance: values 1e-5 absolute; log-probs 1e-5 absolute wherever every probabil
 the (agent, env) lies in [1e-3, 1-1e-3]; elsewhere log(1-p) for p -> 1 is ill-conditioned
 in fp32 for BOTH implementations (a 1-ulp difference in p is a relative 6e-8/(1-p)
 difference in 1-p), so there 1e-3.  Actions exact (sampled actions are compared with the
-same Philox uniforms, ties |u - p| < 1e-6 excluded)."""
+same Philox uniforms, ties |u - p| < 1e-6 excluded).
+Both kernels are covered: the default exact-split bf16 MFMA kernel and the fp32-MFMA one
+(D2D_OPT_POLICY_F32_MFMA); fractional observations exercise the split kernel's six-term path."""
 import numpy as np
 import pytest
 
@@ -14,7 +16,16 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def make(kind, N, E, F, H, A, in_dims=None, seed=0, critic=True):
+@pytest.fixture(params=["split", "f32"], autouse=True)
+def impl(request):
+    from d2dhip import _lib
+    lib = _lib.require_gpu()
+    lib.d2d_set_option(_lib.D2D_OPT_POLICY_F32_MFMA, 1 if request.param == "f32" else 0)
+    yield request.param
+    lib.d2d_set_option(_lib.D2D_OPT_POLICY_F32_MFMA, 0)
+
+
+def make(kind, N, E, F, H, A, in_dims=None, seed=0, critic=True, frac=False):
     from algorithms._core import Policy, StackedNets, Value
     torch.manual_seed(seed)
     dims = in_dims or [F] * N
@@ -25,6 +36,8 @@ def make(kind, N, E, F, H, A, in_dims=None, seed=0, critic=True):
     D = F // 3
     obs[:, :, :D] = torch.randint(0, 3, (E, N, D), generator=g).float()            # buffer counts
     obs[:, :, D:] = torch.randint(-1, 2, (E, N, F - D), generator=g).float()       # channel bits / ACK
+    if frac:  # values that are not bf16-exact
+        obs += torch.rand(obs.shape, generator=g) * 0.3
     for k, d in enumerate(dims):
         obs[:, k, d:] = 0
     dev = "cuda"
@@ -45,16 +58,17 @@ def torch_ref(actor, crit, obs):
 
 CASES = [("comb", 30, 64, 8, None), ("comb", 30, 64, 8, [23, 30, 23, 30, 23, 30, 30]), ("comb", 46, 64, 16, None),
          ("comb", 10, 20, 3, None), ("chsel", 12, 16, 5, None), ("chsel", 24, 64, 16, [24, 20, 24, 21, 24, 24, 24]),
-         ("chsel", 8, 40, 2, None)]
+         ("chsel", 8, 40, 2, None), ("comb", 63, 32, 8, None), ("comb", 64, 64, 8, None), ("chsel", 31, 48, 9, None)]
 
 
+@pytest.mark.parametrize("frac", [False, True])
 @pytest.mark.parametrize("kind,F,H,A,in_dims", CASES)
-def test_forced_and_deterministic_match_torch(kind, F, H, A, in_dims):
+def test_forced_and_deterministic_match_torch(kind, F, H, A, in_dims, frac):
     from d2dhip.envbatch import pack_masks_torch
     from d2dhip.policy import policy_mlp_step
     from torch.distributions import Bernoulli, Categorical
     N, E = 7, 301
-    actor, crit, obs = make(kind, N, E, F, H, A, in_dims)
+    actor, crit, obs = make(kind, N, E, F, H, A, in_dims, frac=frac)
     probs, v = torch_ref(actor, crit, obs)
     g = torch.Generator(device="cuda").manual_seed(3)
     if kind == "comb":
