@@ -43,7 +43,41 @@ struct MlpArgs {
 
 constexpr uint32_t kStreamPolicy = 3;
 
-__device__ __forceinline__ float shfl_xor_f(float v, int m) { return __shfl_xor(v, m, 64); }
+// Exchanges between the four 16-lane groups with the gfx950 lane-swap instructions (VALU; no LDS
+// round trip).  permlane16_swap(v, v) returns {rows 0,0,2,2 ; rows 1,1,3,3} of v, permlane32_swap
+// {lower half twice ; upper half twice}: the sum / max / or of the pair is the xor-16 / xor-32
+// reduction in every lane (same association as v + shfl_xor(v, 16) then + shfl_xor(., 32)), and
+// the element on the other side of lane bit 4 / 5 is the partner value.
+__device__ __forceinline__ uint32_t fu(float v) { return __float_as_uint(v); }
+__device__ __forceinline__ float uf(uint32_t u) { return __uint_as_float(u); }
+template <class Op>
+__device__ __forceinline__ uint32_t group_reduce(uint32_t v, Op op) {
+  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  const uint32_t s = op(p[0], p[1]);
+  const auto q = __builtin_amdgcn_permlane32_swap(s, s, false, false);
+  return op(q[0], q[1]);
+}
+__device__ __forceinline__ float group_sum(float v) {
+  return uf(group_reduce(fu(v), [](uint32_t a, uint32_t b) { return fu(uf(a) + uf(b)); }));
+}
+__device__ __forceinline__ float group_max(float v) {
+  return uf(group_reduce(fu(v), [](uint32_t a, uint32_t b) { return fu(fmaxf(uf(a), uf(b))); }));
+}
+__device__ __forceinline__ uint32_t group_or(uint32_t v) {
+  return group_reduce(v, [](uint32_t a, uint32_t b) { return a | b; });
+}
+__device__ __forceinline__ int group_min(int v) {
+  return (int)group_reduce((uint32_t)v, [](uint32_t a, uint32_t b) { return (uint32_t)min((int)a, (int)b); });
+}
+// value of the lane whose group index differs in bit 0 (xor 16) / bit 1 (xor 32)
+__device__ __forceinline__ uint32_t partner16(uint32_t v, int g) {
+  const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return (g & 1) ? p[0] : p[1];
+}
+__device__ __forceinline__ uint32_t partner32(uint32_t v, int g) {
+  const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (g & 2) ? p[0] : p[1];
+}
 
 // relu as one v_max_i32 on the bit pattern (negative floats are negative ints, -0 -> +0);
 // fmaxf(x, 0) costs a NaN-quieting canonicalize plus the max under the IEEE mode
@@ -116,16 +150,14 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
 #pragma unroll
   for (int r = 0; r < 4; ++r)
     if (4 * g + r < A) mx = fmaxf(mx, lg[r]);
-  mx = fmaxf(mx, shfl_xor_f(mx, 16));
-  mx = fmaxf(mx, shfl_xor_f(mx, 32));
+  mx = group_max(mx);
   float ex[4], sum = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     ex[r] = (4 * g + r < A) ? expf(lg[r] - mx) : 0.f;
     sum += ex[r];
   }
-  sum += shfl_xor_f(sum, 16);
-  sum += shfl_xor_f(sum, 32);
+  sum = group_sum(sum);
   float p[4];
   const float inv = __builtin_amdgcn_rcpf(sum);  // 1 ulp
 #pragma unroll
@@ -138,37 +170,38 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
   int out_id = 0;
   if constexpr (KIND == 0) {
     // ---- Bernoulli per channel (combinatorial): u < p, one Philox block per lane group
-    uint32_t forced_bits = 0;
-    if (a.forced) forced_bits = load_mask(a.forced, env_ok ? cell : 0, a.mask_bytes);
-    u32x4 rr = {0, 0, 0, 0};
-    if (!a.forced && !a.deterministic)
-      rr = philox(genv, (uint32_t)k, a.rng_step, (kStreamPolicy << 24) | (uint32_t)g, a.seed);
-    // selects, not branches: the mode tests are wave-uniform, the action index is per lane
+    // bit r of `taken` = action 4g + r.  Each mode computes it inside its own wave-uniform branch,
+    // so the forced-mask load is waited for there and never drains the obs prefetch in flight.
+    uint32_t taken = 0;
+    if (a.forced) {
+      taken = (load_mask(a.forced, env_ok ? cell : 0, a.mask_bytes) >> (4 * g)) & 0xFu;
+    } else if (a.deterministic) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) taken |= (uint32_t)(p[r] > 0.5f) << r;  // dist.probs > 0.5 (ippo.py:166)
+    } else {
+      const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step, (kStreamPolicy << 24) | (uint32_t)g, a.seed);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) taken |= (uint32_t)((float)(pick(rr, r) >> 8) * (1.f / 16777216.f) < p[r]) << r;
+    }
     float lsum = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int act = 4 * g + r;
-      const bool b_forced = (forced_bits >> act) & 1u;
-      const bool b_det = p[r] > 0.5f;  // dist.probs > 0.5 (ippo.py:166)
-      const bool b_smp = (float)(pick(rr, r) >> 8) * (1.f / 16777216.f) < p[r];
-      const bool bit = act < A && (a.forced ? b_forced : (a.deterministic ? b_det : b_smp));
+      const bool bit = act < A && ((taken >> r) & 1u);
       out_bits |= (uint32_t)bit << act;
       const float l = bernoulli_logp(p[r], bit);
       lsum += act < A ? l : 0.f;
     }
-    lsum += shfl_xor_f(lsum, 16);
-    lsum += shfl_xor_f(lsum, 32);
+    lsum = group_sum(lsum);
     lp = lsum * a.inv_A;  // log_prob(action).mean(-1)
-    out_bits |= (uint32_t)__shfl_xor((int)out_bits, 16, 64);
-    out_bits |= (uint32_t)__shfl_xor((int)out_bits, 32, 64);
+    out_bits = group_or(out_bits);
   } else {
     // ---- Categorical over A ids (channel selection): Categorical(probs) renormalises, log of
     // the clamped probability; sampling by inverse CDF of one Philox uniform; argmax when deterministic
     const float eps = 1.1920928955078125e-07f;
     float psum = p[0] + p[1] + p[2] + p[3];
     float tot = psum;
-    tot += shfl_xor_f(tot, 16);
-    tot += shfl_xor_f(tot, 32);
+    tot = group_sum(tot);
     int chosen = 0;
     if (a.forced) {
       chosen = env_ok ? reinterpret_cast<const unsigned char*>(a.forced)[cell] : 0;
@@ -181,8 +214,8 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
         if (4 * g + r < A && p[r] > bv) { bv = p[r]; bi = 4 * g + r; }
 #pragma unroll
       for (int m = 16; m <= 32; m <<= 1) {
-        const float ov = shfl_xor_f(bv, m);
-        const int oi = __shfl_xor(bi, m, 64);
+        const float ov = uf(m == 16 ? partner16(fu(bv), g) : partner32(fu(bv), g));
+        const int oi = (int)(m == 16 ? partner16((uint32_t)bi, g) : partner32((uint32_t)bi, g));
         if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
       }
       chosen = bi;
@@ -190,9 +223,9 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
       // prefix over lane groups: exclusive sum of psum for groups < g
       const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step, (kStreamPolicy << 24), a.seed);
       const float u = (float)(rr.x >> 8) * (1.f / 16777216.f) * tot;
-      const float s16 = __shfl_xor(psum, 16, 64);  // partner in pair (g ^ 1)
+      const float s16 = uf(partner16(fu(psum), g));  // partner in pair (g ^ 1)
       const float pair = psum + s16;
-      const float s32 = __shfl_xor(pair, 32, 64);
+      const float s32 = uf(partner32(fu(pair), g));
       float before = 0.f;
       if (g & 2) before += s32;
       if (g & 1) before += s16;
@@ -206,16 +239,14 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
         }
       }
       int best = pick_id;
-      best = min(best, __shfl_xor(best, 16, 64));
-      best = min(best, __shfl_xor(best, 32, 64));
+      best = group_min(best);
       chosen = best < A ? best : A - 1;  // rounding at the very top of the CDF
     }
     float lpv = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (4 * g + r == chosen) lpv = __logf(fminf(fmaxf(p[r] * __builtin_amdgcn_rcpf(tot), eps), 1.f - eps));
-    lpv += shfl_xor_f(lpv, 16);
-    lpv += shfl_xor_f(lpv, 32);
+    lpv = group_sum(lpv);
     lp = lpv;
     out_id = chosen;
   }
@@ -238,7 +269,7 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
   const int g = lane >> 4;   // lane group: k-slot of A/B operands, row group of C/D
   const int i = lane & 15;   // row of A / column of B, C/D (the env of the tile)
   const int k = blockIdx.x;  // agent (fast grid axis: all agents of an env chunk run together)
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int N = a.N, F = a.F, H = a.H, A = a.A;
   constexpr bool critic = CRITIC;
 
@@ -319,8 +350,7 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
       for (int t = 0; t < HT; ++t)
 #pragma unroll
         for (int r = 0; r < 4; ++r) pv = fmaf(relu(hv[t][r]), v2f[t][r], pv);
-      pv += shfl_xor_f(pv, 16);
-      pv += shfl_xor_f(pv, 32);
+      pv = group_sum(pv);
       value = pv + c2;
     }
     policy_epilogue<KIND, CRITIC>(a, lg, value, env, env_ok, k, g);
@@ -389,34 +419,29 @@ __device__ __forceinline__ f32x4 mfma_split(const Parts& w, const Parts& x, bool
   return acc;
 }
 
-// obs chunk c of env row: lane group g holds inputs 32c + 8g + j (j < 8); input F is the bias
-// input 1.0.  Every load is an in-row element (column clamped to the row), so the columns past F
-// hold duplicates of this agent's own (finite) inputs, which meet zero weight columns; only the
-// bias column is substituted.  Envs past E read env 0's row (their results are not stored).
+// Raw obs chunk c of env row: lane group g loads inputs 32c + 8g + j (j < 8) with the column
+// clamped into the row, so the columns past F hold duplicates of this agent's own (finite) inputs,
+// which meet zero weight columns.  No value is touched here: any use right after the load would
+// make the compiler wait for it, and these loads are issued two tiles ahead (bias_input() below
+// substitutes the bias input at use).  Envs past E read env 0's row (results not stored).
 template <int KC>
 __device__ __forceinline__ void load_obs_chunks(float (&x)[KC][8], const float* __restrict__ obs, int env,
                                                 bool env_ok, int N, int k, int F, int g) {
+  // one straight-line path of dword loads (a load inside a branch also defeats the counting)
   const float* row = obs + ((size_t)(env_ok ? env : 0) * N + k) * F;
-  if ((F & 1) == 0) {
 #pragma unroll
-    for (int c = 0; c < KC; ++c)
+  for (int c = 0; c < KC; ++c)
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const int col = 32 * c + 8 * g + 2 * m;
-        const float2 v = *reinterpret_cast<const float2*>(row + min(col, F - 2));
-        x[c][2 * m] = col == F ? 1.f : v.x;
-        x[c][2 * m + 1] = col + 1 == F ? 1.f : v.y;
-      }
-  } else {
+    for (int j = 0; j < 8; ++j) x[c][j] = row[min(32 * c + 8 * g + j, F - 1)];
+}
+
+// input column F is the layer-1 bias input 1.0
+template <int KC>
+__device__ __forceinline__ void bias_input(float (&x)[KC][8], int F, int g) {
 #pragma unroll
-    for (int c = 0; c < KC; ++c)
+  for (int c = 0; c < KC; ++c)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int col = 32 * c + 8 * g + j;
-        const float v = row[min(col, F - 1)];
-        x[c][j] = col == F ? 1.f : v;
-      }
-  }
+    for (int j = 0; j < 8; ++j) x[c][j] = 32 * c + 8 * g + j == F ? 1.f : x[c][j];
 }
 
 // KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even)
@@ -427,7 +452,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
   const int g = lane >> 4;
   const int i = lane & 15;
   const int k = blockIdx.x;
-  const int wave = threadIdx.x >> 6;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int N = a.N, F = a.F, H = a.H, A = a.A;
 
   // ---- weight fragments of agent k, split once per workgroup
@@ -482,92 +507,106 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
 
   const int tiles = a.envs_per_wave / 16;
   const int wave_env0 = (blockIdx.y * (blockDim.x >> 6) + wave) * a.envs_per_wave;
-  float xnext[KC][8];
-  load_obs_chunks<KC>(xnext, a.obs, wave_env0 + i, wave_env0 + i < a.E, N, k, F, g);
-  for (int tt = 0; tt < tiles; ++tt) {
-    const int e0 = wave_env0 + tt * 16;
-    if (e0 >= a.E) break;  // wave-uniform
-    const int env = e0 + i;
-    const bool env_ok = env < a.E;
-    // bf16 high parts of the inputs; the residual parts only when some input of the tile is
-    // not bf16-exact (wave-uniform branch, rare for env observations)
-    bf16x8 xh[KC];
-    uint32_t low = 0;
-#pragma unroll
-    for (int c = 0; c < KC; ++c) {
-      uint32_t u[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        low |= (fbits(xnext[c][2 * q]) | fbits(xnext[c][2 * q + 1])) & 0xFFFFu;
-        u[q] = pack_hi(xnext[c][2 * q], xnext[c][2 * q + 1]);
-      }
-      xh[c] = as_frag(u);
-    }
-    const bool x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;  // wave-uniform
-
-    // ---- layer 1 (actor, critic), transposed: H^T = W1' . [X | 1]^T; the three weight parts
-    // against the high parts of X, then (rarely) the residual terms of X
-    f32x4 ha[HT], hv[HT];
-#pragma unroll
-    for (int t = 0; t < HT; ++t) {
-#pragma unroll
+  // Two obs register sets alternate (loop unrolled by two), so each tile's loads are issued two
+  // tiles ahead of their use without a register copy that would wait on them early.
+  auto tile = [&](float (&xc)[KC][8], int tt) {
+      const int e0 = wave_env0 + tt * 16;
+      const int env = e0 + i;
+      const bool env_ok = env < a.E;
+      bias_input<KC>(xc, F, g);
+      // bf16 high parts of the inputs; the residual parts only when some input of the tile is
+      // not bf16-exact (wave-uniform branch, rare for env observations)
+      bf16x8 xh[KC];
+      uint32_t low = 0;
+  #pragma unroll
       for (int c = 0; c < KC; ++c) {
-        const f32x4 za = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ha[t];
-        ha[t] = mfma_bf16(w1p[t][c].l, xh[c], za);
-        ha[t] = mfma_bf16(w1p[t][c].m, xh[c], ha[t]);
-        ha[t] = mfma_bf16(w1p[t][c].h, xh[c], ha[t]);
-        if constexpr (CRITIC) {
-          const f32x4 zv = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : hv[t];
-          hv[t] = mfma_bf16(v1p[t][c].l, xh[c], zv);
-          hv[t] = mfma_bf16(v1p[t][c].m, xh[c], hv[t]);
-          hv[t] = mfma_bf16(v1p[t][c].h, xh[c], hv[t]);
+        uint32_t u[4];
+  #pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          low |= (fbits(xc[c][2 * q]) | fbits(xc[c][2 * q + 1])) & 0xFFFFu;
+          u[q] = pack_hi(xc[c][2 * q], xc[c][2 * q + 1]);
         }
+        xh[c] = as_frag(u);
       }
-    }
-    if (!x_exact) {
-#pragma unroll
-      for (int c = 0; c < KC; ++c) {
-        const Parts xp = split3(xnext[c]);
-#pragma unroll
-        for (int t = 0; t < HT; ++t) {
-          ha[t] = mfma_bf16(w1p[t][c].h, xp.l, ha[t]);
-          ha[t] = mfma_bf16(w1p[t][c].m, xp.m, ha[t]);
-          ha[t] = mfma_bf16(w1p[t][c].h, xp.m, ha[t]);
+      const bool x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;  // wave-uniform
+
+      // ---- layer 1 (actor, critic), transposed: H^T = W1' . [X | 1]^T; the three weight parts
+      // against the high parts of X, then (rarely) the residual terms of X
+      f32x4 ha[HT], hv[HT];
+  #pragma unroll
+      for (int t = 0; t < HT; ++t) {
+  #pragma unroll
+        for (int c = 0; c < KC; ++c) {
+          const f32x4 za = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ha[t];
+          ha[t] = mfma_bf16(w1p[t][c].l, xh[c], za);
+          ha[t] = mfma_bf16(w1p[t][c].m, xh[c], ha[t]);
+          ha[t] = mfma_bf16(w1p[t][c].h, xh[c], ha[t]);
           if constexpr (CRITIC) {
-            hv[t] = mfma_bf16(v1p[t][c].h, xp.l, hv[t]);
-            hv[t] = mfma_bf16(v1p[t][c].m, xp.m, hv[t]);
-            hv[t] = mfma_bf16(v1p[t][c].h, xp.m, hv[t]);
+            const f32x4 zv = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : hv[t];
+            hv[t] = mfma_bf16(v1p[t][c].l, xh[c], zv);
+            hv[t] = mfma_bf16(v1p[t][c].m, xh[c], hv[t]);
+            hv[t] = mfma_bf16(v1p[t][c].h, xh[c], hv[t]);
           }
         }
       }
-    }
-    if (tt + 1 < tiles) load_obs_chunks<KC>(xnext, a.obs, env + 16, env + 16 < a.E, N, k, F, g);
-
-    // ---- actor layer 2 on the accumulators of tile pairs (split, full six terms)
-    f32x4 lg = b2i;
-#pragma unroll
-    for (int c2 = 0; c2 < HT / 2; ++c2) {
-      float hvals[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        hvals[r] = relu(ha[2 * c2][r]);
-        hvals[4 + r] = relu(ha[2 * c2 + 1][r]);
+      if (!x_exact) {
+  #pragma unroll
+        for (int c = 0; c < KC; ++c) {
+          const Parts xp = split3(xc[c]);
+  #pragma unroll
+          for (int t = 0; t < HT; ++t) {
+            ha[t] = mfma_bf16(w1p[t][c].h, xp.l, ha[t]);
+            ha[t] = mfma_bf16(w1p[t][c].m, xp.m, ha[t]);
+            ha[t] = mfma_bf16(w1p[t][c].h, xp.m, ha[t]);
+            if constexpr (CRITIC) {
+              hv[t] = mfma_bf16(v1p[t][c].h, xp.l, hv[t]);
+              hv[t] = mfma_bf16(v1p[t][c].m, xp.m, hv[t]);
+              hv[t] = mfma_bf16(v1p[t][c].h, xp.m, hv[t]);
+            }
+          }
+        }
       }
-      lg = mfma_split(w2p[c2], split3(hvals), false, lg);
-    }
-    // ---- critic layer 2 (64 -> 1) on VALU
-    float value = 0.f;
-    if constexpr (CRITIC) {
-      float pv = 0.f;
-#pragma unroll
-      for (int t = 0; t < HT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pv = fmaf(relu(hv[t][r]), v2f[t][r], pv);
-      pv += shfl_xor_f(pv, 16);
-      pv += shfl_xor_f(pv, 32);
-      value = pv + c2;
-    }
+      // refill this register set with tile tt + 2 (the other set holds tile tt + 1 in flight).
+      // Unconditional (past the end it re-reads env 0's row): a conditional load leaves the
+      // wait-count insertion unable to count the younger loads, and it then drains all of them.
+      load_obs_chunks<KC>(xc, a.obs, env + 32, env + 32 < a.E, N, k, F, g);
+
+      // ---- actor layer 2 on the accumulators of tile pairs (split, full six terms)
+      f32x4 lg = b2i;
+  #pragma unroll
+      for (int c2 = 0; c2 < HT / 2; ++c2) {
+        float hvals[8];
+  #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          hvals[r] = relu(ha[2 * c2][r]);
+          hvals[4 + r] = relu(ha[2 * c2 + 1][r]);
+        }
+        lg = mfma_split(w2p[c2], split3(hvals), false, lg);
+      }
+      // ---- critic layer 2 (64 -> 1) on VALU
+      float value = 0.f;
+      if constexpr (CRITIC) {
+        float pv = 0.f;
+  #pragma unroll
+        for (int t = 0; t < HT; ++t)
+  #pragma unroll
+          for (int r = 0; r < 4; ++r) pv = fmaf(relu(hv[t][r]), v2f[t][r], pv);
+        pv = group_sum(pv);
+        value = pv + c2;
+      }
     policy_epilogue<KIND, CRITIC>(a, lg, value, env, env_ok, k, g);
+  };
+  float xa[KC][8], xb[KC][8];
+  load_obs_chunks<KC>(xa, a.obs, wave_env0 + i, wave_env0 + i < a.E, N, k, F, g);
+  // keep xa's loads older than xb's, as in the loop: otherwise the loop-entry path has the first
+  // used set youngest and the header's wait drains both sets on every iteration
+  __builtin_amdgcn_sched_barrier(0);
+  load_obs_chunks<KC>(xb, a.obs, wave_env0 + 16 + i, wave_env0 + 16 + i < a.E, N, k, F, g);
+  // a fixed, even trip count with no early exit (tiles past E compute on clamped rows and store
+  // nothing): a loop with exits takes several shapes and its wait counting then drains all loads
+  for (int tt = 0; tt < tiles; tt += 2) {
+    tile(xa, tt);
+    tile(xb, tt + 1);
   }
 }
 
