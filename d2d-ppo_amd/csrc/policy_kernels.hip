@@ -42,6 +42,11 @@ struct MlpArgs {
 };
 
 constexpr uint32_t kStreamPolicy = 3;
+enum { kModeSample = 0, kModeDeterministic = 1, kModeForced = 2, kModeRuntime = -1 };
+// The epilogue takes logits pre-multiplied by log2(e) (folded into W2, b2 by the split kernel) so
+// the softmax exponentials are bare v_exp_f32 (exp2, 1 ulp); the relative rounding of the scaled
+// logits is ~2^-24, i.e. a log-prob error ~|logit| * 1e-7.
+constexpr float kLog2e = 1.4426950408889634f;
 
 // Exchanges between the four 16-lane groups with the gfx950 lane-swap instructions (VALU; no LDS
 // round trip).  permlane16_swap(v, v) returns {rows 0,0,2,2 ; rows 1,1,3,3} of v, permlane32_swap
@@ -50,24 +55,30 @@ constexpr uint32_t kStreamPolicy = 3;
 // the element on the other side of lane bit 4 / 5 is the partner value.
 __device__ __forceinline__ uint32_t fu(float v) { return __float_as_uint(v); }
 __device__ __forceinline__ float uf(uint32_t u) { return __uint_as_float(u); }
-template <class Op>
+// HALF: reduce over the two groups of each 32-lane half only (paired epilogue, below)
+template <bool HALF, class Op>
 __device__ __forceinline__ uint32_t group_reduce(uint32_t v, Op op) {
   const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
   const uint32_t s = op(p[0], p[1]);
+  if constexpr (HALF) return s;
   const auto q = __builtin_amdgcn_permlane32_swap(s, s, false, false);
   return op(q[0], q[1]);
 }
+template <bool HALF = false>
 __device__ __forceinline__ float group_sum(float v) {
-  return uf(group_reduce(fu(v), [](uint32_t a, uint32_t b) { return fu(uf(a) + uf(b)); }));
+  return uf(group_reduce<HALF>(fu(v), [](uint32_t a, uint32_t b) { return fu(uf(a) + uf(b)); }));
 }
+template <bool HALF = false>
 __device__ __forceinline__ float group_max(float v) {
-  return uf(group_reduce(fu(v), [](uint32_t a, uint32_t b) { return fu(fmaxf(uf(a), uf(b))); }));
+  return uf(group_reduce<HALF>(fu(v), [](uint32_t a, uint32_t b) { return fu(fmaxf(uf(a), uf(b))); }));
 }
+template <bool HALF = false>
 __device__ __forceinline__ uint32_t group_or(uint32_t v) {
-  return group_reduce(v, [](uint32_t a, uint32_t b) { return a | b; });
+  return group_reduce<HALF>(v, [](uint32_t a, uint32_t b) { return a | b; });
 }
+template <bool HALF = false>
 __device__ __forceinline__ int group_min(int v) {
-  return (int)group_reduce((uint32_t)v, [](uint32_t a, uint32_t b) { return (uint32_t)min((int)a, (int)b); });
+  return (int)group_reduce<HALF>((uint32_t)v, [](uint32_t a, uint32_t b) { return (uint32_t)min((int)a, (int)b); });
 }
 // value of the lane whose group index differs in bit 0 (xor 16) / bit 1 (xor 32)
 __device__ __forceinline__ uint32_t partner16(uint32_t v, int g) {
@@ -138,26 +149,35 @@ __device__ __forceinline__ void store_mask(void* base, size_t cell, int mask_byt
   else reinterpret_cast<uint32_t*>(base)[cell] = v;
 }
 
-// Softmax over the A action logits of env i (lane group g holds actions 4g..4g+3 in lg),
+// Softmax over the A action logits of env i (action group ga holds actions 4ga..4ga+3 in lg),
 // sampling / forced / deterministic actions, log-prob and the stores (ippo.py:154-176).
-template <int KIND, bool CRITIC>
+// HALF (A <= 8): each 32-lane half is its own env tile -- lanes 0-31 one tile, lanes 32-63 the
+// next -- with action group ga = g & 1, so one pass serves two tiles; the Philox counter is
+// (env, agent, step, stream 3 | ga) either way, so the random stream does not depend on it.
+// MODE: kModeSample / kModeDeterministic / kModeForced as a compile-time constant (the split
+// kernel: no forced-mask load exists in the sampling kernel, so nothing in it can drain the obs
+// prefetch), or kModeRuntime (tested per launch from a.forced / a.deterministic).
+template <int KIND, bool CRITIC, bool HALF = false, int MODE = kModeRuntime>
 __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, float value, int env, bool env_ok,
                                                 int k, int g) {
   const int N = a.N, A = a.A;
   constexpr bool critic = CRITIC;
+  const int ga = HALF ? (g & 1) : g;
+  const bool forced = MODE == kModeRuntime ? a.forced != nullptr : MODE == kModeForced;
+  const bool deterministic = MODE == kModeRuntime ? a.deterministic != 0 : MODE == kModeDeterministic;
   // ---- softmax over the A actions of env i (lane group g holds actions 4g..4g+3)
   float mx = -INFINITY;
 #pragma unroll
   for (int r = 0; r < 4; ++r)
-    if (4 * g + r < A) mx = fmaxf(mx, lg[r]);
-  mx = group_max(mx);
+    if (4 * ga + r < A) mx = fmaxf(mx, lg[r]);
+  mx = group_max<HALF>(mx);
   float ex[4], sum = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    ex[r] = (4 * g + r < A) ? expf(lg[r] - mx) : 0.f;
+    ex[r] = (4 * ga + r < A) ? __builtin_amdgcn_exp2f(lg[r] - mx) : 0.f;  // v_exp_f32, 1 ulp
     sum += ex[r];
   }
-  sum = group_sum(sum);
+  sum = group_sum<HALF>(sum);
   float p[4];
   const float inv = __builtin_amdgcn_rcpf(sum);  // 1 ulp
 #pragma unroll
@@ -173,47 +193,47 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
     // bit r of `taken` = action 4g + r.  Each mode computes it inside its own wave-uniform branch,
     // so the forced-mask load is waited for there and never drains the obs prefetch in flight.
     uint32_t taken = 0;
-    if (a.forced) {
-      taken = (load_mask(a.forced, env_ok ? cell : 0, a.mask_bytes) >> (4 * g)) & 0xFu;
-    } else if (a.deterministic) {
+    if (forced) {
+      taken = (load_mask(a.forced, env_ok ? cell : 0, a.mask_bytes) >> (4 * ga)) & 0xFu;
+    } else if (deterministic) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) taken |= (uint32_t)(p[r] > 0.5f) << r;  // dist.probs > 0.5 (ippo.py:166)
     } else {
-      const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step, (kStreamPolicy << 24) | (uint32_t)g, a.seed);
+      const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step, (kStreamPolicy << 24) | (uint32_t)ga, a.seed);
 #pragma unroll
       for (int r = 0; r < 4; ++r) taken |= (uint32_t)((float)(pick(rr, r) >> 8) * (1.f / 16777216.f) < p[r]) << r;
     }
     float lsum = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int act = 4 * g + r;
+      const int act = 4 * ga + r;
       const bool bit = act < A && ((taken >> r) & 1u);
       out_bits |= (uint32_t)bit << act;
       const float l = bernoulli_logp(p[r], bit);
       lsum += act < A ? l : 0.f;
     }
-    lsum = group_sum(lsum);
+    lsum = group_sum<HALF>(lsum);
     lp = lsum * a.inv_A;  // log_prob(action).mean(-1)
-    out_bits = group_or(out_bits);
+    out_bits = group_or<HALF>(out_bits);
   } else {
     // ---- Categorical over A ids (channel selection): Categorical(probs) renormalises, log of
     // the clamped probability; sampling by inverse CDF of one Philox uniform; argmax when deterministic
     const float eps = 1.1920928955078125e-07f;
     float psum = p[0] + p[1] + p[2] + p[3];
     float tot = psum;
-    tot = group_sum(tot);
+    tot = group_sum<HALF>(tot);
     int chosen = 0;
-    if (a.forced) {
+    if (forced) {
       chosen = env_ok ? reinterpret_cast<const unsigned char*>(a.forced)[cell] : 0;
-    } else if (a.deterministic) {
+    } else if (deterministic) {
       // first index of the maximum (torch.argmax)
       float bv = -INFINITY;
       int bi = A;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if (4 * g + r < A && p[r] > bv) { bv = p[r]; bi = 4 * g + r; }
+        if (4 * ga + r < A && p[r] > bv) { bv = p[r]; bi = 4 * ga + r; }
 #pragma unroll
-      for (int m = 16; m <= 32; m <<= 1) {
+      for (int m = 16; m <= (HALF ? 16 : 32); m <<= 1) {
         const float ov = uf(m == 16 ? partner16(fu(bv), g) : partner32(fu(bv), g));
         const int oi = (int)(m == 16 ? partner16((uint32_t)bi, g) : partner32((uint32_t)bi, g));
         if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
@@ -225,32 +245,34 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
       const float u = (float)(rr.x >> 8) * (1.f / 16777216.f) * tot;
       const float s16 = uf(partner16(fu(psum), g));  // partner in pair (g ^ 1)
       const float pair = psum + s16;
-      const float s32 = uf(partner32(fu(pair), g));
       float before = 0.f;
-      if (g & 2) before += s32;
+      if constexpr (!HALF) {
+        const float s32 = uf(partner32(fu(pair), g));
+        if (g & 2) before += s32;
+      }
       if (g & 1) before += s16;
       int pick_id = A;  // A = "not in my group"
       float c = before;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        if (4 * g + r < A && pick_id == A) {
+        if (4 * ga + r < A && pick_id == A) {
           c += p[r];
-          if (u < c) pick_id = 4 * g + r;
+          if (u < c) pick_id = 4 * ga + r;
         }
       }
       int best = pick_id;
-      best = group_min(best);
+      best = group_min<HALF>(best);
       chosen = best < A ? best : A - 1;  // rounding at the very top of the CDF
     }
     float lpv = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (4 * g + r == chosen) lpv = __logf(fminf(fmaxf(p[r] * __builtin_amdgcn_rcpf(tot), eps), 1.f - eps));
-    lpv = group_sum(lpv);
+      if (4 * ga + r == chosen) lpv = __logf(fminf(fmaxf(p[r] * __builtin_amdgcn_rcpf(tot), eps), 1.f - eps));
+    lpv = group_sum<HALF>(lpv);
     lp = lpv;
     out_id = chosen;
   }
-  if (env_ok && g == 0) {
+  if (env_ok && ga == 0) {
     if constexpr (KIND == 0) {
       store_mask(a.act_out, cell, a.mask_bytes, out_bits);
     } else {
@@ -353,6 +375,8 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
       pv = group_sum(pv);
       value = pv + c2;
     }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lg[r] *= kLog2e;
     policy_epilogue<KIND, CRITIC>(a, lg, value, env, env_ok, k, g);
   }
 }
@@ -419,33 +443,42 @@ __device__ __forceinline__ f32x4 mfma_split(const Parts& w, const Parts& x, bool
   return acc;
 }
 
-// Raw obs chunk c of env row: lane group g loads inputs 32c + 8g + j (j < 8) with the column
-// clamped into the row, so the columns past F hold duplicates of this agent's own (finite) inputs,
-// which meet zero weight columns.  No value is touched here: any use right after the load would
-// make the compiler wait for it, and these loads are issued two tiles ahead (bias_input() below
-// substitutes the bias input at use).  Envs past E read env 0's row (results not stored).
+// Obs staging: a per-wave ring of RING tile slots in LDS, filled by buffer->LDS DMA
+// (buffer_load_dword ... lds, no VGPR destination) RING - 2 tiles ahead of use.  Slot layout
+// [c][j][lane] (lane-linear, as the DMA writes it): DMA instruction (c, j) brings lane (g, i) the
+// input 32c + 8g + j of its env row, which is exactly element j of its MFMA B fragment.  The
+// buffer descriptor's range check returns 0 past the obs buffer, so the row is read unclamped:
+// the columns past F hold the next agent's inputs and are zeroed by stage_inputs().
+// hipcc does not order the DMA's LDS write before the ds_read of the slot, so the waits are
+// explicit, counted s_waitcnt vmcnt (see the loop).
+// ring depth: 6 tiles at KC = 1; 4 at KC = 2 (the counted wait must stay below vmcnt's 63)
 template <int KC>
-__device__ __forceinline__ void load_obs_chunks(float (&x)[KC][8], const float* __restrict__ obs, int env,
-                                                bool env_ok, int N, int k, int F, int g) {
-  // one straight-line path of dword loads (a load inside a branch also defeats the counting)
-  const float* row = obs + ((size_t)(env_ok ? env : 0) * N + k) * F;
-#pragma unroll
-  for (int c = 0; c < KC; ++c)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x[c][j] = row[min(32 * c + 8 * g + j, F - 1)];
+constexpr int ring_tiles() { return KC == 1 ? 6 : 4; }
+
+template <int N_OUTSTANDING>
+__device__ __forceinline__ void wait_vmem() {
+  static_assert(N_OUTSTANDING < 64, "vmcnt field is 6 bits");
+  // vmcnt = N (bits 3:0 and 15:14), expcnt / lgkmcnt at their maxima = no wait on them
+  __builtin_amdgcn_s_waitcnt(0x0F70 | (N_OUTSTANDING & 15) | ((N_OUTSTANDING >> 4) << 14));
 }
 
-// input column F is the layer-1 bias input 1.0
+// x[c][j] <- slot, then input F := 1.0 (layer-1 bias input) and inputs past F := 0
 template <int KC>
-__device__ __forceinline__ void bias_input(float (&x)[KC][8], int F, int g) {
+__device__ __forceinline__ void stage_inputs(float (&x)[KC][8], const float* slot, int lane, int F, int g) {
 #pragma unroll
   for (int c = 0; c < KC; ++c)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) x[c][j] = 32 * c + 8 * g + j == F ? 1.f : x[c][j];
+    for (int j = 0; j < 8; ++j) {
+      // (v & keep) | bias: one v_and_or_b32 -- a select of the loaded value would be turned
+      // into a branch around the LDS read
+      const int col = 32 * c + 8 * g + j;
+      const uint32_t keep = col < F ? 0xFFFFFFFFu : 0u, bias = col == F ? 0x3F800000u : 0u;
+      x[c][j] = uf((fu(slot[(c * 8 + j) * 64 + lane]) & keep) | bias);
+    }
 }
 
 // KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even)
-template <int KC, int HT, int KIND, bool CRITIC>
+template <int KC, int HT, int KIND, bool CRITIC, int MODE>
 __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpArgs a) {  // waves / SIMD
   static_assert(HT % 2 == 0, "layer 2 consumes hidden tiles in pairs");
   const int lane = threadIdx.x & 63;
@@ -493,14 +526,14 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int hid = 16 * (2 * c2 + (j >> 2)) + 4 * g + (j & 3);
-        wv[j] = (i < A && hid < H) ? a.w2[((size_t)k * A + i) * H + hid] : 0.f;
+        wv[j] = (i < A && hid < H) ? a.w2[((size_t)k * A + i) * H + hid] * kLog2e : 0.f;
       }
       w2p[c2] = split3(wv);
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int act = 4 * g + r;
-      b2i[r] = act < A ? a.b2[(size_t)k * A + act] : 0.f;
+      b2i[r] = act < A ? a.b2[(size_t)k * A + act] * kLog2e : 0.f;
     }
   }
   const float c2 = CRITIC ? a.c2[k] : 0.f;
@@ -509,19 +542,37 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
   const int wave_env0 = (blockIdx.y * (blockDim.x >> 6) + wave) * a.envs_per_wave;
   // Two obs register sets alternate (loop unrolled by two), so each tile's loads are issued two
   // tiles ahead of their use without a register copy that would wait on them early.
-  auto tile = [&](float (&xc)[KC][8], int tt) {
-      const int e0 = wave_env0 + tt * 16;
-      const int env = e0 + i;
-      const bool env_ok = env < a.E;
-      bias_input<KC>(xc, F, g);
+  constexpr int RING = ring_tiles<KC>();
+  __shared__ float ring[4][RING][KC][8][64];
+  const float* wbase = a.obs + ((size_t)wave_env0 * N + k) * F;
+  const int64_t total = (int64_t)a.E * N * F * 4, done = ((int64_t)wave_env0 * N + k) * F * 4;
+  const int64_t rest = total - done;
+  const uint32_t nbytes = rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), 0, nbytes, 0x00020000);
+  auto issue = [&](int t) {
+    // look-ahead tiles past this wave's last are still issued (the counted waits need a fixed
+    // DMA count) but aimed outside the descriptor's range: no memory traffic, zeros
+    const uint32_t vo = t < tiles ? ((uint32_t)((t * 16 + i) * N * F) + 8 * g) * 4 : 0x80000000u;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsrc, (__attribute__((address_space(3))) void*)&ring[wave][t % RING][c][j][0], 4,
+            vo + 4 * (32 * c + j), 0, 0, 0);
+  };
+  // layers 1-2 of one tile -> (pre-scaled) logits lg and critic value
+  auto tile = [&](int tt, f32x4& lg, float& value) {
+      float xc[KC][8];
+      stage_inputs<KC>(xc, &ring[wave][tt % RING][0][0][0], lane, F, g);
       // bf16 high parts of the inputs; the residual parts only when some input of the tile is
       // not bf16-exact (wave-uniform branch, rare for env observations)
       bf16x8 xh[KC];
       uint32_t low = 0;
-  #pragma unroll
+#pragma unroll
       for (int c = 0; c < KC; ++c) {
         uint32_t u[4];
-  #pragma unroll
+#pragma unroll
         for (int q = 0; q < 4; ++q) {
           low |= (fbits(xc[c][2 * q]) | fbits(xc[c][2 * q + 1])) & 0xFFFFu;
           u[q] = pack_hi(xc[c][2 * q], xc[c][2 * q + 1]);
@@ -533,9 +584,9 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
       // ---- layer 1 (actor, critic), transposed: H^T = W1' . [X | 1]^T; the three weight parts
       // against the high parts of X, then (rarely) the residual terms of X
       f32x4 ha[HT], hv[HT];
-  #pragma unroll
+#pragma unroll
       for (int t = 0; t < HT; ++t) {
-  #pragma unroll
+#pragma unroll
         for (int c = 0; c < KC; ++c) {
           const f32x4 za = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ha[t];
           ha[t] = mfma_bf16(w1p[t][c].l, xh[c], za);
@@ -550,10 +601,10 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
         }
       }
       if (!x_exact) {
-  #pragma unroll
+#pragma unroll
         for (int c = 0; c < KC; ++c) {
           const Parts xp = split3(xc[c]);
-  #pragma unroll
+#pragma unroll
           for (int t = 0; t < HT; ++t) {
             ha[t] = mfma_bf16(w1p[t][c].h, xp.l, ha[t]);
             ha[t] = mfma_bf16(w1p[t][c].m, xp.m, ha[t]);
@@ -566,17 +617,13 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
           }
         }
       }
-      // refill this register set with tile tt + 2 (the other set holds tile tt + 1 in flight).
-      // Unconditional (past the end it re-reads env 0's row): a conditional load leaves the
-      // wait-count insertion unable to count the younger loads, and it then drains all of them.
-      load_obs_chunks<KC>(xc, a.obs, env + 32, env + 32 < a.E, N, k, F, g);
 
       // ---- actor layer 2 on the accumulators of tile pairs (split, full six terms)
-      f32x4 lg = b2i;
-  #pragma unroll
+      lg = b2i;
+#pragma unroll
       for (int c2 = 0; c2 < HT / 2; ++c2) {
         float hvals[8];
-  #pragma unroll
+#pragma unroll
         for (int r = 0; r < 4; ++r) {
           hvals[r] = relu(ha[2 * c2][r]);
           hvals[4 + r] = relu(ha[2 * c2 + 1][r]);
@@ -584,30 +631,47 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
         lg = mfma_split(w2p[c2], split3(hvals), false, lg);
       }
       // ---- critic layer 2 (64 -> 1) on VALU
-      float value = 0.f;
+      value = 0.f;
       if constexpr (CRITIC) {
         float pv = 0.f;
-  #pragma unroll
+#pragma unroll
         for (int t = 0; t < HT; ++t)
-  #pragma unroll
+#pragma unroll
           for (int r = 0; r < 4; ++r) pv = fmaf(relu(hv[t][r]), v2f[t][r], pv);
         pv = group_sum(pv);
         value = pv + c2;
       }
-    policy_epilogue<KIND, CRITIC>(a, lg, value, env, env_ok, k, g);
   };
-  float xa[KC][8], xb[KC][8];
-  load_obs_chunks<KC>(xa, a.obs, wave_env0 + i, wave_env0 + i < a.E, N, k, F, g);
-  // keep xa's loads older than xb's, as in the loop: otherwise the loop-entry path has the first
-  // used set youngest and the header's wait drains both sets on every iteration
-  __builtin_amdgcn_sched_barrier(0);
-  load_obs_chunks<KC>(xb, a.obs, wave_env0 + 16 + i, wave_env0 + 16 + i < a.E, N, k, F, g);
-  // a fixed, even trip count with no early exit (tiles past E compute on clamped rows and store
-  // nothing): a loop with exits takes several shapes and its wait counting then drains all loads
+  // every wave runs the same even number of tiles (tiles past E read zeros and store nothing), so
+  // the DMA count between a tile's issue and its wait is fixed: RING - 2 tiles of KC * 8 DMAs
+  // (anything else issued in between -- the stores -- only makes the counted wait stricter)
+  static_assert(RING >= 4 && RING % 2 == 0, "two tiles per iteration");
+  for (int t = 0; t < RING - 2; ++t) issue(t);
   for (int tt = 0; tt < tiles; tt += 2) {
-    tile(xa, tt);
-    tile(xb, tt + 1);
+    issue(tt + RING - 2);
+    issue(tt + RING - 1);
+    wait_vmem<(RING - 2) * KC * 8>();  // tiles tt, tt + 1 have landed
+    __builtin_amdgcn_sched_barrier(0);        // no LDS read of the slots moves above the wait
+    f32x4 lg0, lg1;
+    float v0, v1;
+    tile(tt, lg0, v0);
+    tile(tt + 1, lg1, v1);
+    __builtin_amdgcn_sched_barrier(0);        // the slots are read before the next DMA reuses them
+    const int env0 = wave_env0 + tt * 16 + i, env1 = env0 + 16;
+    if (A <= 8) {
+      // one epilogue for both tiles: lanes 0-31 keep tile tt (action groups 0, 1), lanes 32-63
+      // take tile tt + 1's lanes 0-31 (permlane32_swap: vdst upper half <- src lower half)
+      f32x4 lgc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lgc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(lg0[r]), fu(lg1[r]), false, false)[0]);
+      const int envc = g < 2 ? env0 : env1;
+      policy_epilogue<KIND, CRITIC, true, MODE>(a, lgc, g < 2 ? v0 : v1, envc, envc < a.E, k, g);
+    } else {
+      policy_epilogue<KIND, CRITIC, false, MODE>(a, lg0, v0, env0, env0 < a.E, k, g);
+      policy_epilogue<KIND, CRITIC, false, MODE>(a, lg1, v1, env1, env1 < a.E, k, g);
+    }
   }
+  wait_vmem<0>();  // no LDS-DMA may land after the wave (and its LDS allocation) is gone
 }
 
 }  // namespace d2d
@@ -630,16 +694,23 @@ static int launch_policy_f32(const MlpArgs& a, hipStream_t s) {
   return D2D_OK;
 }
 
+template <int KC, int HT, int KIND, bool CRITIC>
+static void launch_split_mode(const MlpArgs& a, dim3 grid, hipStream_t s) {
+  if (a.forced) hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeForced>), grid, dim3(256), 0, s, a);
+  else if (a.deterministic)
+    hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeDeterministic>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeSample>), grid, dim3(256), 0, s, a);
+}
+
 template <int KC, int HT>
 static int launch_policy_split(const MlpArgs& a, hipStream_t s) {
-  const int waves = 4;
-  const int envs_per_block = waves * a.envs_per_wave;
+  const int envs_per_block = 4 * a.envs_per_wave;  // 4 waves
   dim3 grid(a.N, (a.E + envs_per_block - 1) / envs_per_block);
   const bool critic = a.v1 != nullptr;
-  if (a.kind == 0 && critic) hipLaunchKernelGGL((policy_split_kernel<KC, HT, 0, true>), grid, dim3(64 * waves), 0, s, a);
-  else if (a.kind == 0) hipLaunchKernelGGL((policy_split_kernel<KC, HT, 0, false>), grid, dim3(64 * waves), 0, s, a);
-  else if (critic) hipLaunchKernelGGL((policy_split_kernel<KC, HT, 1, true>), grid, dim3(64 * waves), 0, s, a);
-  else hipLaunchKernelGGL((policy_split_kernel<KC, HT, 1, false>), grid, dim3(64 * waves), 0, s, a);
+  if (a.kind == 0 && critic) launch_split_mode<KC, HT, 0, true>(a, grid, s);
+  else if (a.kind == 0) launch_split_mode<KC, HT, 0, false>(a, grid, s);
+  else if (critic) launch_split_mode<KC, HT, 1, true>(a, grid, s);
+  else launch_split_mode<KC, HT, 1, false>(a, grid, s);
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
 }
