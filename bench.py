@@ -77,7 +77,7 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-def cpu_baseline(params, seconds=12.0, max_envs=8192):
+def cpu_baseline(params, seconds=12.0, max_envs=8192):  # bounded: ~`seconds` of host work
     """C oracle ("port") on the host cores, Philox mode, same workload, bounded sample."""
     from oracle.c_oracle import COracle
     try:
@@ -99,7 +99,7 @@ def cpu_baseline(params, seconds=12.0, max_envs=8192):
             c.reset(rng_step=rs, want_state=False)
             rs += 1
         el = time.perf_counter() - t0
-        if el >= seconds or steps >= 400:
+        if el >= seconds or steps >= 4000:
             break
     v = E * steps / el
     return {"value": v, "unit": "env-steps/s", "cores": threads, "kind": "port",
@@ -151,7 +151,8 @@ def rollout_leg(env, args, world):
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world)
     v = b.E * world * K / el
-    path = "fused HIP policy kernel (fp32 MFMA)" if lr._fused_ok() else "torch agent-stacked bmm"
+    path = ("fused HIP policy kernel (exact 3-way bf16 split MFMA, fp32-accurate)" if lr._fused_ok()
+            else "torch agent-stacked bmm")
     return {"env_steps_per_s": v, "agent_steps_per_s": v * b.spec.N, "ms_per_step": el / K * 1e3, "steps": K,
             "policy": f"iPPO MLP H=64 actor+critic, 64 agents, Bernoulli sampling, fp32; {path}"}
 
