@@ -53,12 +53,20 @@ def config3_params(episode_length=200):
 
 
 def setup_dist(n_gpus):
+    """One process per GPU over RCCL ("nccl").  Rehearsal switches for a 1-GPU box (never set by
+    the driver): D2D_BENCH_BACKEND=gloo and D2D_BENCH_SHARE_GPU=1 (every rank on cuda:0)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("D2D_BENCH_SHARE_GPU") == "1":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("D2D_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return rank, world, local
