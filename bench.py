@@ -176,21 +176,23 @@ def ppo_leg(args, rank, world, local):
     lr = iPPO(env2, hidden_size=64, gamma=0.6, policy_lr=3e-4, value_lr=1e-3, device=f"cuda:{local}",
               useRNN=False, combinatorial=True)
     ro = lr._rollout(E2)
-    x, acts, logp_old = lr._update_inputs(ro)
-    lr._epoch(x, acts, logp_old, ro.adv, ro.ret)  # warm-up (allocator, hipBLASLt heuristics)
+    upd = lr._update_state(ro)
+    lr._update_epoch(ro, upd)  # warm-up (allocator, hipBLASLt heuristics)
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
     P = args.ppo_epochs
     for _ in range(P):
-        lr._epoch(x, acts, logp_old, ro.adv, ro.ret)
+        lr._update_epoch(ro, upd)
     torch.cuda.synchronize()
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world)
     N = params["n_agents"]
     samples = ro.T * E2 * world
     flop = 6.0 * N * samples * (30 * 64 + 64 * 8 + 30 * 64 + 64)  # fwd+bwd ~ 3x fwd, 2 flop/mac
-    return {"updates_per_s": P / el, "ms_per_update": el / P * 1e3, "epochs": P,
+    path = ("fused HIP update kernels (actor + critic gradients, exact-split bf16 MFMA) + torch Adam"
+            if upd is None else "torch agent-stacked bmm autograd + Adam")
+    return {"updates_per_s": P / el, "ms_per_update": el / P * 1e3, "epochs": P, "path": path,
             "batch": f"{E2} envs/GPU x {ro.T} slots x {N} agents (actor+critic, one Adam step each)",
             "agent_samples_per_update": samples * N, "agent_samples_per_s": samples * N * P / el,
             "gemm_tflops": flop * P / el / 1e12}

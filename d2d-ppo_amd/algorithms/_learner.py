@@ -108,6 +108,43 @@ class BatchedLearnerBase(DataParallelMixin):
                            and os.environ.get("D2D_FUSED_POLICY", "1") != "0")
         return self._fused
 
+    def _fused_update_ok(self):
+        """The fused HIP update kernels (csrc/update_kernels.hip) cover the MLP actors with
+        F + 1 <= 64 inputs (and the iPPO per-agent MLP critics)."""
+        if getattr(self, "_fused_upd", None) is None:
+            self._fused_upd = (self._fused_ok() and self.policy.F + 1 <= 64
+                               and (self.kind == "comb") == bool(self.combinatorial)
+                               and os.environ.get("D2D_FUSED_UPDATE", "1") != "0")
+        return self._fused_upd
+
+    @staticmethod
+    def _grad_buffers(params):
+        """The .grad tensors of agent-stacked params (allocated once; the kernels overwrite them)."""
+        for p in params.values():
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        return {k: p.grad for k, p in params.items()}
+
+    def _update_state(self, ro):
+        """What an epoch of the update needs beyond the rollout: nothing for the fused kernels
+        (they read the rollout buffers in place), the agent-major copies for the torch path."""
+        return None if self._fused_update_ok() else self._update_inputs(ro)
+
+    def _logp_forced(self, ro):
+        """log-probs of the rollout's own actions under the current actor params, for every
+        sample: the policy kernel in forced mode over the T*E slots at once -> [N][T*E] (time-major)."""
+        from d2dhip import _lib
+        lib = _lib.require_gpu()
+        N, TE = self.policy.N, ro.T * ro.E
+        desc = self._mlp_desc(TE, 0)
+        desc.v1 = desc.c1 = desc.v2 = desc.c2 = None
+        logp = torch.empty((N, TE), dtype=torch.float32, device=self.device)
+        scratch = torch.empty_like(ro.actions)
+        rc = lib.d2d_policy_mlp_step(desc, ro.obs.data_ptr(), ro.actions.data_ptr(), 0, 0, scratch.data_ptr(),
+                                     logp.data_ptr(), None, _lib.stream_ptr())
+        _lib.check(rc, "d2d_policy_mlp_step (forced)")
+        return logp
+
     def _policy_seed(self):
         if getattr(self, "_pseed", None) is None:
             # drawn from torch's global RNG, so torch.manual_seed makes rollouts reproducible,

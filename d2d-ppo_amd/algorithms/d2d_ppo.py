@@ -203,6 +203,49 @@ class D2DPPO(BatchedLearnerBase):
         pl = ploss.detach().cpu().numpy()
         return [float(pl[i]) for i in cycle], value_loss.detach()
 
+    def _epoch_fused(self, ro, cliprange=0.1):
+        """The same epoch with the actors on the HIP kernels: epoch-start ratios of every agent
+        from the policy kernel (forced actions), the chain M, then the fused actor-gradient
+        kernel with W = M and beta_entropy; clipping, Adam and the central critic in torch.
+        Sample order here is time-major (t * E + e); the sums do not depend on it."""
+        from d2dhip.update import actor_grads
+        cycle = np.arange(self.n_agents)
+        np.random.shuffle(cycle)
+        cycle = self._sync_perm(cycle)
+        values = self.value_network(ro.state_seq).squeeze()
+        v_te = values.detach().view(ro.E, ro.T).t().unsqueeze(2).contiguous()
+        adv, _ = self._gae(ro.rewards, v_te, ro.dones, normalize_adv=True, normalize_ret=False)
+        T, E, N = ro.T, ro.E, self.n_agents
+        A = adv[:, :, 0].reshape(-1)                                                   # [T*E]
+        logp_old = ro.logp.permute(1, 0, 2).reshape(N, T * E)
+        with torch.no_grad():
+            ratio = torch.exp(self._logp_forced(ro) - logp_old)                        # [N][T*E]
+            M = happo_chain(A, ratio, cycle)
+        pp = self.policy.params
+        kind = "comb" if self.combinatorial else "chsel"
+        beta = float(self.beta_entropy)
+        _, sa = actor_grads({k: v.data for k, v in pp.items()}, ro.obs, ro.actions, ro.logp.permute(0, 2, 1),
+                            M.view(N, T, E).permute(1, 2, 0), kind, clip=cliprange, beta=beta,
+                            grads=self._grad_buffers(pp))
+        self._reduce_grads(self.policy.parameters())
+        self.policy.grad_norm_clip_(20)
+        self.policy_optimizer.step()
+        ploss = -(sa[:, 0] + beta * sa[:, 1]) / (T * E)
+        value_loss = F.mse_loss(values, ro.ret_mean, reduction='mean')
+        self.value_optimizer.zero_grad()
+        value_loss.backward()
+        self._reduce_grads(list(self.value_network.parameters()))
+        torch.nn.utils.clip_grad_norm_(self.value_network.parameters(), 20)
+        self.value_optimizer.step()
+        pl = ploss.detach().cpu().numpy()
+        return [float(pl[i]) for i in cycle], value_loss.detach()
+
+    def _update_epoch(self, ro, upd):
+        if upd is None:
+            return self._epoch_fused(ro)
+        x, acts, logp_old = upd
+        return self._epoch(ro, x, acts, logp_old)
+
     def train(self, num_iter, num_episodes=4, n_epoch=4, test_freq=100):
         scores_episode = []
         score_test_list = []
@@ -212,9 +255,9 @@ class D2DPPO(BatchedLearnerBase):
             ro = self._rollout(num_episodes)
             scores = ro.scores
             scores_episode += scores
-            x, acts, logp_old = self._update_inputs(ro)
+            upd = self._update_state(ro)
             for epoch in range(n_epoch):
-                ploss_agents, value_loss = self._epoch(ro, x, acts, logp_old)
+                ploss_agents, value_loss = self._update_epoch(ro, upd)
                 policy_loss_list.append(ploss_agents)
                 value_loss_list.append(value_loss)
                 if iter % test_freq == 0:

@@ -214,6 +214,28 @@ class iPPO(BatchedLearnerBase):
         self.value_optimizer.step()
         return policy_loss.detach(), value_loss.detach()
 
+    def _epoch_fused(self, ro, cliprange=0.1, beta=0.01):
+        """The same epoch on the fused HIP update kernels: gradients of every agent's policy loss
+        and value loss straight from the rollout buffers, written into .grad; Adam in torch."""
+        from d2dhip.update import actor_grads, critic_grads
+        pp, vp = self.policy.params, self.value.params
+        kind = "comb" if self.combinatorial else "chsel"
+        B = ro.T * ro.E
+        _, sa = actor_grads({k: v.data for k, v in pp.items()}, ro.obs, ro.actions, ro.logp.permute(0, 2, 1),
+                            ro.adv, kind, clip=cliprange, beta=beta, grads=self._grad_buffers(pp))
+        self._reduce_grads(self.policy.parameters())
+        self.policy_optimizer.step()
+        _, sv = critic_grads({k: v.data for k, v in vp.items()}, ro.obs, ro.ret, grads=self._grad_buffers(vp))
+        self._reduce_grads(self.value.parameters())
+        self.value_optimizer.step()
+        return -(sa[:, 0] + beta * sa[:, 1]) / B, sv[:, 0] / B
+
+    def _update_epoch(self, ro, upd):
+        if upd is None:
+            return self._epoch_fused(ro)
+        x, acts, logp_old = upd
+        return self._epoch(x, acts, logp_old, ro.adv, ro.ret)
+
     def train(self, num_iter, n_epoch=4, num_episodes=4, test_freq=100):
         scores_episode = []
         score_test_list = []
@@ -223,9 +245,9 @@ class iPPO(BatchedLearnerBase):
             ro = self._rollout(num_episodes)
             scores = ro.scores
             scores_episode += scores
-            x, acts, logp_old = self._update_inputs(ro)
+            upd = self._update_state(ro)
             for epoch in range(n_epoch):
-                pl, vl = self._epoch(x, acts, logp_old, ro.adv, ro.ret)
+                pl, vl = self._update_epoch(ro, upd)
                 # the reference appends the losses of the last agent of its loop (ippo.py:425-426)
                 policy_loss_list.append(pl[-1].item())
                 value_loss_list.append(vl[-1].item())

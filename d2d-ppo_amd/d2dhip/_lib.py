@@ -70,6 +70,12 @@ _SIGS = {
     "d2d_set_option": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),
     "d2d_policy_mlp_step": (ctypes.c_int, [ctypes.POINTER(MlpDesc), _p, _p, ctypes.c_uint32, ctypes.c_int32, _p, _p,
                                             _p, _p]),
+    "d2d_ppo_workspace": (ctypes.c_int64, [ctypes.c_int32] * 6),
+    "d2d_ppo_actor_grad": (ctypes.c_int, [ctypes.POINTER(MlpDesc), ctypes.c_int32, _p, _p, _p, _p, _p, _p,
+                                           ctypes.c_float, ctypes.c_float, ctypes.c_float, _p, _p, _p, _p, _p, _p,
+                                           ctypes.c_int64, _p]),
+    "d2d_ppo_critic_grad": (ctypes.c_int, [ctypes.POINTER(MlpDesc), ctypes.c_int32, _p, _p, _p, ctypes.c_float,
+                                            _p, _p, _p, _p, _p, _p, ctypes.c_int64, _p]),
     "d2d_last_error": (ctypes.c_char_p, []),
     "d2d_abi_version": (ctypes.c_int, []),
 }

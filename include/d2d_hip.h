@@ -177,6 +177,33 @@ typedef struct d2d_mlp_desc {
 int d2d_policy_mlp_step(const d2d_mlp_desc* desc, const float* obs, const void* forced, uint32_t rng_step,
                         int32_t deterministic, void* actions, float* logp, float* value, void* stream);
 
+/* ---- fused PPO update: per-agent gradients of the MLP learners' losses ----
+ * Replaces evaluate() + loss + backward() of PPO.train_step for every agent at once
+ * (algorithms/ippo.py:178-217; d2d_ppo.py:183-216): the actor loss
+ *   L_k = -mean_s min(r W, clamp(r, 1-clip, 1+clip) W) - beta * mean_s entropy,
+ *   r = exp(logp(a_s) - logp_old_s),  W = advantage (iPPO) or M (D2D chain),
+ * and the critic loss mean_s (V(x_s) - R_s)^2 (ippo.py:210-216).  "mean" is `scale` * sum over
+ * the T * n_envs samples of this call (scale = 1/B; for data-parallel shards 1/B_local, the
+ * caller averages across ranks).  Samples are the rollout slots t < T of envs e < n_envs:
+ *   obs      [T][n_envs][N][F] fp32 (the rollout buffer the env kernel writes),
+ *   actions  [T][n_envs][N] channel masks (kind 0) / uint8 ids (kind 1),
+ *   logp_old, weight, returns: element (t, e, k) at t*s[0] + e*s[1] + k*s[2] (strides in floats).
+ * Network: the d2d_mlp_desc weights (actor w1, b1, w2, b2; critic: its v1, c1, v2, c2 passed as
+ * w1, b1, w2, b2 with n_out ignored).  Outputs (overwritten, agent-stacked like the weights):
+ * gw1 [N][H][F], gb1 [N][H], gw2 [N][A][H], gb2 [N][A]; stats [N][2] = (sum_s min(...),
+ * sum_s entropy) for the actor, (sum_s (V - R)^2, 0) for the critic (NULL = not wanted).
+ * workspace: d2d_ppo_workspace(...) floats of device scratch.  Deterministic (fixed-order sums). */
+int64_t d2d_ppo_workspace(int32_t n_agents, int32_t T, int32_t n_envs, int32_t obs_dim, int32_t hidden,
+                          int32_t n_out);
+int d2d_ppo_actor_grad(const d2d_mlp_desc* desc, int32_t T, const float* obs, const void* actions,
+                       const float* logp_old, const int64_t* logp_strides, const float* weight,
+                       const int64_t* weight_strides, float clip, float beta, float scale, float* gw1, float* gb1,
+                       float* gw2, float* gb2, float* stats, float* workspace, int64_t workspace_floats,
+                       void* stream);
+int d2d_ppo_critic_grad(const d2d_mlp_desc* desc, int32_t T, const float* obs, const float* returns,
+                        const int64_t* return_strides, float scale, float* gw1, float* gb1, float* gw2, float* gb2,
+                        float* stats, float* workspace, int64_t workspace_floats, void* stream);
+
 /* Process-wide tuning options (not part of the reference interface).
  * D2D_OPT_NT_STORES: 1 = write obs/state with non-temporal (streaming) stores.
  * D2D_OPT_POLICY_F32_MFMA: 1 = d2d_policy_mlp_step on v_mfma_f32_16x16x4_f32 instead of the

@@ -1,0 +1,306 @@
+"""GPU parity of the fused PPO-update kernels (csrc/update_kernels.hip) against plain torch
+autograd of the same losses (the reference's PPO.train_step: evaluate + clipped surrogate +
+entropy bonus, algorithms/ippo.py:178-217, d2d_ppo.py:198-216; critic MSE ippo.py:210-216),
+run on the CPU in float64 (the exact-math baseline) and float32 (the reference precision).
+
+Tolerance: every gradient tensor within 2e-5 * max|g| (+1e-7) of the float64 result, which
+is the band the torch fp32 gradients themselves land in (asserted alongside), whenever every
+probability is in [1e-4, 1 - 1e-4]; otherwise (samples at torch's eps clamp or with p -> 1,
+where fp32 rounding decides) within 4x torch fp32's own distance to float64.  Loss sums
+within 1e-5 relative.  Inputs: reference initialisation (orthogonal, gain 2), env-like
+integer observations (the bf16-exact path) or fractional ones (the six-term split path),
+ratios spread over and beyond the clip range, ragged env counts (E not a multiple of 32),
+heterogeneous observation widths (zero-padded columns must get exactly zero gradient)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def make_nets(N, F, H, A, in_dims, seed, critic):
+    from algorithms._core import Policy, StackedNets, Value
+    torch.manual_seed(seed)
+    dims = in_dims or [F] * N
+    if critic:
+        st = StackedNets([Value(d, H) for d in dims], dims, "mlp", "cpu")
+    else:
+        st = StackedNets([Policy(d, A, H) for d in dims], dims, "mlp", "cpu", act="softmax")
+    return {k: v.detach().clone() for k, v in st.params.items()}, dims
+
+
+def make_obs(T, E, N, F, dims, seed, frac):
+    g = torch.Generator().manual_seed(seed)
+    obs = torch.zeros(T, E, N, F)
+    D = max(1, F // 3)
+    obs[..., :D] = torch.randint(0, 4, (T, E, N, D), generator=g).float()
+    obs[..., D:] = torch.randint(-1, 2, (T, E, N, F - D), generator=g).float()
+    if frac:
+        obs += torch.rand(obs.shape, generator=g) * 0.4
+    for k, d in enumerate(dims):
+        obs[:, :, k, d:] = 0
+    return obs
+
+
+def forward_probs(net, x):
+    """x [N][B][F] -> softmax probs [N][B][A] (Policy.forward, ippo.py:69-75)."""
+    h = torch.relu(torch.baddbmm(net["b1"].unsqueeze(1), x, net["w1"].transpose(1, 2)))
+    return torch.softmax(torch.baddbmm(net["b2"].unsqueeze(1), h, net["w2"].transpose(1, 2)), -1)
+
+
+def ref_actor(net, obs, acts_f, logp_old, W, kind, clip, beta, dtype):
+    from torch.distributions import Bernoulli, Categorical
+    p = {k: v.to(dtype).clone().requires_grad_() for k, v in net.items()}
+    T, E, N, F = obs.shape
+    x = obs.to(dtype).permute(2, 0, 1, 3).reshape(N, T * E, F)
+    probs = forward_probs(p, x)
+    if kind == "comb":
+        d = Bernoulli(probs=probs, validate_args=False)
+        logp = d.log_prob(acts_f.to(dtype)).mean(-1)
+        ent = d.entropy().mean(-1)
+    else:
+        d = Categorical(probs=probs, validate_args=False)
+        logp = d.log_prob(acts_f)
+        ent = d.entropy()
+    ratio = torch.exp(logp - logp_old.to(dtype))
+    Wd = W.to(dtype)
+    s = torch.min(ratio * Wd, torch.clamp(ratio, 1 - clip, 1 + clip) * Wd)
+    loss = -s.mean(1) - beta * ent.mean(1)
+    loss.sum().backward()
+    return {k: v.grad for k, v in p.items()}, s.sum(1), ent.sum(1), logp.detach()
+
+
+def ref_critic(net, obs, R, dtype):
+    p = {k: v.to(dtype).clone().requires_grad_() for k, v in net.items()}
+    T, E, N, F = obs.shape
+    x = obs.to(dtype).permute(2, 0, 1, 3).reshape(N, T * E, F)
+    h = torch.relu(torch.baddbmm(p["b1"].unsqueeze(1), x, p["w1"].transpose(1, 2)))
+    v = torch.baddbmm(p["b2"].unsqueeze(1), h, p["w2"].transpose(1, 2))[..., 0]
+    loss = ((v - R.to(dtype)) ** 2).mean(1)
+    loss.sum().backward()
+    return {k: v.grad for k, v in p.items()}, ((v - R.to(dtype)) ** 2).sum(1)
+
+
+def conditioned(probs, lo=1e-4):
+    """Every probability of every sample away from torch's eps clamp and from 1: there the
+    float64 gradient is the exact-math baseline.  Near the clamp (p ~ 1.2e-7, where the
+    gradient jumps between ~1 and 0) or near p -> 1 (1 - p loses its digits in fp32) both
+    fp32 implementations follow their own rounding, so only the fp32 comparison is made."""
+    return bool(probs.min() > lo and probs.max() < 1 - lo)
+
+
+def assert_grads(got, ref64, ref32, dims, F, well_conditioned=True):
+    for name in ref64:
+        g = got[name].cpu().double()
+        r = ref64[name]
+        scale = r.abs().max().item()
+        err64 = (g - r).abs().max().item()
+        err32 = (g - ref32[name].double()).abs().max().item()
+        band = (ref32[name].double() - r).abs().max().item()   # torch fp32's own error
+        print(f"  {name}: max|g| {scale:.3e}  |kernel-f64| {err64:.2e}  |kernel-f32| {err32:.2e}  "
+              f"|torchf32-f64| {band:.2e}")
+        if well_conditioned:
+            tol = 2e-5 * scale + 1e-7
+            assert band <= tol, (name, "fp32 torch outside the band", band, tol)
+            assert err64 <= tol, (name, err64, tol)
+        else:
+            # ill-conditioned samples: the kernel stays within a few times torch fp32's own error
+            tol = max(4 * band, 2e-5 * scale) + 1e-7
+            assert err64 <= tol, (name, err64, tol)
+    if dims is not None:  # padded input columns: exactly zero
+        for k, d in enumerate(dims):
+            assert torch.all(got["w1"][k, :, d:] == 0)
+
+
+CASES = [
+    # kind, N, T, E, F, H, A, in_dims, frac
+    ("comb", 4, 3, 100, 30, 64, 8, None, False),
+    ("comb", 7, 2, 64, 30, 64, 8, [23, 30, 23, 30, 23, 30, 30], False),
+    ("comb", 3, 2, 45, 46, 32, 16, None, True),
+    ("comb", 2, 4, 33, 10, 20, 3, None, False),
+    ("chsel", 3, 3, 70, 12, 64, 5, None, True),
+    ("chsel", 5, 2, 96, 24, 64, 16, [24, 20, 24, 21, 24], False),
+    ("chsel", 2, 1, 17, 40, 48, 9, None, True),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[f"{c[0]}-N{c[1]}-T{c[2]}-E{c[3]}-F{c[4]}-H{c[5]}-A{c[6]}"
+                                              f"{'-het' if c[7] else ''}{'-frac' if c[8] else ''}" for c in CASES])
+def test_actor_grad_matches_autograd(case):
+    from d2dhip.envbatch import pack_masks_torch
+    from d2dhip.update import actor_grads
+    kind, N, T, E, F, H, A, dims, frac = case
+    net, dims_ = make_nets(N, F, H, A, dims, seed=3, critic=False)
+    obs = make_obs(T, E, N, F, dims_, seed=5, frac=frac)
+    g = torch.Generator().manual_seed(9)
+    B = T * E
+    if kind == "comb":
+        acts_f = (torch.rand(N, B, A, generator=g) < 0.4).float()
+        masks = pack_masks_torch(acts_f.view(N, T, E, A).permute(1, 2, 0, 3).contiguous())  # [T][E][N]
+        acts_dev = masks
+    else:
+        acts_f = torch.randint(0, A, (N, B), generator=g)
+        acts_dev = acts_f.view(N, T, E).permute(1, 2, 0).to(torch.uint8).contiguous()
+    with torch.no_grad():
+        x = obs.permute(2, 0, 1, 3).reshape(N, B, F).double()
+        probs = forward_probs({k: v.double() for k, v in net.items()}, x)
+        if kind == "comb":
+            lp = torch.distributions.Bernoulli(probs=probs).log_prob(acts_f.double()).mean(-1)
+        else:
+            lp = torch.distributions.Categorical(probs=probs).log_prob(acts_f)
+    # ratios spread over [0.7, 1.35]: inside and on both sides of the clip range
+    logp_old = (lp + (torch.rand(N, B, generator=g) * 0.6 - 0.3)).float()
+    W = torch.randn(N, B, generator=g)
+    clip, beta = 0.1, 0.05
+    r64, s64, e64, _ = ref_actor(net, obs, acts_f, logp_old, W, kind, clip, beta, torch.float64)
+    r32, s32, e32, _ = ref_actor(net, obs, acts_f, logp_old, W, kind, clip, beta, torch.float32)
+    dev = "cuda"
+    netd = {k: v.to(dev).contiguous() for k, v in net.items()}
+    # logp_old in the rollout layout [T][E][N]; W in the learners' env-major [N][E*T] layout
+    lo_te = logp_old.view(N, T, E).permute(1, 2, 0).contiguous().to(dev)
+    W_env_major = W.view(N, T, E).permute(0, 2, 1).reshape(N, E * T).contiguous().to(dev)
+    grads, stats = actor_grads(netd, obs.to(dev).contiguous(), acts_dev.to(dev), lo_te, W_env_major, kind,
+                               clip=clip, beta=beta)
+    torch.cuda.synchronize()
+    well = conditioned(probs)
+    assert_grads(grads, r64, r32, dims, F, well)
+    st = stats.cpu().double()
+    # loss sums: vs float64 when well conditioned, else vs torch fp32 (log(1 - p) for p -> 1)
+    s_ref, e_ref = (s64, e64) if well else (s32.double(), e32.double())
+    assert torch.allclose(st[:, 0], s_ref, rtol=1e-5, atol=1e-4), (st[:, 0], s_ref)
+    assert torch.allclose(st[:, 1], e_ref, rtol=1e-5, atol=1e-4), (st[:, 1], e_ref)
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[0] == "comb"],
+                         ids=lambda c: f"N{c[1]}-T{c[2]}-E{c[3]}-F{c[4]}-H{c[5]}{'-frac' if c[8] else ''}")
+def test_critic_grad_matches_autograd(case):
+    from d2dhip.update import critic_grads
+    _, N, T, E, F, H, _, dims, frac = case
+    net, dims_ = make_nets(N, F, H, 1, dims, seed=4, critic=True)
+    obs = make_obs(T, E, N, F, dims_, seed=6, frac=frac)
+    g = torch.Generator().manual_seed(2)
+    R = torch.randn(N, T * E, generator=g)
+    r64, l64 = ref_critic(net, obs, R, torch.float64)
+    r32, _ = ref_critic(net, obs, R, torch.float32)
+    dev = "cuda"
+    netd = {k: v.to(dev).contiguous() for k, v in net.items()}
+    R_te = R.view(N, T, E).permute(1, 2, 0).contiguous().to(dev)   # [T][E][N] (GAE output layout)
+    grads, stats = critic_grads(netd, obs.to(dev).contiguous(), R_te)
+    torch.cuda.synchronize()
+    assert_grads(grads, r64, r32, dims, F)
+    assert torch.allclose(stats.cpu().double()[:, 0], l64, rtol=1e-5, atol=1e-4)
+
+
+def test_update_deterministic_and_large():
+    """64 x 8 at 256 envs x 20 slots: bitwise-identical on repeat; fp32-band vs float64 autograd."""
+    from d2dhip.envbatch import pack_masks_torch
+    from d2dhip.update import actor_grads
+    N, T, E, F, H, A = 64, 20, 256, 30, 64, 8
+    net, dims = make_nets(N, F, H, A, None, seed=1, critic=False)
+    obs = make_obs(T, E, N, F, dims, seed=2, frac=False)
+    g = torch.Generator().manual_seed(3)
+    B = T * E
+    acts_f = (torch.rand(N, B, A, generator=g) < 0.3).float()
+    masks = pack_masks_torch(acts_f.view(N, T, E, A).permute(1, 2, 0, 3).contiguous())
+    logp_old = -torch.rand(N, B, generator=g) * 3
+    W = torch.randn(N, B, generator=g)
+    r64, _, _, _ = ref_actor(net, obs, acts_f, logp_old, W, "comb", 0.1, 0.01, torch.float64)
+    r32, _, _, _ = ref_actor(net, obs, acts_f, logp_old, W, "comb", 0.1, 0.01, torch.float32)
+    with torch.no_grad():
+        probs = forward_probs({k: v.double() for k, v in net.items()}, obs.permute(2, 0, 1, 3).reshape(N, B, F).double())
+    dev = "cuda"
+    netd = {k: v.to(dev).contiguous() for k, v in net.items()}
+    # [N][T*E] time-major -> strided [T][E][N] views (no copy: the kernel takes element strides)
+    lo_v = logp_old.to(dev).view(N, T, E).permute(1, 2, 0)
+    W_v = W.to(dev).view(N, T, E).permute(1, 2, 0)
+    args = (netd, obs.to(dev).contiguous(), masks.to(dev), lo_v, W_v, "comb")
+    g1, s1 = actor_grads(*args)
+    g1 = {k: v.clone() for k, v in g1.items()}
+    s1 = s1.clone()
+    g2, s2 = actor_grads(*args)
+    torch.cuda.synchronize()
+    for k in g1:
+        assert torch.equal(g1[k], g2[k])
+    assert torch.equal(s1, s2)
+    assert_grads(g1, r64, r32, None, F, conditioned(probs))
+
+
+def test_update_rejects_bad_shapes():
+    from d2dhip.update import actor_grads
+    N, T, E, F, H, A = 2, 1, 8, 70, 16, 4   # F + 1 > 64
+    net = {"w1": torch.zeros(N, H, F, device="cuda"), "b1": torch.zeros(N, H, device="cuda"),
+           "w2": torch.zeros(N, A, H, device="cuda"), "b2": torch.zeros(N, A, device="cuda")}
+    obs = torch.zeros(T, E, N, F, device="cuda")
+    acts = torch.zeros(T, E, N, dtype=torch.uint8, device="cuda")
+    lo = torch.zeros(T, E, N, device="cuda")
+    with pytest.raises(NotImplementedError):
+        actor_grads(net, obs, acts, lo, lo, "comb")
+
+
+def _learner_pair(cls, kind, seed=0, E=96):
+    """Two identical learners (same init, same rollout) on a small batched env."""
+    import copy
+    import json
+    import os
+    from envs.combinatorial_env import CombinatorialEnv
+    from envs.channel_selection_env import ChannelSelectionEnv
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    N = 6
+    if kind == "comb":
+        cs8 = np.array(json.load(open(os.path.join(root, "d2d-ppo_amd", "combinatorial_load",
+                                                   "channel_switch_8.json")))["__nd__"])
+        params = dict(n_agents=N, n_channels=8, deadlines=np.array([7, 14] * 3), lbdas=np.full(N, 0.5),
+                      period=np.full(N, 2), arrival_probs=np.resize(np.array([.2, .4, .8, 1, 1, 1]), N),
+                      offsets=np.zeros(N), episode_length=40, traffic_model="heterogeneous",
+                      homogeneous_size=False, periodic_devices=[0, 1, 2], channel_switch=np.resize(cs8, (N, 8)))
+        make_env = lambda: CombinatorialEnv(**params, n_envs=E, device="cuda", seed=seed)  # noqa: E731
+    else:
+        params = dict(n_agents=N, n_channels=4, deadlines=np.array([7] * N), lbdas=np.full(N, 1 / 3.5),
+                      period=np.full(N, 2), arrival_probs=np.full(N, 0.5), offsets=np.zeros(N),
+                      episode_length=40, traffic_model="aperiodic", periodic_devices=[],
+                      channel_switch=np.full(5, 0.8))
+        make_env = lambda: ChannelSelectionEnv(**params, n_envs=E, device="cuda", seed=seed)  # noqa: E731
+    out = []
+    for _ in range(2):
+        torch.manual_seed(seed)
+        env = make_env()
+        kw = dict(hidden_size=64, gamma=0.6, policy_lr=3e-3, value_lr=1e-3, device="cuda", useRNN=False,
+                  combinatorial=kind == "comb")
+        lr = cls(env, beta_entropy=0.05, **kw) if cls.__name__ == "D2DPPO" else cls(env, **kw)
+        out.append(lr)
+    torch.manual_seed(seed + 1)
+    ro = out[0]._rollout(E)
+    return out, ro, copy
+
+
+@pytest.mark.parametrize("kind", ["comb", "chsel"])
+@pytest.mark.parametrize("algo", ["ippo", "d2d"])
+def test_fused_epoch_matches_torch_epoch(kind, algo):
+    """One learner epoch on the fused kernels == the torch agent-stacked epoch (same rollout, same
+    permutation): losses 1e-5; post-Adam weights within 2% of the learning rate.  Adam's first
+    steps are lr * g / (|g| + 1e-8): sign-like, so elements whose gradient is ~1e-8 move by a
+    lr-sized amount that fp32-level gradient differences can change by a few 1e-3 of lr."""
+    from algorithms.d2d_ppo import D2DPPO
+    from algorithms.ippo import iPPO
+    cls = iPPO if algo == "ippo" else D2DPPO
+    (fused, ref), ro, _ = _learner_pair(cls, kind)
+    assert fused._fused_update_ok()
+    upd = ref._update_inputs(ro)
+    for ep in range(2):
+        np.random.seed(100 + ep)
+        a = fused._update_epoch(ro, None)
+        np.random.seed(100 + ep)
+        b = ref._update_epoch(ro, upd)
+        if algo == "ippo":
+            assert torch.allclose(a[0], b[0], atol=1e-5), (a[0], b[0])
+            assert torch.allclose(a[1], b[1], rtol=1e-5, atol=1e-5), (a[1], b[1])
+        else:
+            assert np.allclose(a[0], b[0], atol=1e-5), (a[0], b[0])
+            assert abs(float(a[1]) - float(b[1])) < 1e-5
+        nets = [(fused.policy.params, ref.policy.params, 3e-3)]
+        if algo == "ippo":
+            nets.append((fused.value.params, ref.value.params, 1e-3))
+        for pf, pr, lr in nets:
+            for k in pf:
+                err = (pf[k].data - pr[k].data).abs().max().item()
+                assert err < 0.02 * lr, (ep, k, err)
