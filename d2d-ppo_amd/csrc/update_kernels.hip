@@ -95,37 +95,61 @@ __device__ __forceinline__ float ld_st(const float* base, const int64_t (&st)[3]
   return base[(int64_t)t * st[0] + (int64_t)e * st[1] + (int64_t)k * st[2]];
 }
 
-// Layer-1 operand of one 16-sample half: lane (g, i) <- x[sample e][32c + 8g + j], bias 1 at
-// column F, 0 past it and for samples past E.
-template <int KC>
-__device__ __forceinline__ void load_x_rows(float (&x)[KC][8], const UpdArgs& a, int t, int e, bool ok, int k, int g) {
-  const float* row = a.obs + ((size_t)((size_t)t * a.E + (ok ? e : 0)) * a.N + k) * a.F;
-  const int F = a.F;
-#pragma unroll
-  for (int c = 0; c < KC; ++c)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int col = 32 * c + 8 * g + j;
-      const float v = row[min(col, F - 1)];
-      x[c][j] = !ok ? 0.f : col < F ? v : col == F ? 1.f : 0.f;
-    }
-}
+// Per-tile inputs of the actor kernel, loaded one tile ahead (registers): the obs rows of the
+// 32 samples (lane (g, i) of half s: x[sample 16s + i][32c + 8g + j], raw -- columns past F and
+// samples past E are fixed up by stage_tile) and the per-sample action / logp_old / weight of
+// the epilogue lanes (PAIR: lane (g, i) serves sample 16 (g >> 1) + i; else sample 16s + i).
+template <int KC, bool PAIR>
+struct ActorIn {
+  float x[2][KC][8];
+  uint32_t act[PAIR ? 1 : 2];
+  float lo[PAIR ? 1 : 2], w[PAIR ? 1 : 2];
+};
 
-// Sample-on-k operand of dW1 = dH^T . X for input tile q (inputs 16q .. 16q+15): lane (g, i)
-// slot j <- x[sample 16(j >> 2) + 4g + (j & 3)][16q + i] (the row order of the dH accumulator).
-__device__ __forceinline__ void load_x_cols(float (&x)[8], const UpdArgs& a, int t, int e0, int k, int g, int i, int q) {
-  const int F = a.F, col = 16 * q + i;
-  const int cc = min(col, F - 1);
+// obs rows of one tile through a range-checked buffer descriptor based at the tile's first row
+// (rows of samples past E, or past the buffer, read as 0)
+template <int KC>
+__device__ __forceinline__ void load_rows(float (&x)[2][KC][8], const UpdArgs& a, int t, int e0, int k, int g,
+                                          int i) {
+  const size_t row0 = ((size_t)t * a.E + e0) * a.N + k;
+  const int64_t rest = ((int64_t)a.T * a.E * a.N - (int64_t)row0) * a.F * 4;
+  const uint32_t nbytes = rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.obs + row0 * a.F), 0, nbytes, 0x00020000);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int e = e0 + 16 * (j >> 2) + 4 * g + (j & 3);
-    const bool ok = e < a.E;
-    const float v = a.obs[((size_t)((size_t)t * a.E + (ok ? e : 0)) * a.N + k) * F + cc];
-    x[j] = !ok ? 0.f : col < F ? v : col == F ? 1.f : 0.f;
+  for (int s = 0; s < 2; ++s) {
+    const int e = e0 + 16 * s + i;
+    const uint32_t vo = e < a.E ? ((uint32_t)((16 * s + i) * a.N * a.F) + 8 * g) * 4 : 0x80000000u;
+#pragma unroll
+    for (int c = 0; c < KC; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[s][c][j] = uf(__builtin_amdgcn_raw_buffer_load_b32(rsrc, vo + 4 * (32 * c + j), 0, 0));
   }
 }
 
-// dL/dz for one 16-sample half (lane (g, i): sample e, actions 4g + r), plus loss sums.
+__device__ __forceinline__ uint32_t load_action(const UpdArgs& a, int t, int e, int k) {
+  const size_t cell = ((size_t)t * a.E + e) * a.N + k;
+  if (a.kind == 1) return reinterpret_cast<const unsigned char*>(a.actions)[cell];
+  return load_mask(a.actions, cell, a.mask_bytes);
+}
+
+template <int KC, bool PAIR>
+__device__ __forceinline__ void load_actor_in(ActorIn<KC, PAIR>& in, const UpdArgs& a, int tile, int k, int g, int i) {
+  const int t = tile / a.tiles_per_t;
+  const int e0 = (tile - t * a.tiles_per_t) * 32;
+  load_rows<KC>(in.x, a, t, e0, k, g, i);
+#pragma unroll
+  for (int s = 0; s < (PAIR ? 1 : 2); ++s) {
+    const int e = e0 + 16 * (PAIR ? (g >> 1) : s) + i;
+    const int ec = e < a.E ? e : a.E - 1;
+    in.act[s] = load_action(a, t, ec, k);
+    in.lo[s] = ld_st(a.logp_old, a.lo_st, t, ec, k);
+    in.w[s] = ld_st(a.weight, a.w_st, t, ec, k);
+  }
+}
+
+// dL/dz for one epilogue pass.  Lane (g, i): sample i of its half, actions 4 ga + r (HALF: the
+// two 32-lane halves are independent tiles, ga = g & 1; else ga = g).
 // Bernoulli (KIND 0, ippo.py:157-160 + 185-189, quirk Q6: softmax probs as Bernoulli probs):
 //   logp = mean_c log_prob(a_c) with torch's clamp(p, eps, 1-eps); entropy = mean_c
 //   BCEWithLogits(logit(pc), p) = -p log pc - (1-p) log(1-pc).
@@ -133,41 +157,34 @@ __device__ __forceinline__ void load_x_cols(float (&x)[8], const UpdArgs& a, int
 //   entropy = -sum q log clamp(q).
 // Surrogate -min(r W, clamp(r) W) with torch.min's tie rule (each side gets half the gradient,
 // so inside [1-eps, 1+eps] the slope is r W) and clamp passing the gradient inclusively.
-template <int KIND>
-__device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, int t, int e, bool ok, int k, int g,
+template <int KIND, bool HALF>
+__device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, uint32_t act, float lo, float W, bool ok, int ga,
                                         float& surr_acc, float& ent_acc) {
   const int A = a.A;
   bool valid[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) valid[r] = 4 * g + r < A;
+  for (int r = 0; r < 4; ++r) valid[r] = 4 * ga + r < A;
   float mx = -INFINITY;
 #pragma unroll
   for (int r = 0; r < 4; ++r)
     if (valid[r]) mx = fmaxf(mx, z[r]);
-  mx = group_max(mx);
+  mx = group_max<HALF>(mx);
   float ex[4], sum = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     ex[r] = valid[r] ? __expf(z[r] - mx) : 0.f;
     sum += ex[r];
   }
-  sum = group_sum(sum);
+  sum = group_sum<HALF>(sum);
   const float inv = 1.f / sum;
   float p[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) p[r] = ex[r] * inv;
-
-  const size_t cell = ((size_t)t * a.E + (ok ? e : 0)) * a.N + k;
-  const float lo = ok ? ld_st(a.logp_old, a.lo_st, t, e, k) : 0.f;
-  const float W = ok ? ld_st(a.weight, a.w_st, t, e, k) : 0.f;
-  float gr[4];
+  float gr[4], dsur[4];
   float logp, ent;
-  // per-action pieces that scale with the surrogate coefficient (known after logp)
-  float dsur[4];
   if constexpr (KIND == 0) {
-    const uint32_t bits = ok ? (load_mask(a.actions, cell, a.mask_bytes) >> (4 * g)) : 0u;
-    float lsum = 0.f, esum = 0.f;
-    float logit[4];
+    const uint32_t bits = act >> (4 * ga);
+    float lsum = 0.f, esum = 0.f, logit[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float pc = fminf(fmaxf(p[r], kEps), 1.f - kEps);
@@ -179,8 +196,8 @@ __device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, int t, int e,
       logit[r] = l1 - l0;
       dsur[r] = (valid[r] && inside) ? (bit ? 1.f / pc : -1.f / (1.f - pc)) : 0.f;
     }
-    logp = group_sum(lsum) * a.inv_A;
-    ent = group_sum(esum) * a.inv_A;
+    logp = group_sum<HALF>(lsum) * a.inv_A;
+    ent = group_sum<HALF>(esum) * a.inv_A;
     const float ratio = __expf(logp - lo);
     const float cr = fminf(fmaxf(ratio, a.clip_lo), a.clip_hi);
     const float s1 = ratio * W, s2 = cr * W;
@@ -189,41 +206,41 @@ __device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, int t, int e,
     const float eb = a.beta * a.scale * a.inv_A;  // d(-beta*mean ent)/dp_c = +beta * logit_c / A / B
 #pragma unroll
     for (int r = 0; r < 4; ++r) gr[r] = valid[r] ? coef * dsur[r] + eb * logit[r] : 0.f;
-    if (ok && g == 0) {
+    if (ok && ga == 0) {
       surr_acc += fminf(s1, s2);
       ent_acc += ent;
     }
     float dot = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) dot += p[r] * gr[r];
-    dot = group_sum(dot);
+    dot = group_sum<HALF>(dot);
     f32x4 dz;
 #pragma unroll
     for (int r = 0; r < 4; ++r) dz[r] = (ok && valid[r]) ? p[r] * (gr[r] - dot) : 0.f;
     return dz;
   } else {
-    const int aid = ok ? (int)reinterpret_cast<const unsigned char*>(a.actions)[cell] : -1;
+    const int aid = (int)act;
     float psum = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) psum += p[r];
-    psum = group_sum(psum);
+    psum = group_sum<HALF>(psum);
     const float ipsum = 1.f / psum;
-    float q[4], lq[4], lsel = 0.f, esum = 0.f;
-    bool inside[4];
+    float q[4], lsel = 0.f, esum = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       q[r] = p[r] * ipsum;
       const float qc = fminf(fmaxf(q[r], kEps), 1.f - kEps);
-      inside[r] = q[r] >= kEps && q[r] <= 1.f - kEps;
-      lq[r] = __logf(qc);
-      lsel += (valid[r] && 4 * g + r == aid) ? lq[r] : 0.f;
-      esum += valid[r] ? q[r] * lq[r] : 0.f;
-      dsur[r] = (valid[r] && inside[r] && 4 * g + r == aid) ? 1.f / qc : 0.f;
+      const bool inside = q[r] >= kEps && q[r] <= 1.f - kEps;
+      const float lq = __logf(qc);
+      const bool chosen = valid[r] && 4 * ga + r == aid;
+      lsel += chosen ? lq : 0.f;
+      esum += valid[r] ? q[r] * lq : 0.f;
+      dsur[r] = (chosen && inside) ? 1.f / qc : 0.f;
       // d(-beta * ent)/dq = beta * (log qc + q * [inside] / qc)
-      gr[r] = valid[r] ? (lq[r] + (inside[r] ? q[r] / qc : 0.f)) : 0.f;
+      gr[r] = valid[r] ? (lq + (inside ? q[r] / qc : 0.f)) : 0.f;
     }
-    logp = group_sum(lsel);
-    ent = -group_sum(esum);
+    logp = group_sum<HALF>(lsel);
+    ent = -group_sum<HALF>(esum);
     const float ratio = __expf(logp - lo);
     const float cr = fminf(fmaxf(ratio, a.clip_lo), a.clip_hi);
     const float s1 = ratio * W, s2 = cr * W;
@@ -236,15 +253,15 @@ __device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, int t, int e,
       gr[r] = coef * dsur[r] + eb * gr[r];  // dL/dq
       gq += gr[r] * q[r];
     }
-    gq = group_sum(gq);
+    gq = group_sum<HALF>(gq);
     float dp[4], dot = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       dp[r] = valid[r] ? (gr[r] - gq) * ipsum : 0.f;  // through q = p / sum p
       dot += p[r] * dp[r];
     }
-    dot = group_sum(dot);
-    if (ok && g == 0) {
+    dot = group_sum<HALF>(dot);
+    if (ok && ga == 0) {
       surr_acc += fminf(s1, s2);
       ent_acc += ent;
     }
@@ -273,11 +290,30 @@ __device__ __forceinline__ void reduce_waves(float (&acc)[NV], float* red, int w
   }
 }
 
+template <int XS>
+__device__ __forceinline__ void lds_row(float (&v)[8], const float (*xw)[XS], int row, int col) {
+  const f32x4 p = *reinterpret_cast<const f32x4*>(&xw[row][col]), q = *reinterpret_cast<const f32x4*>(&xw[row][col + 4]);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[j] = p[j];
+    v[4 + j] = q[j];
+  }
+}
+
+__device__ __forceinline__ void lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // ------------------------------------------------------------------------- actor gradients
-// KC = input chunks of 32 (F + 1 <= 32 KC), HT = hidden tiles of 16 (H <= 16 HT, even), A <= 16.
-template <int KC, int HT, int KIND>
-__global__ __launch_bounds__(256) void ppo_actor_grad_kernel(UpdArgs a) {
-  static_assert(HT % 2 == 0, "layer 2 consumes hidden tiles in pairs");
+// KC = input chunks of 32 (F + 1 <= 32 KC), HT = hidden tiles of 16 (H <= 16 HT), A <= 16;
+// PAIR (A <= 8): one epilogue pass serves both halves (lanes 0-31 half 0, 32-63 half 1).
+// Products: layer 1 (both orientations), dH and dW1 on the exact bf16 split (the weight splits
+// are made once; x is bf16-exact on env observations, so 3 MFMAs per 16x16x32); the logits and
+// dW2, whose operands would need a split of their own per tile, on v_mfma_f32_16x16x4_f32 (an
+// exact fmaf chain) straight from the accumulator registers.
+template <int KC, int HT, int KIND, bool PAIR>
+__global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(UpdArgs a) {
   constexpr int QT = 2 * KC;  // input tiles of 16 in dW1
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, i = lane & 15;
@@ -285,12 +321,15 @@ __global__ __launch_bounds__(256) void ppo_actor_grad_kernel(UpdArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, A = a.A, F = a.F;
 
-  // ---- weights of agent k
-  Parts w1p[HT][KC], w2p[HT / 2];
-  Parts4 w2b[HT];
+  // ---- weights of agent k: the W1 split in registers; the two W2 operand sets (used once per
+  // half per hidden tile) in LDS, shared by the workgroup's four waves
+  Parts w1p[HT][KC];
   f32x4 b2i;
+  __shared__ __attribute__((aligned(16))) uint32_t w2b_s[HT][3][64][2];  // dH's B operand parts h, m, l
+  __shared__ __attribute__((aligned(16))) float w2f_s[HT][64][4];        // Z^T's fp32 A operand
   {
     const float* W1 = a.w1 + (size_t)k * H * F;
+    const float* W2 = a.w2 + (size_t)k * A * H;
 #pragma unroll
     for (int t = 0; t < HT; ++t) {
       const int hrow = 16 * t + i;
@@ -305,27 +344,31 @@ __global__ __launch_bounds__(256) void ppo_actor_grad_kernel(UpdArgs a) {
         }
         w1p[t][c] = split3(wv);
       }
+    }
+    for (int t = wave; t < HT; t += 4) {
+      const int hrow = 16 * t + i;
+      const bool hok = hrow < H;
       // B operand of dH = dZ . W2: k-slot (g, j < 4) <-> action 4g + j, column = hidden 16t + i
       float wb[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int act = 4 * g + j;
-        wb[j] = (hok && act < A) ? a.w2[((size_t)k * A + act) * H + hrow] : 0.f;
-      }
-      w2b[t] = split3_4(wb);
-    }
+      for (int j = 0; j < 4; ++j) wb[j] = (hok && 4 * g + j < A) ? W2[(size_t)(4 * g + j) * H + hrow] : 0.f;
+      const Parts4 p4 = split3_4(wb);
 #pragma unroll
-    for (int c2 = 0; c2 < HT / 2; ++c2) {
-      float wv[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int hid = 16 * (2 * c2 + (j >> 2)) + 4 * g + (j & 3);
-        wv[j] = (i < A && hid < H) ? a.w2[((size_t)k * A + i) * H + hid] : 0.f;
+      for (int q = 0; q < 2; ++q) {
+        w2b_s[t][0][lane][q] = p4.h[q];
+        w2b_s[t][1][lane][q] = p4.m[q];
+        w2b_s[t][2][lane][q] = p4.l[q];
       }
-      w2p[c2] = split3(wv);
+      // A operand of Z^T = W2 . relu(HT) (fp32 16x16x4): row = action i, k = hidden 16t + 4g + r
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int hid = 16 * t + 4 * g + r;
+        w2f_s[t][lane][r] = (i < A && hid < H) ? W2[(size_t)i * H + hid] : 0.f;
+      }
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) b2i[r] = 4 * g + r < A ? a.b2[(size_t)k * A + 4 * g + r] : 0.f;
+    __syncthreads();
   }
 
   f32x4 dw1[HT][QT], dw2[HT];
@@ -338,40 +381,55 @@ __global__ __launch_bounds__(256) void ppo_actor_grad_kernel(UpdArgs a) {
   f32x4 db2 = {0.f, 0.f, 0.f, 0.f};
   float surr_acc = 0.f, ent_acc = 0.f;
 
-  __shared__ __attribute__((aligned(16))) float dzt[4][2][16][20];  // per-wave dZ transpose (row stride 20: conflict-light)
-  __shared__ float red[(HT * QT * 4 + HT * 4 + 4 + 2) * 64];
+  // per-wave LDS: the obs tile row-major and the dZ transpose (row stride 20)
+  constexpr int XS = 32 * KC + 4;  // row stride = 4 mod 16 floats: sample-on-k reads hit 64 banks
+  __shared__ __attribute__((aligned(16))) float xs[4][32][XS];
+  __shared__ __attribute__((aligned(16))) float dzt[4][2][16][20];
+  constexpr int NV = HT * QT * 4 + HT * 4 + 4 + 2;
+  __shared__ float red[NV * 64];
+  float(*xw)[XS] = xs[wave];
+  float(*zb)[16][20] = dzt[wave];
 
   const int stride = a.G * 4;
-  for (int tile = blockIdx.y * 4 + wave; tile < a.n_tiles; tile += stride) {
-    const int t = tile / a.tiles_per_t;  // wave-uniform
+  int tile = blockIdx.y * 4 + wave;
+  // one tile of look-ahead: the next tile's loads are issued as soon as this tile's obs are
+  // staged (the registers are reused), so they fly during the whole tile's compute
+  ActorIn<KC, PAIR> in;
+  if (tile < a.n_tiles) load_actor_in<KC, PAIR>(in, a, tile, k, g, i);
+  for (; tile < a.n_tiles; tile += stride) {
+    const int t = tile / a.tiles_per_t;
     const int e0 = (tile - t * a.tiles_per_t) * 32;
-
-    // ---- inputs, sample-on-i (layer 1 A/B operand)
-    bf16x8 xh[2][KC];
-    Parts xp[2][KC];
-    uint32_t low = 0;
-    float xr[2][KC][8];
+    ActorIn<KC, PAIR> cur;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int e = e0 + 16 * s + i;
-      load_x_rows<KC>(xr[s], a, t, e, e < a.E, k, g);
+    for (int s = 0; s < (PAIR ? 1 : 2); ++s) {
+      cur.act[s] = in.act[s];
+      cur.lo[s] = in.lo[s];
+      cur.w[s] = in.w[s];
+    }
+
+    // ---- inputs: bias column, zeros past it; bf16 high parts; the tile to LDS for dW1
+    float xr[2][KC][8];
+    uint32_t low = 0;
+    bf16x8 xh[2][KC];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) low |= fbits(xr[s][c][j]) & 0xFFFFu;
+        for (int j = 0; j < 8; ++j) {
+          const int col = 32 * c + 8 * g + j;
+          xr[s][c][j] = col < F ? in.x[s][c][j] : col == F ? 1.f : 0.f;
+          low |= fbits(xr[s][c][j]) & 0xFFFFu;
+        }
         xh[s][c] = hi_frag(xr[s][c]);
+        *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g]) = f32x4{xr[s][c][0], xr[s][c][1], xr[s][c][2], xr[s][c][3]};
+        *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g + 4]) = f32x4{xr[s][c][4], xr[s][c][5], xr[s][c][6], xr[s][c][7]};
       }
-    }
     const bool x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;  // wave-uniform
-    if (!x_exact) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int c = 0; c < KC; ++c) xp[s][c] = split3(xr[s][c]);
-    }
+    if (tile + stride < a.n_tiles) load_actor_in<KC, PAIR>(in, a, tile + stride, k, g, i);
 
-    // ---- forward (transposed): HT = W1 . X^T, Z^T = W2 . relu(HT) + b2; epilogue -> dZ
-    f32x4 dz[2];
+    // ---- forward (transposed): HT = W1 . X^T (bf16 split), Z^T = W2 . relu(HT) + b2 (fp32)
+    f32x4 zt[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       f32x4 ht[HT];
@@ -384,122 +442,131 @@ __global__ __launch_bounds__(256) void ppo_actor_grad_kernel(UpdArgs a) {
           ht[t2] = mfma_bf16(w1p[t2][c].m, xh[s][c], ht[t2]);
           ht[t2] = mfma_bf16(w1p[t2][c].h, xh[s][c], ht[t2]);
         }
-        if (!x_exact) {
-#pragma unroll
-          for (int c = 0; c < KC; ++c) {
-            ht[t2] = mfma_bf16(w1p[t2][c].h, xp[s][c].l, ht[t2]);
-            ht[t2] = mfma_bf16(w1p[t2][c].m, xp[s][c].m, ht[t2]);
-            ht[t2] = mfma_bf16(w1p[t2][c].h, xp[s][c].m, ht[t2]);
-          }
-        }
       }
-      f32x4 zt = b2i;
-#pragma unroll
-      for (int c2 = 0; c2 < HT / 2; ++c2) {
-        float hv[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          hv[r] = relu(ht[2 * c2][r]);
-          hv[4 + r] = relu(ht[2 * c2 + 1][r]);
-        }
-        zt = mfma_split(w2p[c2], split3(hv), false, zt);
-      }
-      const int e = e0 + 16 * s + i;
-      dz[s] = ppo_dz<KIND>(a, zt, t, e, e < a.E, k, g, surr_acc, ent_acc);
-      db2 += dz[s];
-    }
-
-    // ---- hidden layer again, sample-on-rows: HN = X . W1^T
-    f32x4 hn[2][HT];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int t2 = 0; t2 < HT; ++t2) {
+      if (!x_exact) {  // rare (fractional observations): residual parts, x re-read from LDS
 #pragma unroll
         for (int c = 0; c < KC; ++c) {
-          const f32x4 z0 = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : hn[s][t2];
-          hn[s][t2] = mfma_bf16(xh[s][c], w1p[t2][c].l, z0);
-          hn[s][t2] = mfma_bf16(xh[s][c], w1p[t2][c].m, hn[s][t2]);
-          hn[s][t2] = mfma_bf16(xh[s][c], w1p[t2][c].h, hn[s][t2]);
-        }
-        if (!x_exact) {
+          float xv[8];
+          lds_row(xv, xw, 16 * s + i, 32 * c + 8 * g);
+          const Parts xp = split3(xv);
 #pragma unroll
-          for (int c = 0; c < KC; ++c) {
-            hn[s][t2] = mfma_bf16(xp[s][c].l, w1p[t2][c].h, hn[s][t2]);
-            hn[s][t2] = mfma_bf16(xp[s][c].m, w1p[t2][c].m, hn[s][t2]);
-            hn[s][t2] = mfma_bf16(xp[s][c].m, w1p[t2][c].h, hn[s][t2]);
+          for (int t2 = 0; t2 < HT; ++t2) {
+            ht[t2] = mfma_bf16(w1p[t2][c].h, xp.l, ht[t2]);
+            ht[t2] = mfma_bf16(w1p[t2][c].m, xp.m, ht[t2]);
+            ht[t2] = mfma_bf16(w1p[t2][c].h, xp.m, ht[t2]);
           }
         }
       }
+      f32x4 z = b2i;
+#pragma unroll
+      for (int t2 = 0; t2 < HT; ++t2) {
+        const f32x4 w2f = *reinterpret_cast<const f32x4*>(&w2f_s[t2][lane][0]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) z = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[r], relu(ht[t2][r]), z, 0, 0, 0);
+      }
+      zt[s] = z;
+    }
 
-    // ---- dH = (dZ . W2) * [HN > 0]; the 4 live k-slots of each fragment half carry a second
-    // split part, so the six split terms take three MFMAs
-    f32x4 dh[2][HT];
+    // ---- epilogue -> dZ (lane (g, i): sample 16s + i, actions 4g + r), written transposed to LDS
+    f32x4 dz[2];
+    if constexpr (PAIR) {
+      f32x4 zc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) zc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(zt[0][r]), fu(zt[1][r]), false, false)[0]);
+      const int e = e0 + 16 * (g >> 1) + i;
+      const f32x4 dzc = ppo_dz<KIND, true>(a, zc, cur.act[0], cur.lo[0], cur.w[0], e < a.E, g & 1, surr_acc, ent_acc);
+      db2 += dzc;
+      *reinterpret_cast<f32x4*>(&zb[g >> 1][i][4 * (g & 1)]) = dzc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(fu(dzc[r]), 0u, false, false);
+        dz[0][r] = uf(sw[0]);  // lanes 0-31: half 0's dZ, lanes 32-63: 0
+        dz[1][r] = uf(sw[1]);  // lanes 0-31: half 1's dZ, lanes 32-63: 0
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int e = e0 + 16 * s + i;
+        dz[s] = ppo_dz<KIND, false>(a, zt[s], cur.act[s], cur.lo[s], cur.w[s], e < a.E, g, surr_acc, ent_acc);
+        db2 += dz[s];
+        *reinterpret_cast<f32x4*>(&zb[s][i][4 * g]) = dz[s];
+      }
+    }
+    lds_order();
+
+    // ---- per half s: HN = X . W1^T (sample on rows), dH = (dZ . W2) * [HN > 0],
+    //      dW2^T += relu(HN)^T . dZ  (fp32, k = sample 16s + 4g + r of step r),
+    //      dW1 += dH^T . X (k-slots: dH's 4 samples x two split parts; X sample-on-k from LDS)
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
+      float dzn[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dzn[r] = zb[s][4 * g + r][i];
+      bf16x8 bx1[QT], bx2[QT], bx3[QT];
+#pragma unroll
+      for (int q = 0; q < QT; ++q) {
+        float xc[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xc[r] = xw[16 * s + 4 * g + r][16 * q + i];
+        const Parts4 xq = split3_4(xc);
+        bx1[q] = cat(xq.h, xq.h);  // dH_h x_h + dH_m x_h
+        bx2[q] = cat(xq.m, xq.m);  // dH_h x_m + dH_m x_m   (fractional x only)
+        bx3[q] = cat(xq.l, xq.h);  // dH_h x_l + dH_l x_h
+      }
       const float dv[4] = {dz[s][0], dz[s][1], dz[s][2], dz[s][3]};
       const Parts4 zp = split3_4(dv);
       const bf16x8 a_hm = cat(zp.h, zp.m), a_hl = cat(zp.h, zp.l);
 #pragma unroll
       for (int t2 = 0; t2 < HT; ++t2) {
-        f32x4 acc = mfma_bf16(a_hl, cat(w2b[t2].l, w2b[t2].h), f32x4{0.f, 0.f, 0.f, 0.f});
-        acc = mfma_bf16(a_hm, cat(w2b[t2].m, w2b[t2].h), acc);
-        acc = mfma_bf16(a_hm, cat(w2b[t2].h, w2b[t2].m), acc);
+        f32x4 hn = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[r] = hn[s][t2][r] > 0.f ? acc[r] : 0.f;
-        dh[s][t2] = acc;
-      }
-    }
-
-    // ---- dZ transposed through LDS: lane (g, i) <- dZ[action i][sample 16(j>>2) + 4g + (j&3)]
-    float dzn[8];
-    {
-      float(*buf)[16][20] = dzt[wave];
+        for (int c = 0; c < KC; ++c) {
+          hn = mfma_bf16(xh[s][c], w1p[t2][c].l, hn);
+          hn = mfma_bf16(xh[s][c], w1p[t2][c].m, hn);
+          hn = mfma_bf16(xh[s][c], w1p[t2][c].h, hn);
+        }
+        if (!x_exact) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-        *reinterpret_cast<f32x4*>(&buf[s][i][4 * g]) = dz[s];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+          for (int c = 0; c < KC; ++c) {
+            float xv[8];
+            lds_row(xv, xw, 16 * s + i, 32 * c + 8 * g);
+            const Parts xp = split3(xv);
+            hn = mfma_bf16(xp.l, w1p[t2][c].h, hn);
+            hn = mfma_bf16(xp.m, w1p[t2][c].m, hn);
+            hn = mfma_bf16(xp.m, w1p[t2][c].h, hn);
+          }
+        }
+        // the 4 live k-slots of each fragment half carry a second split part: 6 terms, 3 MFMAs
+        uint32_t wh[2], wm[2], wl[2];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) dzn[j] = buf[j >> 2][4 * g + (j & 3)][i];
-      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-    const Parts dznp = split3(dzn);
-
-    // ---- dW2^T += relu(HN)^T . dZ   (hidden on i / rows, samples on k)
-#pragma unroll
-    for (int t2 = 0; t2 < HT; ++t2) {
-      float hv[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        hv[r] = relu(hn[0][t2][r]);
-        hv[4 + r] = relu(hn[1][t2][r]);
-      }
-      dw2[t2] = mfma_split(split3(hv), dznp, false, dw2[t2]);
-    }
-
-    // ---- dW1 += dH^T . X  (X loaded sample-on-k)
-#pragma unroll
-    for (int q = 0; q < QT; ++q) {
-      float xc[8];
-      load_x_cols(xc, a, t, e0, k, g, i, q);
-      const Parts xq = x_exact ? Parts{hi_frag(xc), {}, {}} : split3(xc);
-#pragma unroll
-      for (int t2 = 0; t2 < HT; ++t2) {
-        float hv[8];
+        for (int q = 0; q < 2; ++q) {
+          wh[q] = w2b_s[t2][0][lane][q];
+          wm[q] = w2b_s[t2][1][lane][q];
+          wl[q] = w2b_s[t2][2][lane][q];
+        }
+        f32x4 acc = mfma_bf16(a_hl, cat(wl, wh), f32x4{0.f, 0.f, 0.f, 0.f});
+        acc = mfma_bf16(a_hm, cat(wm, wh), acc);
+        acc = mfma_bf16(a_hm, cat(wh, wm), acc);
+        float dh[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          hv[r] = dh[0][t2][r];
-          hv[4 + r] = dh[1][t2][r];
+          dh[r] = hn[r] > 0.f ? acc[r] : 0.f;
+          dw2[t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(relu(hn[r]), dzn[r], dw2[t2], 0, 0, 0);
         }
-        dw1[t2][q] = mfma_split(split3(hv), xq, x_exact, dw1[t2][q]);
+        const Parts4 dp = split3_4(dh);
+        const bf16x8 d_hm = cat(dp.h, dp.m), d_hl = cat(dp.h, dp.l);
+#pragma unroll
+        for (int q = 0; q < QT; ++q) {
+          dw1[t2][q] = mfma_bf16(d_hl, bx3[q], dw1[t2][q]);
+          if (!x_exact) dw1[t2][q] = mfma_bf16(d_hm, bx2[q], dw1[t2][q]);
+          dw1[t2][q] = mfma_bf16(d_hm, bx1[q], dw1[t2][q]);
+        }
       }
     }
+    lds_order();
   }
 
   // ---- workgroup partial
-  constexpr int NV = HT * QT * 4 + HT * 4 + 4 + 2;
   float acc[NV];
   {
     int n = 0;
@@ -544,10 +611,14 @@ __global__ __launch_bounds__(256) void ppo_actor_grad_kernel(UpdArgs a) {
       const float v = acc[n++];
       if (hid < H && i < A) out[OW2 + i * H + hid] = v;
     }
+  // db2: lane (g, i) holds action 4 ga + r summed over its samples; PAIR: ga = g & 1 and the two
+  // 32-lane halves hold different samples of the same actions
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const float v = row_sum16(acc[n++]);
-    if (i == 0 && 4 * g + r < A) out[OB2 + 4 * g + r] = v;
+    float v = row_sum16(acc[n++]);
+    if constexpr (PAIR) v += uf(partner32(fu(v), g));
+    const int act = 4 * (PAIR ? (g & 1) : g) + r;
+    if (i == 0 && (!PAIR || g < 2) && act < A) out[OB2 + act] = v;
   }
   const float ss = group_sum(row_sum16(acc[n++]));
   const float es = group_sum(row_sum16(acc[n++]));
@@ -561,8 +632,28 @@ __global__ __launch_bounds__(256) void ppo_actor_grad_kernel(UpdArgs a) {
 // Value(x) = V2 relu(V1 x + c1) + c2, loss = mean (v - R)^2 (ippo.py:210-216).  Hidden layer in
 // the sample-on-rows orientation only: the 64 -> 1 layer is a per-lane product + a 16-lane row
 // sum, dV1 = dHv^T . X as in the actor.  a.w2 = V2 [N][1][H], a.b2 = c2 [N][1], a.weight = R.
+template <int KC>
+struct CriticIn {
+  float x[2][KC][8];
+  float R[2][4];  // returns of samples 16s + 4g + r
+};
+
+template <int KC>
+__device__ __forceinline__ void load_critic_in(CriticIn<KC>& in, const UpdArgs& a, int tile, int k, int g, int i) {
+  const int t = tile / a.tiles_per_t;
+  const int e0 = (tile - t * a.tiles_per_t) * 32;
+  load_rows<KC>(in.x, a, t, e0, k, g, i);
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = e0 + 16 * s + 4 * g + r;
+      in.R[s][r] = ld_st(a.weight, a.w_st, t, e < a.E ? e : a.E - 1, k);
+    }
+}
+
 template <int KC, int HT>
-__global__ __launch_bounds__(256) void ppo_critic_grad_kernel(UpdArgs a) {
+__global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(UpdArgs a) {
   constexpr int QT = 2 * KC;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, i = lane & 15;
@@ -602,101 +693,118 @@ __global__ __launch_bounds__(256) void ppo_critic_grad_kernel(UpdArgs a) {
     for (int q = 0; q < QT; ++q) dv1[t][q] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   float dc2 = 0.f, loss_acc = 0.f;
-  __shared__ float red[(HT * QT * 4 + HT + 2) * 64];
+  constexpr int XS = 32 * KC + 4;  // row stride = 4 mod 16 floats: sample-on-k reads hit 64 banks
+  __shared__ __attribute__((aligned(16))) float xs[4][32][XS];
+  constexpr int NV = HT * QT * 4 + HT + 2;
+  __shared__ float red[NV * 64];
+  float(*xw)[XS] = xs[wave];
 
   const int stride = a.G * 4;
-  for (int tile = blockIdx.y * 4 + wave; tile < a.n_tiles; tile += stride) {
+  int tile = blockIdx.y * 4 + wave;
+  CriticIn<KC> in;
+  if (tile < a.n_tiles) load_critic_in<KC>(in, a, tile, k, g, i);
+  for (; tile < a.n_tiles; tile += stride) {
     const int t = tile / a.tiles_per_t;
     const int e0 = (tile - t * a.tiles_per_t) * 32;
-    bf16x8 xh[2][KC];
-    Parts xp[2][KC];
-    uint32_t low = 0;
-    float xr[2][KC][8];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int e = e0 + 16 * s + i;
-      load_x_rows<KC>(xr[s], a, t, e, e < a.E, k, g);
-#pragma unroll
-      for (int c = 0; c < KC; ++c) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) low |= fbits(xr[s][c][j]) & 0xFFFFu;
-        xh[s][c] = hi_frag(xr[s][c]);
-      }
-    }
-    const bool x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;
-    if (!x_exact) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int c = 0; c < KC; ++c) xp[s][c] = split3(xr[s][c]);
-    }
-    // HV = X . V1^T (sample 16s + 4g + r on rows, hidden 16t + i on lanes)
-    f32x4 hv[2][HT];
+    float R[2][4];
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
+      for (int r = 0; r < 4; ++r) R[s][r] = in.R[s][r];
+    uint32_t low = 0;
+    bf16x8 xh[2][KC];
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        float xr[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int col = 32 * c + 8 * g + j;
+          xr[j] = col < F ? in.x[s][c][j] : col == F ? 1.f : 0.f;
+          low |= fbits(xr[j]) & 0xFFFFu;
+        }
+        xh[s][c] = hi_frag(xr);
+        *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g]) = f32x4{xr[0], xr[1], xr[2], xr[3]};
+        *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g + 4]) = f32x4{xr[4], xr[5], xr[6], xr[7]};
+      }
+    const bool x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;
+    if (tile + stride < a.n_tiles) load_critic_in<KC>(in, a, tile + stride, k, g, i);
+    lds_order();
+
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      // HV = X . V1^T (sample 16s + 4g + r on rows, hidden 16t + i on lanes)
+      f32x4 hv[HT];
+#pragma unroll
       for (int t2 = 0; t2 < HT; ++t2) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < KC; ++c) {
-          const f32x4 z0 = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : hv[s][t2];
-          hv[s][t2] = mfma_bf16(xh[s][c], v1p[t2][c].l, z0);
-          hv[s][t2] = mfma_bf16(xh[s][c], v1p[t2][c].m, hv[s][t2]);
-          hv[s][t2] = mfma_bf16(xh[s][c], v1p[t2][c].h, hv[s][t2]);
+          acc = mfma_bf16(xh[s][c], v1p[t2][c].l, acc);
+          acc = mfma_bf16(xh[s][c], v1p[t2][c].m, acc);
+          acc = mfma_bf16(xh[s][c], v1p[t2][c].h, acc);
         }
         if (!x_exact) {
 #pragma unroll
           for (int c = 0; c < KC; ++c) {
-            hv[s][t2] = mfma_bf16(xp[s][c].l, v1p[t2][c].h, hv[s][t2]);
-            hv[s][t2] = mfma_bf16(xp[s][c].m, v1p[t2][c].m, hv[s][t2]);
-            hv[s][t2] = mfma_bf16(xp[s][c].m, v1p[t2][c].h, hv[s][t2]);
+            float xv[8];
+            lds_row(xv, xw, 16 * s + i, 32 * c + 8 * g);
+            const Parts xp = split3(xv);
+            acc = mfma_bf16(xp.l, v1p[t2][c].h, acc);
+            acc = mfma_bf16(xp.m, v1p[t2][c].m, acc);
+            acc = mfma_bf16(xp.m, v1p[t2][c].h, acc);
           }
         }
+        hv[t2] = acc;
       }
-    // value, dL/dv = 2 (v - R) / B
-    float dvs[2][4];
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
+      // value and dL/dv = 2 (v - R) / B of samples 16s + 4g + r
+      float dvs[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float pv = 0.f;
 #pragma unroll
-        for (int t2 = 0; t2 < HT; ++t2) pv = fmaf(relu(hv[s][t2][r]), v2f[t2], pv);
+        for (int t2 = 0; t2 < HT; ++t2) pv = fmaf(relu(hv[t2][r]), v2f[t2], pv);
         const float v = row_sum16(pv) + c2;
-        const int e = e0 + 16 * s + 4 * g + r;
-        const bool ok = e < a.E;
-        const float R = ok ? ld_st(a.weight, a.w_st, t, e, k) : 0.f;
-        const float d = v - R;
-        dvs[s][r] = ok ? 2.f * a.scale * d : 0.f;
+        const bool ok = e0 + 16 * s + 4 * g + r < a.E;
+        const float d = v - R[s][r];
+        dvs[r] = ok ? 2.f * a.scale * d : 0.f;
         if (ok && i == 0) loss_acc += d * d;
+        dc2 += i == 0 ? dvs[r] : 0.f;
       }
+      // X sample-on-k for this half: B fragments with the split parts paired to dHv's
+      bf16x8 bx1[QT], bx2[QT], bx3[QT];
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int q = 0; q < QT; ++q) {
+        float xc[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        dc2 += i == 0 ? dvs[s][r] : 0.f;
-#pragma unroll
-        for (int t2 = 0; t2 < HT; ++t2) dv2[t2] = fmaf(dvs[s][r], relu(hv[s][t2][r]), dv2[t2]);
+        for (int r = 0; r < 4; ++r) xc[r] = xw[16 * s + 4 * g + r][16 * q + i];
+        const Parts4 xq = split3_4(xc);
+        bx1[q] = cat(xq.h, xq.h);
+        bx2[q] = cat(xq.m, xq.m);
+        bx3[q] = cat(xq.l, xq.h);
       }
-    // dV1 += dHv^T . X
-#pragma unroll
-    for (int q = 0; q < QT; ++q) {
-      float xc[8];
-      load_x_cols(xc, a, t, e0, k, g, i, q);
-      const Parts xq = x_exact ? Parts{hi_frag(xc), {}, {}} : split3(xc);
 #pragma unroll
       for (int t2 = 0; t2 < HT; ++t2) {
-        float dv[8];
+        float dh[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          dv[r] = hv[0][t2][r] > 0.f ? dvs[0][r] * v2f[t2] : 0.f;
-          dv[4 + r] = hv[1][t2][r] > 0.f ? dvs[1][r] * v2f[t2] : 0.f;
+          dv2[t2] = fmaf(dvs[r], relu(hv[t2][r]), dv2[t2]);
+          dh[r] = hv[t2][r] > 0.f ? dvs[r] * v2f[t2] : 0.f;
         }
-        dv1[t2][q] = mfma_split(split3(dv), xq, x_exact, dv1[t2][q]);
+        const Parts4 dp = split3_4(dh);
+        const bf16x8 d_hm = cat(dp.h, dp.m), d_hl = cat(dp.h, dp.l);
+#pragma unroll
+        for (int q = 0; q < QT; ++q) {
+          dv1[t2][q] = mfma_bf16(d_hl, bx3[q], dv1[t2][q]);
+          if (!x_exact) dv1[t2][q] = mfma_bf16(d_hm, bx2[q], dv1[t2][q]);
+          dv1[t2][q] = mfma_bf16(d_hm, bx1[q], dv1[t2][q]);
+        }
       }
     }
+    lds_order();
   }
 
-  constexpr int NV = HT * QT * 4 + HT + 2;
   float acc[NV];
   {
     int n = 0;
@@ -823,8 +931,11 @@ static int launch_reduce(const UpdArgs& a, float* gw1, float* gb1, float* gw2, f
 template <int KC, int HT>
 static void launch_actor(const UpdArgs& a, hipStream_t s) {
   dim3 grid(a.N, a.G);
-  if (a.kind == 0) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1>), grid, dim3(256), 0, s, a);
+  const bool pair = a.A <= 8;
+  if (a.kind == 0 && pair) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, true>), grid, dim3(256), 0, s, a);
+  else if (a.kind == 0) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, false>), grid, dim3(256), 0, s, a);
+  else if (pair) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, true>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, false>), grid, dim3(256), 0, s, a);
 }
 
 extern "C" int d2d_ppo_actor_grad(const d2d_mlp_desc* d, int32_t T, const float* obs, const void* actions,
