@@ -25,14 +25,17 @@
 // dZ (sample on i, action on rows) is both the A operand of dH = dZ . W2 and, transposed
 // through LDS, the B operand of dW2^T = h^T . dZ.  dW1 = dH^T . X takes dH straight from its
 // accumulator (hidden on i, samples on rows) against X loaded sample-on-k.  Layer-1 bias = input
-// column F (x = 1), so db1 is column F of dW1.  All products use the exact three-way bf16 split
-// (mlp_common.h): fp32-accurate, parity with torch fp32 autograd at 1e-5-relative.
+// column F (x = 1), so db1 is column F of dW1.  Precision: the forward (both layer-1
+// orientations, dH) on the exact three-way bf16 split (mlp_common.h), the logits and dW2 on fp32
+// MFMA -- fp32-accurate; dW1's operand dH on a two-way RNE split (<= 2^-17 relative per term).
+// Parity with torch autograd: tests/test_update_gpu.py (2e-5 of max|grad| vs float64).
 //
 // Partial sums: every wave accumulates its tiles in registers; the four waves of a workgroup
 // are summed in fixed order through LDS and written as one partial per (workgroup, agent);
 // update_reduce_kernel sums the partials in fixed order.  No atomics: bitwise reproducible.
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 
 #include "mlp_common.h"
 
@@ -74,6 +77,29 @@ __device__ __forceinline__ bf16x8 cat(const uint32_t (&a)[2], const uint32_t (&b
   u32x4v v = {a[0], a[1], b[0], b[1]};
   return __builtin_bit_cast(bf16x8, v);
 }
+// Two-way round-to-nearest bf16 split of 4 floats: v = h + m + e, |e| <= 2^-17 |v| (the dW1 / dV1
+// operand dH: a per-tile value used against 2 x-tiles only, where the 3-way split's VALU cost
+// outweighs its MFMAs; the weight gradients then carry ~2^-17 relative error per product term,
+// below the fp32 accumulation error of their 10^5-10^6-sample sums)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t rne2(float a, float b) {
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32
+  return __builtin_bit_cast(uint32_t, v);
+}
+struct Parts2x4 {
+  uint32_t h[2], m[2];
+};
+__device__ __forceinline__ Parts2x4 split2_4(const float (&v)[4]) {
+  Parts2x4 o;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const uint32_t h = rne2(v[2 * p], v[2 * p + 1]);
+    o.h[p] = h;
+    o.m[p] = rne2(v[2 * p] - ffrom(h << 16), v[2 * p + 1] - ffrom(h & 0xFFFF0000u));
+  }
+  return o;
+}
+
 // high parts only (bf16-exact values)
 __device__ __forceinline__ bf16x8 hi_frag(const float (&v)[8]) {
   uint32_t u[4];
@@ -176,7 +202,7 @@ __device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, uint32_t act,
     sum += ex[r];
   }
   sum = group_sum<HALF>(sum);
-  const float inv = 1.f / sum;
+  const float inv = __builtin_amdgcn_rcpf(sum);  // v_rcp_f32, 1 ulp (IEEE division: ~10 VALU + branches)
   float p[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) p[r] = ex[r] * inv;
@@ -194,7 +220,7 @@ __device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, uint32_t act,
       lsum += valid[r] ? (bit ? l1 : l0) : 0.f;
       esum += valid[r] ? -(p[r] * l1 + (1.f - p[r]) * l0) : 0.f;
       logit[r] = l1 - l0;
-      dsur[r] = (valid[r] && inside) ? (bit ? 1.f / pc : -1.f / (1.f - pc)) : 0.f;
+      dsur[r] = (valid[r] && inside) ? (bit ? __builtin_amdgcn_rcpf(pc) : -__builtin_amdgcn_rcpf(1.f - pc)) : 0.f;
     }
     logp = group_sum<HALF>(lsum) * a.inv_A;
     ent = group_sum<HALF>(esum) * a.inv_A;
@@ -206,10 +232,8 @@ __device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, uint32_t act,
     const float eb = a.beta * a.scale * a.inv_A;  // d(-beta*mean ent)/dp_c = +beta * logit_c / A / B
 #pragma unroll
     for (int r = 0; r < 4; ++r) gr[r] = valid[r] ? coef * dsur[r] + eb * logit[r] : 0.f;
-    if (ok && ga == 0) {
-      surr_acc += fminf(s1, s2);
-      ent_acc += ent;
-    }
+    surr_acc += (ok && ga == 0) ? fminf(s1, s2) : 0.f;
+    ent_acc += (ok && ga == 0) ? ent : 0.f;
     float dot = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) dot += p[r] * gr[r];
@@ -224,7 +248,7 @@ __device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, uint32_t act,
 #pragma unroll
     for (int r = 0; r < 4; ++r) psum += p[r];
     psum = group_sum<HALF>(psum);
-    const float ipsum = 1.f / psum;
+    const float ipsum = __builtin_amdgcn_rcpf(psum);
     float q[4], lsel = 0.f, esum = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -235,9 +259,10 @@ __device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, uint32_t act,
       const bool chosen = valid[r] && 4 * ga + r == aid;
       lsel += chosen ? lq : 0.f;
       esum += valid[r] ? q[r] * lq : 0.f;
-      dsur[r] = (chosen && inside) ? 1.f / qc : 0.f;
+      const float iqc = __builtin_amdgcn_rcpf(qc);
+      dsur[r] = (chosen && inside) ? iqc : 0.f;
       // d(-beta * ent)/dq = beta * (log qc + q * [inside] / qc)
-      gr[r] = valid[r] ? (lq + (inside ? q[r] / qc : 0.f)) : 0.f;
+      gr[r] = valid[r] ? (lq + (inside ? q[r] * iqc : 0.f)) : 0.f;
     }
     logp = group_sum<HALF>(lsel);
     ent = -group_sum<HALF>(esum);
@@ -261,10 +286,8 @@ __device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, uint32_t act,
       dot += p[r] * dp[r];
     }
     dot = group_sum<HALF>(dot);
-    if (ok && ga == 0) {
-      surr_acc += fminf(s1, s2);
-      ent_acc += ent;
-    }
+    surr_acc += (ok && ga == 0) ? fminf(s1, s2) : 0.f;
+    ent_acc += (ok && ga == 0) ? ent : 0.f;
     f32x4 dz;
 #pragma unroll
     for (int r = 0; r < 4; ++r) dz[r] = (ok && valid[r]) ? p[r] * (dp[r] - dot) : 0.f;
@@ -428,141 +451,156 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
     const bool x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;  // wave-uniform
     if (tile + stride < a.n_tiles) load_actor_in<KC, PAIR>(in, a, tile + stride, k, g, i);
 
-    // ---- forward (transposed): HT = W1 . X^T (bf16 split), Z^T = W2 . relu(HT) + b2 (fp32)
-    f32x4 zt[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      f32x4 ht[HT];
-#pragma unroll
-      for (int t2 = 0; t2 < HT; ++t2) {
-#pragma unroll
-        for (int c = 0; c < KC; ++c) {
-          const f32x4 z0 = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ht[t2];
-          ht[t2] = mfma_bf16(w1p[t2][c].l, xh[s][c], z0);
-          ht[t2] = mfma_bf16(w1p[t2][c].m, xh[s][c], ht[t2]);
-          ht[t2] = mfma_bf16(w1p[t2][c].h, xh[s][c], ht[t2]);
-        }
-      }
-      if (!x_exact) {  // rare (fractional observations): residual parts, x re-read from LDS
-#pragma unroll
-        for (int c = 0; c < KC; ++c) {
-          float xv[8];
-          lds_row(xv, xw, 16 * s + i, 32 * c + 8 * g);
-          const Parts xp = split3(xv);
-#pragma unroll
-          for (int t2 = 0; t2 < HT; ++t2) {
-            ht[t2] = mfma_bf16(w1p[t2][c].h, xp.l, ht[t2]);
-            ht[t2] = mfma_bf16(w1p[t2][c].m, xp.m, ht[t2]);
-            ht[t2] = mfma_bf16(w1p[t2][c].h, xp.m, ht[t2]);
-          }
-        }
-      }
-      f32x4 z = b2i;
-#pragma unroll
-      for (int t2 = 0; t2 < HT; ++t2) {
-        const f32x4 w2f = *reinterpret_cast<const f32x4*>(&w2f_s[t2][lane][0]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) z = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[r], relu(ht[t2][r]), z, 0, 0, 0);
-      }
-      zt[s] = z;
-    }
-
-    // ---- epilogue -> dZ (lane (g, i): sample 16s + i, actions 4g + r), written transposed to LDS
-    f32x4 dz[2];
-    if constexpr (PAIR) {
-      f32x4 zc;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) zc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(zt[0][r]), fu(zt[1][r]), false, false)[0]);
-      const int e = e0 + 16 * (g >> 1) + i;
-      const f32x4 dzc = ppo_dz<KIND, true>(a, zc, cur.act[0], cur.lo[0], cur.w[0], e < a.E, g & 1, surr_acc, ent_acc);
-      db2 += dzc;
-      *reinterpret_cast<f32x4*>(&zb[g >> 1][i][4 * (g & 1)]) = dzc;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const auto sw = __builtin_amdgcn_permlane32_swap(fu(dzc[r]), 0u, false, false);
-        dz[0][r] = uf(sw[0]);  // lanes 0-31: half 0's dZ, lanes 32-63: 0
-        dz[1][r] = uf(sw[1]);  // lanes 0-31: half 1's dZ, lanes 32-63: 0
-      }
-    } else {
+    // the tile body; XE = true would specialise it on bf16-exact inputs (no branch inside), but
+    // carrying both bodies spills at 2 waves/SIMD, so the general body with wave-uniform runtime
+    // branches on x_exact runs (exact-only measured 5 % faster)
+    auto body = [&](auto xe) {
+      constexpr bool XE = decltype(xe)::value;
+      // ---- forward (transposed): HT = W1 . X^T (bf16 split), Z^T = W2 . relu(HT) + b2 (fp32)
+      f32x4 zt[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        const int e = e0 + 16 * s + i;
-        dz[s] = ppo_dz<KIND, false>(a, zt[s], cur.act[s], cur.lo[s], cur.w[s], e < a.E, g, surr_acc, ent_acc);
-        db2 += dz[s];
-        *reinterpret_cast<f32x4*>(&zb[s][i][4 * g]) = dz[s];
-      }
-    }
-    lds_order();
-
-    // ---- per half s: HN = X . W1^T (sample on rows), dH = (dZ . W2) * [HN > 0],
-    //      dW2^T += relu(HN)^T . dZ  (fp32, k = sample 16s + 4g + r of step r),
-    //      dW1 += dH^T . X (k-slots: dH's 4 samples x two split parts; X sample-on-k from LDS)
+        __builtin_amdgcn_sched_barrier(0);  // bound live ranges: phases do not interleave
+        f32x4 ht[HT];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      float dzn[4];
+        for (int t2 = 0; t2 < HT; ++t2) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dzn[r] = zb[s][4 * g + r][i];
-      bf16x8 bx1[QT], bx2[QT], bx3[QT];
-#pragma unroll
-      for (int q = 0; q < QT; ++q) {
-        float xc[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) xc[r] = xw[16 * s + 4 * g + r][16 * q + i];
-        const Parts4 xq = split3_4(xc);
-        bx1[q] = cat(xq.h, xq.h);  // dH_h x_h + dH_m x_h
-        bx2[q] = cat(xq.m, xq.m);  // dH_h x_m + dH_m x_m   (fractional x only)
-        bx3[q] = cat(xq.l, xq.h);  // dH_h x_l + dH_l x_h
-      }
-      const float dv[4] = {dz[s][0], dz[s][1], dz[s][2], dz[s][3]};
-      const Parts4 zp = split3_4(dv);
-      const bf16x8 a_hm = cat(zp.h, zp.m), a_hl = cat(zp.h, zp.l);
-#pragma unroll
-      for (int t2 = 0; t2 < HT; ++t2) {
-        f32x4 hn = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < KC; ++c) {
-          hn = mfma_bf16(xh[s][c], w1p[t2][c].l, hn);
-          hn = mfma_bf16(xh[s][c], w1p[t2][c].m, hn);
-          hn = mfma_bf16(xh[s][c], w1p[t2][c].h, hn);
+          for (int c = 0; c < KC; ++c) {
+            const f32x4 z0 = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ht[t2];
+            ht[t2] = mfma_bf16(w1p[t2][c].l, xh[s][c], z0);
+            ht[t2] = mfma_bf16(w1p[t2][c].m, xh[s][c], ht[t2]);
+            ht[t2] = mfma_bf16(w1p[t2][c].h, xh[s][c], ht[t2]);
+          }
         }
-        if (!x_exact) {
+        if (!(XE || x_exact)) {  // rare (fractional observations): residual parts, x re-read from LDS
 #pragma unroll
           for (int c = 0; c < KC; ++c) {
             float xv[8];
             lds_row(xv, xw, 16 * s + i, 32 * c + 8 * g);
             const Parts xp = split3(xv);
-            hn = mfma_bf16(xp.l, w1p[t2][c].h, hn);
-            hn = mfma_bf16(xp.m, w1p[t2][c].m, hn);
-            hn = mfma_bf16(xp.m, w1p[t2][c].h, hn);
+#pragma unroll
+            for (int t2 = 0; t2 < HT; ++t2) {
+              ht[t2] = mfma_bf16(w1p[t2][c].h, xp.l, ht[t2]);
+              ht[t2] = mfma_bf16(w1p[t2][c].m, xp.m, ht[t2]);
+              ht[t2] = mfma_bf16(w1p[t2][c].h, xp.m, ht[t2]);
+            }
           }
         }
-        // the 4 live k-slots of each fragment half carry a second split part: 6 terms, 3 MFMAs
-        uint32_t wh[2], wm[2], wl[2];
+        f32x4 z = b2i;
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          wh[q] = w2b_s[t2][0][lane][q];
-          wm[q] = w2b_s[t2][1][lane][q];
-          wl[q] = w2b_s[t2][2][lane][q];
+        for (int t2 = 0; t2 < HT; ++t2) {
+          const f32x4 w2f = *reinterpret_cast<const f32x4*>(&w2f_s[t2][lane][0]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) z = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[r], relu(ht[t2][r]), z, 0, 0, 0);
         }
-        f32x4 acc = mfma_bf16(a_hl, cat(wl, wh), f32x4{0.f, 0.f, 0.f, 0.f});
-        acc = mfma_bf16(a_hm, cat(wm, wh), acc);
-        acc = mfma_bf16(a_hm, cat(wh, wm), acc);
-        float dh[4];
+        zt[s] = z;
+      }
+
+      __builtin_amdgcn_sched_barrier(0);  // bound live ranges: phases do not interleave
+      // ---- epilogue -> dZ (lane (g, i): sample 16s + i, actions 4g + r), written transposed to LDS
+      f32x4 dz[2];
+      if constexpr (PAIR) {
+        f32x4 zc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(zt[0][r]), fu(zt[1][r]), false, false)[0]);
+        const int e = e0 + 16 * (g >> 1) + i;
+        const f32x4 dzc = ppo_dz<KIND, true>(a, zc, cur.act[0], cur.lo[0], cur.w[0], e < a.E, g & 1, surr_acc, ent_acc);
+        db2 += dzc;
+        *reinterpret_cast<f32x4*>(&zb[g >> 1][i][4 * (g & 1)]) = dzc;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          dh[r] = hn[r] > 0.f ? acc[r] : 0.f;
-          dw2[t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(relu(hn[r]), dzn[r], dw2[t2], 0, 0, 0);
+          const auto sw = __builtin_amdgcn_permlane32_swap(fu(dzc[r]), 0u, false, false);
+          dz[0][r] = uf(sw[0]);  // lanes 0-31: half 0's dZ, lanes 32-63: 0
+          dz[1][r] = uf(sw[1]);  // lanes 0-31: half 1's dZ, lanes 32-63: 0
         }
-        const Parts4 dp = split3_4(dh);
-        const bf16x8 d_hm = cat(dp.h, dp.m), d_hl = cat(dp.h, dp.l);
+      } else {
 #pragma unroll
-        for (int q = 0; q < QT; ++q) {
-          dw1[t2][q] = mfma_bf16(d_hl, bx3[q], dw1[t2][q]);
-          if (!x_exact) dw1[t2][q] = mfma_bf16(d_hm, bx2[q], dw1[t2][q]);
-          dw1[t2][q] = mfma_bf16(d_hm, bx1[q], dw1[t2][q]);
+        for (int s = 0; s < 2; ++s) {
+          const int e = e0 + 16 * s + i;
+          dz[s] = ppo_dz<KIND, false>(a, zt[s], cur.act[s], cur.lo[s], cur.w[s], e < a.E, g, surr_acc, ent_acc);
+          db2 += dz[s];
+          *reinterpret_cast<f32x4*>(&zb[s][i][4 * g]) = dz[s];
         }
       }
-    }
+      lds_order();
+
+      // ---- per half s: HN = X . W1^T (sample on rows), dH = (dZ . W2) * [HN > 0],
+      //      dW2^T += relu(HN)^T . dZ  (fp32, k = sample 16s + 4g + r of step r),
+      //      dW1 += dH^T . X (k-slots: dH's 4 samples x its two RNE split parts; X sample-on-k
+      //      from LDS, bf16-exact on env observations, else split too)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        __builtin_amdgcn_sched_barrier(0);  // bound live ranges: phases do not interleave
+        float dzn[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dzn[r] = zb[s][4 * g + r][i];
+        bf16x8 bx1[QT], bx2[QT];
+#pragma unroll
+        for (int q = 0; q < QT; ++q) {
+          float xc[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xc[r] = xw[16 * s + 4 * g + r][16 * q + i];
+          if (XE || x_exact) {
+            const uint32_t xh2[2] = {pack_hi(xc[0], xc[1]), pack_hi(xc[2], xc[3])};
+            bx1[q] = cat(xh2, xh2);  // (dH_h + dH_m) x
+          } else {
+            const Parts2x4 xq = split2_4(xc);
+            const uint32_t z2[2] = {0u, 0u};
+            bx1[q] = cat(xq.h, xq.h);  // (dH_h + dH_m) x_h
+            bx2[q] = cat(xq.m, z2);    // dH_h x_m
+          }
+        }
+        const float dv[4] = {dz[s][0], dz[s][1], dz[s][2], dz[s][3]};
+        const Parts4 zp = split3_4(dv);
+        const bf16x8 a_hm = cat(zp.h, zp.m), a_hl = cat(zp.h, zp.l);
+#pragma unroll
+        for (int t2 = 0; t2 < HT; ++t2) {
+          f32x4 hn = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < KC; ++c) {
+            hn = mfma_bf16(xh[s][c], w1p[t2][c].l, hn);
+            hn = mfma_bf16(xh[s][c], w1p[t2][c].m, hn);
+            hn = mfma_bf16(xh[s][c], w1p[t2][c].h, hn);
+          }
+          if (!(XE || x_exact)) {
+#pragma unroll
+            for (int c = 0; c < KC; ++c) {
+              float xv[8];
+              lds_row(xv, xw, 16 * s + i, 32 * c + 8 * g);
+              const Parts xp = split3(xv);
+              hn = mfma_bf16(xp.l, w1p[t2][c].h, hn);
+              hn = mfma_bf16(xp.m, w1p[t2][c].m, hn);
+              hn = mfma_bf16(xp.m, w1p[t2][c].h, hn);
+            }
+          }
+          // the 4 live k-slots of each fragment half carry a second split part: 6 terms, 3 MFMAs
+          uint32_t wh[2], wm[2], wl[2];
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            wh[q] = w2b_s[t2][0][lane][q];
+            wm[q] = w2b_s[t2][1][lane][q];
+            wl[q] = w2b_s[t2][2][lane][q];
+          }
+          f32x4 acc = mfma_bf16(a_hl, cat(wl, wh), f32x4{0.f, 0.f, 0.f, 0.f});
+          acc = mfma_bf16(a_hm, cat(wm, wh), acc);
+          acc = mfma_bf16(a_hm, cat(wh, wm), acc);
+          float dh[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dh[r] = hn[r] > 0.f ? acc[r] : 0.f;
+            dw2[t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(relu(hn[r]), dzn[r], dw2[t2], 0, 0, 0);
+          }
+          const Parts2x4 dp = split2_4(dh);
+          const bf16x8 d_hm = cat(dp.h, dp.m);
+#pragma unroll
+          for (int q = 0; q < QT; ++q) {
+            if (!(XE || x_exact)) dw1[t2][q] = mfma_bf16(d_hm, bx2[q], dw1[t2][q]);
+            dw1[t2][q] = mfma_bf16(d_hm, bx1[q], dw1[t2][q]);
+          }
+        }
+      }
+    };
+    body(std::false_type{});  // runtime x_exact branches (a deferred-tile XE=true mode: DESIGN.md)
     lds_order();
   }
 
@@ -732,76 +770,88 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
     if (tile + stride < a.n_tiles) load_critic_in<KC>(in, a, tile + stride, k, g, i);
     lds_order();
 
+    // the tile body; XE = true would specialise it on bf16-exact inputs (no branch inside), but
+    // carrying both bodies spills at 2 waves/SIMD, so the general body with wave-uniform runtime
+    // branches on x_exact runs (exact-only measured 5 % faster)
+    auto body = [&](auto xe) {
+      constexpr bool XE = decltype(xe)::value;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      // HV = X . V1^T (sample 16s + 4g + r on rows, hidden 16t + i on lanes)
-      f32x4 hv[HT];
+      for (int s = 0; s < 2; ++s) {
+        __builtin_amdgcn_sched_barrier(0);  // bound live ranges: phases do not interleave
+        // HV = X . V1^T (sample 16s + 4g + r on rows, hidden 16t + i on lanes)
+        f32x4 hv[HT];
 #pragma unroll
-      for (int t2 = 0; t2 < HT; ++t2) {
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < KC; ++c) {
-          acc = mfma_bf16(xh[s][c], v1p[t2][c].l, acc);
-          acc = mfma_bf16(xh[s][c], v1p[t2][c].m, acc);
-          acc = mfma_bf16(xh[s][c], v1p[t2][c].h, acc);
-        }
-        if (!x_exact) {
+        for (int t2 = 0; t2 < HT; ++t2) {
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int c = 0; c < KC; ++c) {
-            float xv[8];
-            lds_row(xv, xw, 16 * s + i, 32 * c + 8 * g);
-            const Parts xp = split3(xv);
-            acc = mfma_bf16(xp.l, v1p[t2][c].h, acc);
-            acc = mfma_bf16(xp.m, v1p[t2][c].m, acc);
-            acc = mfma_bf16(xp.m, v1p[t2][c].h, acc);
+            acc = mfma_bf16(xh[s][c], v1p[t2][c].l, acc);
+            acc = mfma_bf16(xh[s][c], v1p[t2][c].m, acc);
+            acc = mfma_bf16(xh[s][c], v1p[t2][c].h, acc);
           }
+          if (!(XE || x_exact)) {
+#pragma unroll
+            for (int c = 0; c < KC; ++c) {
+              float xv[8];
+              lds_row(xv, xw, 16 * s + i, 32 * c + 8 * g);
+              const Parts xp = split3(xv);
+              acc = mfma_bf16(xp.l, v1p[t2][c].h, acc);
+              acc = mfma_bf16(xp.m, v1p[t2][c].m, acc);
+              acc = mfma_bf16(xp.m, v1p[t2][c].h, acc);
+            }
+          }
+          hv[t2] = acc;
         }
-        hv[t2] = acc;
-      }
-      // value and dL/dv = 2 (v - R) / B of samples 16s + 4g + r
-      float dvs[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float pv = 0.f;
-#pragma unroll
-        for (int t2 = 0; t2 < HT; ++t2) pv = fmaf(relu(hv[t2][r]), v2f[t2], pv);
-        const float v = row_sum16(pv) + c2;
-        const bool ok = e0 + 16 * s + 4 * g + r < a.E;
-        const float d = v - R[s][r];
-        dvs[r] = ok ? 2.f * a.scale * d : 0.f;
-        if (ok && i == 0) loss_acc += d * d;
-        dc2 += i == 0 ? dvs[r] : 0.f;
-      }
-      // X sample-on-k for this half: B fragments with the split parts paired to dHv's
-      bf16x8 bx1[QT], bx2[QT], bx3[QT];
-#pragma unroll
-      for (int q = 0; q < QT; ++q) {
-        float xc[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) xc[r] = xw[16 * s + 4 * g + r][16 * q + i];
-        const Parts4 xq = split3_4(xc);
-        bx1[q] = cat(xq.h, xq.h);
-        bx2[q] = cat(xq.m, xq.m);
-        bx3[q] = cat(xq.l, xq.h);
-      }
-#pragma unroll
-      for (int t2 = 0; t2 < HT; ++t2) {
-        float dh[4];
+        // value and dL/dv = 2 (v - R) / B of samples 16s + 4g + r
+        float dvs[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          dv2[t2] = fmaf(dvs[r], relu(hv[t2][r]), dv2[t2]);
-          dh[r] = hv[t2][r] > 0.f ? dvs[r] * v2f[t2] : 0.f;
+          float pv = 0.f;
+#pragma unroll
+          for (int t2 = 0; t2 < HT; ++t2) pv = fmaf(relu(hv[t2][r]), v2f[t2], pv);
+          const float v = row_sum16(pv) + c2;
+          const bool ok = e0 + 16 * s + 4 * g + r < a.E;
+          const float d = v - R[s][r];
+          dvs[r] = ok ? 2.f * a.scale * d : 0.f;
+          if (ok && i == 0) loss_acc += d * d;
+          dc2 += i == 0 ? dvs[r] : 0.f;
         }
-        const Parts4 dp = split3_4(dh);
-        const bf16x8 d_hm = cat(dp.h, dp.m), d_hl = cat(dp.h, dp.l);
+        // X sample-on-k for this half: B fragments with the split parts paired to dHv's
+        bf16x8 bx1[QT], bx2[QT];
 #pragma unroll
         for (int q = 0; q < QT; ++q) {
-          dv1[t2][q] = mfma_bf16(d_hl, bx3[q], dv1[t2][q]);
-          if (!x_exact) dv1[t2][q] = mfma_bf16(d_hm, bx2[q], dv1[t2][q]);
-          dv1[t2][q] = mfma_bf16(d_hm, bx1[q], dv1[t2][q]);
+          float xc[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) xc[r] = xw[16 * s + 4 * g + r][16 * q + i];
+          if (XE || x_exact) {
+            const uint32_t xh2[2] = {pack_hi(xc[0], xc[1]), pack_hi(xc[2], xc[3])};
+            bx1[q] = cat(xh2, xh2);
+          } else {
+            const Parts2x4 xq = split2_4(xc);
+            const uint32_t z2[2] = {0u, 0u};
+            bx1[q] = cat(xq.h, xq.h);
+            bx2[q] = cat(xq.m, z2);
+          }
+        }
+#pragma unroll
+        for (int t2 = 0; t2 < HT; ++t2) {
+          float dh[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            dv2[t2] = fmaf(dvs[r], relu(hv[t2][r]), dv2[t2]);
+            dh[r] = hv[t2][r] > 0.f ? dvs[r] * v2f[t2] : 0.f;
+          }
+          const Parts2x4 dp = split2_4(dh);
+          const bf16x8 d_hm = cat(dp.h, dp.m);
+#pragma unroll
+          for (int q = 0; q < QT; ++q) {
+            if (!(XE || x_exact)) dv1[t2][q] = mfma_bf16(d_hm, bx2[q], dv1[t2][q]);
+            dv1[t2][q] = mfma_bf16(d_hm, bx1[q], dv1[t2][q]);
+          }
         }
       }
-    }
+    };
+    body(std::false_type{});  // runtime x_exact branches (a deferred-tile XE=true mode: DESIGN.md)
     lds_order();
   }
 
