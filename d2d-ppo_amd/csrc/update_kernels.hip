@@ -27,7 +27,8 @@
 // accumulator (hidden on i, samples on rows) against X loaded sample-on-k.  Layer-1 bias = input
 // column F (x = 1), so db1 is column F of dW1.  Precision: the forward (both layer-1
 // orientations, dH) on the exact three-way bf16 split (mlp_common.h), the logits and dW2 on fp32
-// MFMA -- fp32-accurate; dW1's operand dH on a two-way RNE split (<= 2^-17 relative per term).
+// MFMA -- fp32-accurate; the weight-gradient GEMMs dW1 = dH^T X and dW2 = h^T dZ on two-way RNE
+// splits of their per-tile operands (<= 2^-17 relative per term).
 // Parity with torch autograd: tests/test_update_gpu.py (2e-5 of max|grad| vs float64).
 //
 // Partial sums: every wave accumulates its tiles in registers; the four waves of a workgroup
@@ -331,10 +332,10 @@ __device__ __forceinline__ void lds_order() {
 // ------------------------------------------------------------------------- actor gradients
 // KC = input chunks of 32 (F + 1 <= 32 KC), HT = hidden tiles of 16 (H <= 16 HT), A <= 16;
 // PAIR (A <= 8): one epilogue pass serves both halves (lanes 0-31 half 0, 32-63 half 1).
-// Products: layer 1 (both orientations), dH and dW1 on the exact bf16 split (the weight splits
-// are made once; x is bf16-exact on env observations, so 3 MFMAs per 16x16x32); the logits and
-// dW2, whose operands would need a split of their own per tile, on v_mfma_f32_16x16x4_f32 (an
-// exact fmaf chain) straight from the accumulator registers.
+// Products: layer 1 (both orientations) and dH on the exact bf16 split (the weight splits are
+// made once; x is bf16-exact on env observations, so 3 MFMAs per 16x16x32); the logits on
+// v_mfma_f32_16x16x4_f32 (an exact fmaf chain) straight from the accumulator registers; the
+// weight gradients dW1, dW2 on two-way RNE splits of their per-tile operands.
 template <int KC, int HT, int KIND, bool PAIR>
 __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(UpdArgs a) {
   constexpr int QT = 2 * KC;  // input tiles of 16 in dW1
@@ -534,6 +535,10 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
         float dzn[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) dzn[r] = zb[s][4 * g + r][i];
+        // dW2^T operand B: dZ (k = sample 4g + j of this half, column = action i), two-way split
+        const Parts2x4 zn = split2_4(dzn);
+        const uint32_t zz[2] = {0u, 0u};
+        const bf16x8 bz1 = cat(zn.h, zn.h), bz2 = cat(zn.m, zz);
         bf16x8 bx1[QT], bx2[QT];
 #pragma unroll
         for (int q = 0; q < QT; ++q) {
@@ -584,12 +589,17 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
           f32x4 acc = mfma_bf16(a_hl, cat(wl, wh), f32x4{0.f, 0.f, 0.f, 0.f});
           acc = mfma_bf16(a_hm, cat(wm, wh), acc);
           acc = mfma_bf16(a_hm, cat(wh, wm), acc);
-          float dh[4];
+          float dh[4], hr[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             dh[r] = hn[r] > 0.f ? acc[r] : 0.f;
-            dw2[t2] = __builtin_amdgcn_mfma_f32_16x16x4f32(relu(hn[r]), dzn[r], dw2[t2], 0, 0, 0);
+            hr[r] = relu(hn[r]);
           }
+          // dW2^T += relu(HN)^T . dZ: (h_h + h_m) dz_h + h_h dz_m, k-slots = 4 samples x 2 parts
+          const Parts2x4 hp = split2_4(hr);
+          const bf16x8 h_hm = cat(hp.h, hp.m);
+          dw2[t2] = mfma_bf16(h_hm, bz2, dw2[t2]);
+          dw2[t2] = mfma_bf16(h_hm, bz1, dw2[t2]);
           const Parts2x4 dp = split2_4(dh);
           const bf16x8 d_hm = cat(dp.h, dp.m);
 #pragma unroll
