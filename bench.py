@@ -189,13 +189,52 @@ def ppo_leg(args, rank, world, local):
     el = max_over_ranks(time.perf_counter() - t0, world)
     N = params["n_agents"]
     samples = ro.T * E2 * world
-    flop = 6.0 * N * samples * (30 * 64 + 64 * 8 + 30 * 64 + 64)  # fwd+bwd ~ 3x fwd, 2 flop/mac
-    path = ("fused HIP update kernels (actor + critic gradients, exact-split bf16 MFMA) + torch Adam"
-            if upd is None else "torch agent-stacked bmm autograd + Adam")
-    return {"updates_per_s": P / el, "ms_per_update": el / P * 1e3, "epochs": P, "path": path,
-            "batch": f"{E2} envs/GPU x {ro.T} slots x {N} agents (actor+critic, one Adam step each)",
-            "agent_samples_per_update": samples * N, "agent_samples_per_s": samples * N * P / el,
-            "gemm_tflops": flop * P / el / 1e12}
+    F, H, A = lr.policy.F, lr.policy.H, lr.policy.A
+    out = {"updates_per_s": P / el, "ms_per_update": el / P * 1e3, "epochs": P,
+           "batch": f"{E2} envs/GPU x {ro.T} slots x {N} agents (actor+critic, one Adam step each)",
+           "agent_samples_per_update": samples * N, "agent_samples_per_s": samples * N * P / el}
+    if upd is None:
+        out["path"] = "fused HIP update kernels (actor + critic gradients) + torch Adam"
+        out["kernels"] = update_kernel_roofline(lr, ro, F, H, A, reps=P)
+    else:
+        out["path"] = "torch agent-stacked bmm autograd + Adam"
+    return out
+
+
+def update_kernel_roofline(lr, ro, F, H, A, reps=4):
+    """Live HIP-event timing of the two gradient kernels (each incl. its partial-sum reduce) on
+    the leg's rollout, and their algorithmic FLOPs per agent-sample (SURVEY §8d MFMA roofline):
+      actor  fwd 2(FH + HA), bwd dW2 2HA + dH 2AH + dW1 2FH (no input gradient)
+      critic fwd 2(FH + H),  bwd dV2 2H + dHv 2H + dV1 2FH
+    The result is fp32-accurate (exact-split bf16 / fp32 MFMA), so `peak` is the
+    dense fp32 matrix peak (157.3 TFLOP/s)."""
+    from d2dhip.update import actor_grads, critic_grads
+    pp, vp = lr.policy.params, lr.value.params
+    N = lr.policy.N
+    agent_samples = ro.T * ro.E * N
+    f_actor = 2 * (F * H + H * A) + 2 * H * A + 2 * A * H + 2 * F * H
+    f_critic = 2 * (F * H + H) + 2 * H + 2 * H + 2 * F * H
+    ga = {k: torch.empty_like(v) for k, v in pp.items()}
+    gv = {k: torch.empty_like(v) for k, v in vp.items()}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ta = tc = 0.0
+    for _ in range(reps):
+        ev[0].record()
+        actor_grads({k: v.data for k, v in pp.items()}, ro.obs, ro.actions, ro.logp.permute(0, 2, 1), ro.adv, "comb",
+                    grads=ga)
+        ev[1].record()
+        critic_grads({k: v.data for k, v in vp.items()}, ro.obs, ro.ret, grads=gv)
+        ev[2].record()
+        torch.cuda.synchronize()
+        ta += ev[0].elapsed_time(ev[1]) / reps
+        tc += ev[1].elapsed_time(ev[2]) / reps
+    peak = 157.3
+    res = {}
+    for name, ms, fl in (("actor", ta, f_actor), ("critic", tc, f_critic)):
+        tf = agent_samples * fl / (ms / 1e3) / 1e12
+        res[name] = {"ms": ms, "flop_per_agent_sample": fl, "achieved_tflops": tf, "peak_tflops": peak,
+                     "frac": tf / peak, "bound": "mfma"}
+    return res
 
 
 def main():
