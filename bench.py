@@ -12,14 +12,16 @@ Bernoulli(0.1) per agent-channel) + the env-step kernel, fp32 obs emitted to
 HBM; every episode_length slots the envs reset (inside the timed loop).
 Inputs are HBM-resident before timing starts.
 
-Two more legs are reported in the same JSON line (they do not change `value`):
+Three more legs are reported in the same JSON line (they do not change `value`):
   rollout : the iPPO behaviour-policy slot at the same 65,536 envs — agent-stacked
             actor + critic forward (H=64), Bernoulli sampling, log-probs, action
             packing and the env kernel (ippo.py:293-330 batched);
   ppo     : PPO updates/s — one update = one epoch of the iPPO clipped-surrogate
             + value update for all 64 actors and 64 critics (ippo.py:194-217,
             418-426) over a full-episode rollout of --ppo-envs envs per GPU
-            (200 slots), incl. the RCCL gradient all-reduce when N > 1.
+            (200 slots), incl. the RCCL gradient all-reduce when N > 1;
+  train   : one whole iPPO training iteration (rollout + GAE + --train-epochs PPO epochs)
+            at the full 65,536 envs per GPU (ippo.py:406-441).
 """
 import argparse
 import json
@@ -244,6 +246,31 @@ def update_kernel_roofline(lr, ro, F, H, A, reps=4):
     return res
 
 
+def train_leg(env, args, rank, world, local):
+    """One full iPPO training iteration at the bench's env batch (the north-star scale):
+    `iPPO.train(1, n_epoch, num_episodes=E)` = a 200-slot rollout of every env (policy kernel +
+    env kernel per slot), GAE/returns, and n_epoch fused PPO epochs over all T*E*N agent-samples
+    (ippo.py:406-441).  Reported: seconds per iteration and end-to-end env-steps/s."""
+    from algorithms.ippo import iPPO
+    torch.manual_seed(2)
+    lr = iPPO(env, hidden_size=64, gamma=0.6, policy_lr=3e-4, value_lr=1e-3, device=env.batch().device,
+              useRNN=False, combinatorial=True)
+    E = env.batch().E
+    lr.train(1, n_epoch=1, num_episodes=E, test_freq=10 ** 9)  # warm-up: allocations, kernels
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    lr.train(1, n_epoch=args.train_epochs, num_episodes=E, test_freq=10 ** 9)
+    torch.cuda.synchronize()
+    barrier(world)
+    el = max_over_ranks(time.perf_counter() - t0, world)
+    T = env.episode_length
+    return {"s_per_iteration": el, "n_epoch": args.train_epochs, "envs_per_gpu": E, "slots": T,
+            "agent_samples_per_epoch": E * world * T * env.n_agents,
+            "env_steps_per_s_end_to_end": E * world * T / el,
+            "path": "fused policy kernel + env kernel rollout, HIP GAE, fused PPO gradient kernels + Adam"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -253,10 +280,11 @@ def main():
     ap.add_argument("--episode-length", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--legs", default="env,rollout,ppo")
+    ap.add_argument("--legs", default="env,rollout,ppo,train")
     ap.add_argument("--rollout-steps", type=int, default=60)
     ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
     ap.add_argument("--ppo-epochs", type=int, default=6)
+    ap.add_argument("--train-epochs", type=int, default=4, help="n_epoch of the train leg")
     args = ap.parse_args()
 
     rank, world, local = setup_dist(args.gpus)
@@ -317,6 +345,7 @@ def main():
         rollout = rollout_leg(env, args, world)
     if "ppo" in legs:
         ppo = ppo_leg(args, rank, world, local)
+    train = train_leg(env, args, rank, world, local) if "train" in legs else None
 
     if rank == 0:
         res = {
@@ -348,6 +377,8 @@ def main():
             res["rollout"] = rollout
         if ppo is not None:
             res["ppo"] = ppo
+        if train is not None:
+            res["train"] = train
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(params, seconds=args.cpu_seconds)
         print(json.dumps(res))
