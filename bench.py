@@ -222,10 +222,10 @@ def update_kernel_roofline(lr, ro, F, H, A, reps=4):
     ta = tc = 0.0
     for _ in range(reps):
         ev[0].record()
-        actor_grads({k: v.data for k, v in pp.items()}, ro.obs, ro.actions, ro.logp.permute(0, 2, 1), ro.adv, "comb",
-                    grads=ga)
+        actor_grads({k: v.data for k, v in pp.items()}, ro.obs, ro.actions, ro.logp.permute(0, 2, 1),
+                    ro.adv_tne.permute(0, 2, 1), "comb", grads=ga)
         ev[1].record()
-        critic_grads({k: v.data for k, v in vp.items()}, ro.obs, ro.ret, grads=gv)
+        critic_grads({k: v.data for k, v in vp.items()}, ro.obs, ro.ret_tne.permute(0, 2, 1), grads=gv)
         ev[2].record()
         torch.cuda.synchronize()
         ta += ev[0].elapsed_time(ev[1]) / reps
@@ -247,20 +247,30 @@ def update_kernel_roofline(lr, ro, F, H, A, reps=4):
 
 
 def train_leg(env, args, rank, world, local):
-    """One full iPPO training iteration at the bench's env batch (the north-star scale):
-    `iPPO.train(1, n_epoch, num_episodes=E)` = a 200-slot rollout of every env (policy kernel +
-    env kernel per slot), GAE/returns, and n_epoch fused PPO epochs over all T*E*N agent-samples
-    (ippo.py:406-441).  Reported: seconds per iteration and end-to-end env-steps/s."""
+    """One full iPPO training iteration at the bench's env batch (the north-star scale): a
+    200-slot rollout of every env (policy kernel + env kernel per slot), GAE/returns, and n_epoch
+    fused PPO epochs over all T*E*N agent-samples (the loop body of iPPO.train, ippo.py:410-426,
+    without its periodic test()).  Reported: seconds per iteration and end-to-end env-steps/s."""
     from algorithms.ippo import iPPO
     torch.manual_seed(2)
     lr = iPPO(env, hidden_size=64, gamma=0.6, policy_lr=3e-4, value_lr=1e-3, device=env.batch().device,
               useRNN=False, combinatorial=True)
     E = env.batch().E
-    lr.train(1, n_epoch=1, num_episodes=E, test_freq=10 ** 9)  # warm-up: allocations, kernels
+
+    def iteration(n_epoch):
+        # the body of iPPO.train for one iteration (ippo.py:410-426) without the test(50) calls
+        # the reference makes when iter % test_freq == 0 (always true at iter 0)
+        ro = lr._rollout(E)
+        upd = lr._update_state(ro)
+        for _ in range(n_epoch):
+            lr._update_epoch(ro, upd)
+        del ro, upd
+
+    iteration(1)  # warm-up: allocations, kernels
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
-    lr.train(1, n_epoch=args.train_epochs, num_episodes=E, test_freq=10 ** 9)
+    iteration(args.train_epochs)
     torch.cuda.synchronize()
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world)

@@ -31,10 +31,21 @@ from .data_parallel import DataParallelMixin, allreduce_mean_scalar
 
 
 class Rollout:
-    """Device tensors of one rollout ([T][E]... time-major as produced)."""
+    """Device tensors of one rollout ([T][E]... time-major as produced).  `adv` / `ret` (agent-
+    major [N][E*T], env-major sample order) are materialised from `adv_tne` / `ret_tne`
+    ([T][N][E], the GAE output) only when a consumer asks for them; the fused update kernels
+    read the [T][N][E] tensors in place."""
 
     def __init__(self, **kw):
         self.__dict__.update(kw)
+
+    def __getattr__(self, name):
+        src = self.__dict__.get(name + "_tne") if name in ("adv", "ret") else None
+        if src is None:
+            raise AttributeError(name)
+        v = src.permute(1, 2, 0).reshape(src.shape[1], -1)
+        self.__dict__[name] = v
+        return v
 
 
 class BatchedLearnerBase(DataParallelMixin):
@@ -351,8 +362,8 @@ class BatchedLearnerBase(DataParallelMixin):
         return rnn_windows(obs_agent.unsqueeze(0), self.history_len, self.env.episode_length)[0]
 
     # ----------------------------------------------------- GAE wrapper
-    def _gae(self, rewards_te, values_tec, dones, normalize_adv=True, normalize_ret=True):
-        return gae_returns(rewards_te, values_tec, dones, self.gamma, 0.97, normalize_adv=normalize_adv,
+    def _gae(self, rewards_te, values_tec, dones, normalize_adv=True, normalize_ret=True, layout="tec"):
+        return gae_returns(rewards_te, values_tec, dones, self.gamma, 0.97, normalize_adv=normalize_adv, layout=layout,
                            normalize_ret=normalize_ret, group=self.process_group,
                            last_shard=self._last_shard(), n_envs_total=self._n_envs_total())
 

@@ -166,10 +166,8 @@ class iPPO(BatchedLearnerBase):
     # ------------------------------------------------------------ rollouts
     def _rollout(self, num_episodes, teacher=None):
         ro = self._collect(num_episodes, train=True, want_values=True, teacher=teacher)
-        vals = ro.values.permute(0, 2, 1)                          # [T][E][N]
-        adv, ret = self._gae(ro.rewards, vals, ro.dones)             # ippo.py:337-338
-        ro.adv = self._seq(adv.permute(0, 2, 1))                     # [N][E*T]
-        ro.ret = self._seq(ret.permute(0, 2, 1))
+        # values [T][N][E] as the policy kernel wrote them; adv / ret in the same layout (ippo.py:337-338)
+        ro.adv_tne, ro.ret_tne = self._gae(ro.rewards, ro.values, ro.dones, layout="tce")
         return ro
 
     def create_rollouts(self, num_episodes=4):
@@ -222,10 +220,12 @@ class iPPO(BatchedLearnerBase):
         kind = "comb" if self.combinatorial else "chsel"
         B = ro.T * ro.E
         _, sa = actor_grads({k: v.data for k, v in pp.items()}, ro.obs, ro.actions, ro.logp.permute(0, 2, 1),
-                            ro.adv, kind, clip=cliprange, beta=beta, grads=self._grad_buffers(pp))
+                            ro.adv_tne.permute(0, 2, 1), kind, clip=cliprange, beta=beta,
+                            grads=self._grad_buffers(pp))
         self._reduce_grads(self.policy.parameters())
         self.policy_optimizer.step()
-        _, sv = critic_grads({k: v.data for k, v in vp.items()}, ro.obs, ro.ret, grads=self._grad_buffers(vp))
+        _, sv = critic_grads({k: v.data for k, v in vp.items()}, ro.obs, ro.ret_tne.permute(0, 2, 1),
+                             grads=self._grad_buffers(vp))
         self._reduce_grads(self.value.parameters())
         self.value_optimizer.step()
         return -(sa[:, 0] + beta * sa[:, 1]) / B, sv[:, 0] / B

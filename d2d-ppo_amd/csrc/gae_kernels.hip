@@ -6,9 +6,11 @@
 // column (adv: numpy std ddof=0, returns: torch std ddof=1; each gated on ALL
 // columns having std > 0, quirk Q2).
 //
-// Layout [T][E][cols]: for a fixed t, the (env, column) pairs are contiguous,
-// so one thread per (env, column) walking t backwards reads and writes fully
-// coalesced rows; the recursion state (gae, R) lives in f64 registers.
+// Layout [T][E][cols] or [T][cols][E] (`_tce` entry points: the policy kernel's
+// value layout, and the update kernels' preferred per-sample layout): for a fixed
+// t, the (env, column) pairs are contiguous, so one thread per (env, column)
+// walking t backwards reads and writes fully coalesced rows; the recursion state
+// (gae, R) lives in f64 registers.
 // Normalisation = deterministic two-level column sums (block partials in a
 // fixed order), so results do not depend on atomics ordering and the stats can
 // be all-reduced across ranks between the passes.
@@ -21,11 +23,12 @@ namespace d2d {
 __global__ __launch_bounds__(256) void gae_scan_kernel(int T, int E, int cols, int rcols, const float* __restrict__ rew,
                                                        const float* __restrict__ val, const uint8_t* __restrict__ done,
                                                        double gamma, double lam, int last_shard, float* __restrict__ adv,
-                                                       float* __restrict__ ret) {
+                                                       float* __restrict__ ret, int tce) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t width = (int64_t)E * cols;
   if (i >= width) return;
-  const int e = (int)(i / cols);
+  // [T][E][cols]: i = e * cols + c; [T][cols][E] (tce): i = c * E + e -- coalesced either way
+  const int e = tce ? (int)(i % E) : (int)(i / cols);
   const bool global_last = last_shard && (e == E - 1);
   double gae = 0.0, R = 0.0, v_next = 0.0;
   for (int t = T - 1; t >= 0; --t) {
@@ -77,6 +80,30 @@ __global__ __launch_bounds__(256) void colstats_partial_kernel(int64_t rows, int
   }
 }
 
+// [T][cols][E] layout: block (c, b) sums column c over slots t = b, b + nb, ... (fixed order)
+__global__ __launch_bounds__(256) void colstats_tce_partial_kernel(int T, int cols, int E, const float* __restrict__ x,
+                                                                   const double* __restrict__ center,
+                                                                   double* __restrict__ partial) {
+  __shared__ double acc[256];
+  const int c = blockIdx.x, b = blockIdx.y, nb = gridDim.y;
+  const double m = center ? center[c] : 0.0;
+  double s = 0.0;
+  for (int t = b; t < T; t += nb) {
+    const float* row = x + ((int64_t)t * cols + c) * E;
+    for (int e = threadIdx.x; e < E; e += blockDim.x) {
+      const double v = (double)row[e] - m;
+      s += center ? v * v : v;
+    }
+  }
+  acc[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = 0.0;
+    for (int j = 0; j < (int)blockDim.x; ++j) tot += acc[j];
+    partial[(int64_t)b * cols + c] = tot;
+  }
+}
+
 __global__ void colstats_reduce_kernel(int nb, int cols, const double* __restrict__ partial, double* __restrict__ out) {
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < cols; c += gridDim.x * blockDim.x) {
     double t = 0.0;
@@ -104,10 +131,11 @@ __global__ __launch_bounds__(256) void colstats_finalize_kernel(int cols, const 
 
 __global__ __launch_bounds__(256) void normalize_kernel(int64_t n, int cols, float* __restrict__ x,
                                                         const double* __restrict__ mean,
-                                                        const double* __restrict__ scale, const int32_t* __restrict__ gate) {
+                                                        const double* __restrict__ scale, const int32_t* __restrict__ gate,
+                                                        int inner) {
   if (!*gate) return;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % cols);
+    const int c = inner > 0 ? (int)((i / inner) % cols) : (int)(i % cols);
     x[i] = (float)(((double)x[i] - mean[c]) * scale[c]);
   }
 }
@@ -116,9 +144,9 @@ __global__ __launch_bounds__(256) void normalize_kernel(int64_t n, int cols, flo
 
 using namespace d2d;
 
-extern "C" int d2d_gae_scan(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards, const float* values,
-                            const uint8_t* dones, double gamma, double lam, int32_t last_shard, float* adv, float* ret,
-                            void* stream) {
+static int gae_scan(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards, const float* values,
+                    const uint8_t* dones, double gamma, double lam, int32_t last_shard, float* adv, float* ret, void* stream,
+                    int tce) {
   if (T < 0 || E < 0 || cols < 1 || (reward_cols != 1 && reward_cols != cols) || !rewards || !values || !dones || !adv || !ret) {
     d2d_set_error("d2d_gae_scan: bad arguments");
     return D2D_EINVAL;
@@ -127,9 +155,21 @@ extern "C" int d2d_gae_scan(int32_t T, int32_t E, int32_t cols, int32_t reward_c
   if (T == 0 || width == 0) return D2D_OK;
   hipLaunchKernelGGL(gae_scan_kernel, dim3((unsigned)((width + 255) / 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), T, E, cols, reward_cols, rewards, values, dones, gamma, lam, last_shard,
-                     adv, ret);
+                     adv, ret, tce);
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
+}
+
+extern "C" int d2d_gae_scan(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards, const float* values,
+                            const uint8_t* dones, double gamma, double lam, int32_t last_shard, float* adv, float* ret,
+                            void* stream) {
+  return gae_scan(T, E, cols, reward_cols, rewards, values, dones, gamma, lam, last_shard, adv, ret, stream, 0);
+}
+
+extern "C" int d2d_gae_scan_tce(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards,
+                                const float* values, const uint8_t* dones, double gamma, double lam, int32_t last_shard,
+                                float* adv, float* ret, void* stream) {
+  return gae_scan(T, E, cols, reward_cols, rewards, values, dones, gamma, lam, last_shard, adv, ret, stream, 1);
 }
 
 extern "C" int64_t d2d_colstats_workspace(int64_t rows, int32_t cols) {
@@ -157,6 +197,21 @@ extern "C" int d2d_colstats(int64_t rows, int32_t cols, const float* x, const do
   return D2D_OK;
 }
 
+extern "C" int d2d_colstats_tce(int32_t T, int32_t cols, int32_t E, const float* x, const double* center, double* partial,
+                                double* out, void* stream) {
+  if (T < 0 || E < 0 || cols < 1 || !x || !partial || !out) {
+    d2d_set_error("d2d_colstats_tce: bad arguments");
+    return D2D_EINVAL;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int nb = T < 1 ? 1 : (T > kStatRowBlocks ? kStatRowBlocks : T);
+  hipLaunchKernelGGL(colstats_tce_partial_kernel, dim3(cols, nb), dim3(256), 0, s, T, cols, E, x, center, partial);
+  D2D_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(colstats_reduce_kernel, dim3((cols + 255) / 256), dim3(256), 0, s, nb, cols, partial, out);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
 extern "C" int d2d_colstats_finalize(int32_t cols, const double* sum, const double* m2, double n, int32_t ddof,
                                      double* mean, double* scale, int32_t* gate, void* stream) {
   if (cols < 1 || !sum || !mean || (m2 && (!scale || !gate))) {
@@ -169,18 +224,31 @@ extern "C" int d2d_colstats_finalize(int32_t cols, const double* sum, const doub
   return D2D_OK;
 }
 
+static int normalize(int64_t n, int32_t cols, int32_t inner, float* x, const double* mean, const double* scale,
+                     const int32_t* gate, void* stream) {
+  if (n == 0) return D2D_OK;
+  int64_t grid = (n + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(normalize_kernel, dim3((unsigned)grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), n, cols,
+                     x, mean, scale, gate, inner);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
 extern "C" int d2d_normalize_columns(int64_t rows, int32_t cols, float* x, const double* mean, const double* scale,
                                      const int32_t* gate, void* stream) {
   if (rows < 0 || cols < 1 || !x || !mean || !scale || !gate) {
     d2d_set_error("d2d_normalize_columns: bad arguments");
     return D2D_EINVAL;
   }
-  const int64_t n = rows * cols;
-  if (n == 0) return D2D_OK;
-  int64_t grid = (n + 255) / 256;
-  if (grid > 8192) grid = 8192;
-  hipLaunchKernelGGL(normalize_kernel, dim3((unsigned)grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), n, cols,
-                     x, mean, scale, gate);
-  D2D_CHECK_HIP(hipGetLastError());
-  return D2D_OK;
+  return normalize(rows * cols, cols, 0, x, mean, scale, gate, stream);
+}
+
+extern "C" int d2d_normalize_columns_tce(int32_t T, int32_t cols, int32_t E, float* x, const double* mean,
+                                         const double* scale, const int32_t* gate, void* stream) {
+  if (T < 0 || E < 0 || cols < 1 || !x || !mean || !scale || !gate) {
+    d2d_set_error("d2d_normalize_columns_tce: bad arguments");
+    return D2D_EINVAL;
+  }
+  return normalize((int64_t)T * cols * E, cols, E, x, mean, scale, gate, stream);
 }

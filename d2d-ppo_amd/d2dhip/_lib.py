@@ -62,6 +62,10 @@ _SIGS = {
     "d2d_buffer_words": (ctypes.c_int, [ctypes.c_int32]),
     "d2d_gae_scan": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p, ctypes.c_double,
                                      ctypes.c_double, ctypes.c_int32, _p, _p, _p]),
+    "d2d_gae_scan_tce": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p,
+                                         ctypes.c_double, ctypes.c_double, ctypes.c_int32, _p, _p, _p]),
+    "d2d_colstats_tce": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p, _p, _p]),
+    "d2d_normalize_columns_tce": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p, _p, _p]),
     "d2d_colstats_workspace": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32]),
     "d2d_colstats": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, _p, _p, _p, _p, _p]),
     "d2d_colstats_finalize": (ctypes.c_int, [ctypes.c_int32, _p, _p, ctypes.c_double, ctypes.c_int32, _p, _p, _p,

@@ -140,12 +140,22 @@ int d2d_gae_scan(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const 
                  const uint8_t* dones, double gamma, double lam, int32_t last_shard, float* adv, float* ret,
                  void* stream);
 
+/* The same scan on the [T][cols][E] layout (values / adv / ret element (t, e, c) at
+ * (t * cols + c) * E + e; rewards [T][E] when reward_cols == 1, else [T][cols][E]). */
+int d2d_gae_scan_tce(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards,
+                     const float* values, const uint8_t* dones, double gamma, double lam, int32_t last_shard,
+                     float* adv, float* ret, void* stream);
+
 /* Column sums over rows of x [rows][cols]: out[c] = sum_r (x[r][c] - center[c])^p,
  * p = 1 when center == NULL else 2.  Deterministic two-level reduction in
  * double; `partial` is a workspace of d2d_colstats_workspace(rows, cols) doubles. */
 int64_t d2d_colstats_workspace(int64_t rows, int32_t cols);
 int d2d_colstats(int64_t rows, int32_t cols, const float* x, const double* center, double* partial,
                  double* out, void* stream);
+
+/* d2d_colstats over x [T][cols][E] (column c = the T*E elements (t, c, e)); same workspace. */
+int d2d_colstats_tce(int32_t T, int32_t cols, int32_t E, const float* x, const double* center, double* partial,
+                     double* out, void* stream);
 
 /* mean = sum / n ; when m2 != NULL: std = sqrt(m2 / (n - ddof)), scale = 1/std and
  * *gate = all columns std > 0 (ippo.py:100-101, 114-115); when m2 == NULL only mean. */
@@ -155,6 +165,9 @@ int d2d_colstats_finalize(int32_t cols, const double* sum, const double* m2, dou
 /* x = gate ? (x - mean) * scale : x  (per column) */
 int d2d_normalize_columns(int64_t rows, int32_t cols, float* x, const double* mean, const double* scale,
                           const int32_t* gate, void* stream);
+/* the same on x [T][cols][E] */
+int d2d_normalize_columns_tce(int32_t T, int32_t cols, int32_t E, float* x, const double* mean, const double* scale,
+                              const int32_t* gate, void* stream);
 
 /* ---- fused behaviour-policy slot (MLP learners) ----
  * Replaces Policy/Value.forward + PPO.select_action for every agent of every env

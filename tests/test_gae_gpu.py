@@ -93,3 +93,25 @@ def test_gae_kernel_size_independent_properties():
     lhs = ret_raw[:-1].double()
     rhs = rew[:-1, :, None].double() + 0.6 * ret_raw[1:].double()
     assert float((lhs - rhs).abs().max()) < 1e-4
+
+
+@pytest.mark.parametrize("T,E,cols,rcols", [(200, 64, 8, 1), (400, 33, 64, 1), (50, 300, 5, 5), (120, 1, 4, 1)])
+def test_gae_kernel_tce_layout(T, E, cols, rcols):
+    """The [T][cols][E] entry points (values as the policy kernel writes them) give the [T][E][cols]
+    results transposed, and match the oracle (ragged E, per-column and broadcast rewards)."""
+    from oracle.gae_oracle import gae_returns_batched
+    rng = np.random.default_rng(T * 7 + E + cols)
+    rew = rng.integers(0, 5, size=(T, E) if rcols == 1 else (T, E, cols)).astype(np.float32)
+    val = rng.normal(size=(T, E, cols)).astype(np.float32)
+    done = np.zeros(T, dtype=bool)
+    done[T // 2 - 1] = True
+    done[-1] = True
+    adv, ret = run(rew, val, done, 0.6)
+    rew_tce = rew if rcols == 1 else np.ascontiguousarray(rew.transpose(0, 2, 1))
+    adv_t, ret_t = run(rew_tce, np.ascontiguousarray(val.transpose(0, 2, 1)), done, 0.6, layout="tce")
+    np.testing.assert_allclose(adv_t.transpose(0, 2, 1), adv, rtol=0, atol=1e-6)
+    np.testing.assert_allclose(ret_t.transpose(0, 2, 1), ret, rtol=0, atol=1e-6)
+    if rcols == 1:
+        adv_o, ret_o = gae_returns_batched(rew, val, done, 0.6, 0.97)
+        np.testing.assert_allclose(adv_t.transpose(0, 2, 1), adv_o, rtol=0, atol=ATOL)
+        np.testing.assert_allclose(ret_t.transpose(0, 2, 1), ret_o, rtol=0, atol=ATOL)
