@@ -12,7 +12,7 @@ Bernoulli(0.1) per agent-channel) + the env-step kernel, fp32 obs emitted to
 HBM; every episode_length slots the envs reset (inside the timed loop).
 Inputs are HBM-resident before timing starts.
 
-Three more legs are reported in the same JSON line (they do not change `value`):
+More legs are reported in the same JSON line (they do not change `value`):
   rollout : the iPPO behaviour-policy slot at the same 65,536 envs — agent-stacked
             actor + critic forward (H=64), Bernoulli sampling, log-probs, action
             packing and the env kernel (ippo.py:293-330 batched);
@@ -21,7 +21,10 @@ Three more legs are reported in the same JSON line (they do not change `value`):
             418-426) over a full-episode rollout of --ppo-envs envs per GPU
             (200 slots), incl. the RCCL gradient all-reduce when N > 1;
   train   : one whole iPPO training iteration (rollout + GAE + --train-epochs PPO epochs)
-            at the full 65,536 envs per GPU (ippo.py:406-441).
+            at the full 65,536 envs per GPU (ippo.py:406-441);
+  configs : BASELINE.json configs[1] (chsel 16x4, 4,096 envs, D2D-PPO) and configs[4]
+            (agent sweep 8..256 x 8 channels, 4,096 envs/GPU, D2D-PPO): env-step rates and
+            one D2D-PPO training iteration each.
 """
 import argparse
 import json
@@ -281,6 +284,90 @@ def train_leg(env, args, rank, world, local):
             "path": "fused policy kernel + env kernel rollout, HIP GAE, fused PPO gradient kernels + Adam"}
 
 
+def _env_rate(env, steps=40):
+    """Env-step throughput of a batched env (device-sampled actions + env kernel, obs emitted)."""
+    b = env.batch()
+    act = b.action_buffer()
+    b.reset(want_obs=True)
+    for _ in range(5):
+        b.sample_actions(0.1, out=act)
+        b.step(act, want_obs=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        if b.timestep >= env.episode_length:
+            b.reset(want_obs=True)
+        b.sample_actions(0.1, out=act)
+        b.step(act, want_obs=True)
+    torch.cuda.synchronize()
+    return b.E * steps / (time.perf_counter() - t0)
+
+
+def _d2d_iteration(env, n_epoch, combinatorial):
+    """One D2D-PPO training iteration (d2d_ppo.py:405-448 loop body without test()): rollout of
+    every env, returns, n_epoch epochs (critic values, GAE, chain over a random agent cycle,
+    fused actor gradients, clip + Adam, central critic).  Seconds, after one warm-up iteration."""
+    from algorithms.d2d_ppo import D2DPPO
+    torch.manual_seed(3)
+    np.random.seed(3)
+    lr = D2DPPO(env, hidden_size=64, gamma=0.4, policy_lr=3e-4, value_lr=1e-3, beta_entropy=0.01,
+                device=env.batch().device, useRNN=False, combinatorial=combinatorial)
+    E = env.batch().E
+
+    def it(ne):
+        ro = lr._rollout(E)
+        upd = lr._update_state(ro)
+        for _ in range(ne):
+            lr._update_epoch(ro, upd)
+
+    it(1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    it(n_epoch)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, lr._fused_update_ok()
+
+
+def configs_leg(args, rank, world, local):
+    """The other BASELINE.json GPU configs, per GPU (weak scaling shards):
+      c2  channel_selection_env 16 agents x 4 channels, 4,096 envs, D2D-PPO (categorical);
+      c5  xp_n_agents sweep: combinatorial N in {8..256} x 8 channels, deadlines 7, switch 0.8,
+          lambda 1/14 aperiodic, 32,768 envs over 8 GPUs = 4,096 per GPU, D2D-PPO.
+    Env-step rates and one training iteration each (MLP policies, H = 64, n_epoch = 5 as in
+    xp_load.py:106)."""
+    from envs.channel_selection_env import ChannelSelectionEnv
+    from envs.combinatorial_env import CombinatorialEnv
+    dev = f"cuda:{local}"
+    out = {}
+    N = 16
+    p2 = dict(n_agents=N, n_channels=4, deadlines=np.full(N, 7), lbdas=np.full(N, 1 / 3.5), period=np.full(N, 2),
+              arrival_probs=np.full(N, 0.5), offsets=np.zeros(N), episode_length=args.episode_length,
+              traffic_model="aperiodic", periodic_devices=[], channel_switch=np.full(5, 0.8))
+    env = ChannelSelectionEnv(**p2, n_envs=4096, device=dev, seed=21)
+    env.shard(rank, world)
+    rate = _env_rate(env)
+    it_s, fused = _d2d_iteration(env, 5, combinatorial=False)
+    out["c2"] = {"envs_per_gpu": 4096, "agents": N, "channels": 4, "env_steps_per_s": rate * world,
+                 "d2d_iteration_s": it_s, "fused_update": fused,
+                 "d2d_env_steps_per_s_end_to_end": 4096 * world * args.episode_length / it_s}
+    del env
+    sweep = []
+    for N in (8, 16, 32, 64, 128, 256):
+        p5 = dict(n_agents=N, n_channels=8, deadlines=np.full(N, 7), lbdas=np.full(N, 1 / 14), period=None,
+                  arrival_probs=None, offsets=None, episode_length=args.episode_length, traffic_model="aperiodic",
+                  periodic_devices=[], channel_switch=np.ones((N, 8)) * 0.8)
+        env = CombinatorialEnv(**p5, n_envs=4096, device=dev, seed=22)
+        env.shard(rank, world)
+        rate = _env_rate(env)
+        it_s, fused = _d2d_iteration(env, 5, combinatorial=True)
+        sweep.append({"agents": N, "env_steps_per_s": rate * world, "agent_steps_per_s": rate * world * N,
+                      "d2d_iteration_s": it_s, "fused_update": fused})
+        del env
+        torch.cuda.empty_cache()
+    out["c5"] = {"envs_per_gpu": 4096, "channels": 8, "sweep": sweep}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -290,7 +377,7 @@ def main():
     ap.add_argument("--episode-length", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--legs", default="env,rollout,ppo,train")
+    ap.add_argument("--legs", default="env,rollout,ppo,train,configs")
     ap.add_argument("--rollout-steps", type=int, default=60)
     ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
     ap.add_argument("--ppo-epochs", type=int, default=6)
@@ -356,6 +443,7 @@ def main():
     if "ppo" in legs:
         ppo = ppo_leg(args, rank, world, local)
     train = train_leg(env, args, rank, world, local) if "train" in legs else None
+    configs = configs_leg(args, rank, world, local) if "configs" in legs else None
 
     if rank == 0:
         res = {
@@ -389,6 +477,8 @@ def main():
             res["ppo"] = ppo
         if train is not None:
             res["train"] = train
+        if configs is not None:
+            res["configs"] = configs
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(params, seconds=args.cpu_seconds)
         print(json.dumps(res))
