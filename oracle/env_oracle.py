@@ -12,6 +12,9 @@ following the reference's own control flow line by line:
   ChannelSelectionEnv /root/reference/envs/channel_selection_env.py
       reset 49-98, evolve_channel 104-107, evolve_buffer 109-113,
       step 116-214, metrics 217-236
+  D2DEnv ("single")   /root/reference/envs/env.py
+      reset 51-99, decode_signal 101-103, evolve_channel 105-107,
+      evolve_buffer 109-113, step 116-213, metrics 216-233
 
 Randomness comes from one of two sources:
   * replay  — the draws recorded from the reference (tests/golden/env_*.npz):
@@ -23,6 +26,8 @@ Output layout (shared with the HIP kernels):
   obs   [E][N][F]  agent k's row = [B[k,:w_k], chan_obs, ack, 0...]   (prefix-compact)
         comb:  w_k = D if homogeneous_size else d_k, F = D + 2C
         chsel: w_k = d_k, F = D + C + 1
+        single: [B[j,:d_j] for j in nbr(k)], H[nbr(k)] (post-evolve), ack, 0...;
+                F = max_k (sum_{j in nbr(k)} d_j + |nbr(k)| + 1)
   state [E][S]     the reference's np.concatenate(state)
 """
 import numpy as np
@@ -40,9 +45,9 @@ def _as_array(x, n=None, dtype=np.float64):
 class _Spec:
     """Per-agent tables derived from the reference constructor kwargs."""
 
-    def __init__(self, kind, n_agents, n_channels, deadlines, lbdas, period=5, arrival_probs=None, offsets=None,
+    def __init__(self, kind, n_agents, deadlines, lbdas, n_channels=1, period=5, arrival_probs=None, offsets=None,
                  episode_length=100, traffic_model="aperiodic", periodic_devices=(), homogeneous_size=False,
-                 channel_switch=None, **_ignored):
+                 channel_switch=None, neighbourhoods=None, **_ignored):
         self.kind = kind
         N, C = int(n_agents), int(n_channels)
         self.N, self.C = N, C
@@ -62,12 +67,21 @@ class _Spec:
         if kind == "comb":
             cs = np.zeros((N, C)) if channel_switch is None else np.broadcast_to(
                 np.asarray(channel_switch, dtype=np.float64), (N, C))
+        elif kind == "single":
+            # env.py:33, 106: one scalar (or per-agent) flip probability, default 0.2
+            cs = np.broadcast_to(np.asarray(0.2 if channel_switch is None else channel_switch, dtype=np.float64), (N,))
         else:
             cs = np.zeros(N) if channel_switch is None else np.asarray(channel_switch, dtype=np.float64)
         self.switch = np.array(cs, dtype=np.float64)
         if kind == "comb":
             self.F = self.D + 2 * C
             self.S = int(self.d.sum()) + C * (N + 1)
+        elif kind == "single":
+            self.nbr = [[int(k)] for k in range(N)] if neighbourhoods is None else \
+                [[int(j) for j in nb] for nb in neighbourhoods]                              # env.py:39-42
+            self.obs_len = np.array([int(self.d[nb].sum()) + len(nb) + 1 for nb in self.nbr])   # env.py:44-45
+            self.F = int(self.obs_len.max())
+            self.S = int(self.d.sum()) + N + 1                                                # env.py:48-49
         else:
             self.F = self.D + C + 1
             self.S = int(self.d.sum()) + C + 1
@@ -106,7 +120,11 @@ class EnvOracle:
         self.env_base = int(env_base)
         s = self.spec
         self.buffers = np.zeros((self.E, s.N, s.D), dtype=np.int64)
-        self.chan = np.ones((self.E, s.N, s.C) if kind == "comb" else (self.E, s.C + 1), dtype=np.int64)
+        self.chan = np.ones((self.E, s.N, s.C) if kind == "comb" else (self.E, s.N) if kind == "single"
+                            else (self.E, s.C + 1), dtype=np.int64)
+        self.channel_errors = np.zeros(self.E, dtype=np.int64)
+        self.n_collisions = np.zeros(self.E, dtype=np.int64)
+        self.successful_transmissions = np.zeros(self.E, dtype=np.int64)
         self.received = np.zeros((self.E, s.N), dtype=np.int64)
         self.discarded = np.zeros((self.E, s.N), dtype=np.int64)
         self.sel_q = np.zeros(self.E, dtype=np.int64)
@@ -140,6 +158,10 @@ class EnvOracle:
         if replay is not None:
             return np.asarray(replay, dtype=np.int64)
         envs = self.env_base + np.arange(self.E, dtype=np.uint64)
+        if self.kind == "single":  # one word per (env, agent) against the agent's switch threshold
+            r = philox.words(envs[:, None], np.arange(s.N, dtype=np.uint64)[None, :], rng_step,
+                             philox.STREAM_FLIP, 1, self.seed)[..., 0]
+            return (r < philox.threshold(s.switch)[None]).astype(np.int64)
         if self.kind == "comb":
             r = philox.words(envs[:, None], np.arange(s.N, dtype=np.uint64)[None, :], rng_step,
                              philox.STREAM_FLIP, s.C, self.seed)
@@ -156,6 +178,15 @@ class EnvOracle:
         s = self.spec
         obs = np.zeros((self.E, s.N, s.F), dtype=np.float64)
         state = np.zeros((self.E, s.S), dtype=np.float64)
+        if self.kind == "single":
+            for e in range(self.E):
+                for k in range(s.N):
+                    nb = s.nbr[k]
+                    row = np.concatenate([self.buffers[e, j, :s.d[j]] for j in nb] + [self.chan[e, nb], ack[e]])
+                    obs[e, k, :row.shape[0]] = row                                   # env.py:91-95 / 198-202
+                allb = np.concatenate([self.buffers[e, k, :s.d[k]] for k in range(s.N)])
+                state[e] = np.concatenate([allb, self.chan[e], ack[e]])              # env.py:97-98 / 204-205
+            return obs, state
         for e in range(self.E):
             for k in range(s.N):
                 w = s.w[k]
@@ -186,7 +217,12 @@ class EnvOracle:
         self.received[:] = self.buffers.sum(2)
         self.sel_q[:] = 0
         self.sel_n[:] = 0
-        if self.kind == "comb":
+        self.channel_errors[:] = 0
+        self.n_collisions[:] = 0
+        self.successful_transmissions[:] = 0
+        if self.kind == "single":
+            obs, state = self._obs_state(None, np.zeros((self.E, 1)))   # last_feedback = 0 (env.py:85)
+        elif self.kind == "comb":
             chan_obs = np.ones((self.E, s.N, s.C))
             ack = np.ones((self.E, s.C))   # reset state/obs use ones (combinatorial_env.py:108-112)
             obs, state = self._obs_state(chan_obs, ack)
@@ -205,6 +241,8 @@ class EnvOracle:
         actions = np.asarray(actions)
         rewards = np.zeros(E, dtype=np.int64)
         success = np.zeros((E, N), dtype=bool)
+        if self.kind == "single":
+            return self._step_single(actions, rng_step, flips, arrivals)
         if self.kind == "comb":
             ack = np.zeros((E, C))
         else:
@@ -256,6 +294,54 @@ class EnvOracle:
                     buffers=self.buffers.copy(), chan=self.chan.copy(), received=self.received.copy(),
                     discarded=self.discarded.copy(), sel_q=self.sel_q.copy(), sel_n=self.sel_n.copy(),
                     flips=F, arrivals=arr)
+
+    def _step_single(self, actions, rng_step, flips, arrivals):
+        """D2DEnv.step (env.py:116-213) for every env; self.timestep already incremented."""
+        s = self.spec
+        t = self.timestep
+        E, N = self.E, s.N
+        actions = np.asarray(actions).reshape(E, N)
+        ack = np.zeros((E, 1))
+        success = np.zeros((E, N), dtype=bool)
+        nxt = self.buffers.copy()
+        for e in range(E):
+            has = (self.buffers[e].sum(1) > 0) * 1.                                 # 124
+            att = (actions[e] != 0) * has                                           # 125
+            n_att = att.sum()                                                       # 126
+            if n_att == 1:                                                          # 129
+                idx = int(att.nonzero()[0][0])
+                decoded = self.chan[e, idx]   # binomial(1, channel_state[idx]), state in {0, 1} (101-103)
+                if decoded:
+                    a = 1                                                           # 136
+                    self.successful_transmissions[e] += 1
+                    col = nxt[e, idx].nonzero()[0]                                  # 141-142
+                    nxt[e, idx, col.min()] -= 1
+                    success[e, idx] = True
+                else:
+                    a = 0                                                           # 144-145
+                    self.channel_errors[e] += 1
+            elif n_att > 1:
+                a = -1                                                              # 147-148
+                self.n_collisions[e] += 1
+            else:
+                a = 0                                                               # 150
+            ack[e, 0] = a
+        expired = nxt[:, :, 0].copy()                                               # 109-113, 155-156
+        nxt = np.concatenate([nxt[:, :, 1:], np.zeros((E, N, 1), dtype=np.int64)], axis=2)
+        self.discarded += expired
+        Fl = self._flips(rng_step, flips)                                           # 105-107, 157
+        self.chan = np.where(Fl != 0, 1 - self.chan, self.chan)
+        arr, draws = self._arrivals(t, rng_step, arrivals)                         # 160-181
+        for (i, _k) in draws:
+            nxt[:, i, s.d[i] - 1] = arr[:, i]
+            self.received[:, i] += arr[:, i]
+        self.buffers = nxt
+        obs, state = self._obs_state(None, ack)                                     # 184-205
+        done = t >= s.episode_length                                                # 223-226
+        return dict(obs=obs, state=state, rewards=ack[:, 0].copy(), done=done, ack=ack, success=success,
+                    buffers=self.buffers.copy(), chan=self.chan.copy(), received=self.received.copy(),
+                    discarded=self.discarded.copy(), channel_errors=self.channel_errors.copy(),
+                    n_collisions=self.n_collisions.copy(), flips=Fl, arrivals=arr)
 
     # -------------------------------------------------------------- metrics
     def compute_jains(self):

@@ -207,6 +207,132 @@ def gen_env():
         run_env(name, kind, params, episodes, p_act)
 
 
+def d2denv_configs():
+    """D2DEnv (envs/env.py) cases: test.ipynb cell 5, a busier one with full neighbourhoods and
+    channel flips, ring neighbourhoods with mixed deadlines, the heterogeneous and periodic
+    traffic models, a single agent."""
+    ring = lambda n: [[(k - 1) % n, k, (k + 1) % n] for k in range(n)]  # noqa: E731
+    return [
+        ("4_notebook", dict(n_agents=4, deadlines=np.array([7] * 4), lbdas=np.array([1 / 14] * 4), period=None,
+                            arrival_probs=None, offsets=None, episode_length=200, traffic_model="aperiodic",
+                            periodic_devices=[], reward_type=0, channel_switch=0, channel_decoding=1.,
+                            neighbourhoods=[[i] for i in range(4)]), 2, 0.3),
+        ("6_full_nbr", dict(n_agents=6, deadlines=np.array([4, 7, 5, 7, 3, 6]), lbdas=np.array([0.4] * 6),
+                            episode_length=80, traffic_model="aperiodic", channel_switch=0.3,
+                            neighbourhoods=[list(range(6)) for _ in range(6)]), 2, 0.25),
+        ("8_ring_het", dict(n_agents=8, deadlines=np.array([7, 3, 5, 7, 2, 6, 7, 4]), lbdas=np.array([0.6] * 8),
+                            period=np.array([2, 3, 2, 3, 2, 3, 2, 3]), arrival_probs=np.array([0.9, 0.5] * 4),
+                            offsets=np.array([0, 1, 0, 2, 1, 0, 0, 1]), episode_length=60,
+                            traffic_model="heterogeneous", periodic_devices=[1, 3, 5],
+                            channel_switch=np.array([0.1, 0.5, 0.2, 0.3, 0.05, 0.4, 0.25, 0.15]),
+                            neighbourhoods=ring(8)), 2, 0.2),
+        ("5_periodic", dict(n_agents=5, deadlines=np.array([5] * 5), lbdas=np.array([1.0] * 5), period=3,
+                            arrival_probs=np.array([1.0, 0.7, 0.5, 0.9, 0.8]), offsets=np.array([0, 1, 2, 0, 1]),
+                            episode_length=40, traffic_model="periodic", channel_switch=0.2,
+                            neighbourhoods=[[0, 4], [1, 0], [2], [3, 2, 1], [4, 3]]), 2, 0.35),
+        ("1_single", dict(n_agents=1, deadlines=np.array([3]), lbdas=np.array([1.5]), episode_length=30,
+                          traffic_model="aperiodic", channel_switch=0.4), 2, 0.6),
+    ]
+
+
+def run_d2denv(name, params, episodes, p_act, seed=42):
+    """Record a D2DEnv trace (envs/env.py).  Draws recovered from state diffs: the channel flip
+    mask |H_after - H_before| and the arrivals B_after[k, d_k - 1]; the decode draw needs no
+    record (the channel state is 0/1, so binomial(1, state) is the state, env.py:101-103)."""
+    mod = ref_module("envs.env")
+    env = mod.D2DEnv(**params)
+    N = env.n_agents
+    d = np.asarray(env.deadlines)
+    nbr = env.neighbourhoods
+    obs_len = np.array([int(d[nb].sum()) + len(nb) + 1 for nb in nbr])
+    F = int(obs_len.max())
+    act_rng = np.random.default_rng(4321)
+    np.random.seed(seed)
+
+    def pad_obs(obs):
+        out = np.zeros((N, F))
+        for k in range(N):
+            assert obs[k].shape[0] == obs_len[k]
+            out[k, :obs_len[k]] = obs[k]
+        return out
+
+    rec = {k: [] for k in ["actions", "flips", "arrivals", "obs", "state", "rewards", "done", "ack", "buffers",
+                           "chan", "received", "discarded", "channel_errors", "n_collisions", "success"]}
+    rrec = {k: [] for k in ["arrivals", "obs", "state", "buffers", "chan", "received"]}
+    metrics = {k: [] for k in ["jains", "urllc", "successful_transmissions", "channel_errors", "n_collisions"]}
+    for ep in range(episodes):
+        obs, state = env.reset()
+        rrec["arrivals"].append(np.array([env.current_buffers[k, d[k] - 1] for k in range(N)]))
+        rrec["obs"].append(pad_obs(obs))
+        rrec["state"].append(np.asarray(state, dtype=np.float64))
+        rrec["buffers"].append(env.current_buffers.copy())
+        rrec["chan"].append(np.array(env.channel_state, dtype=np.float64).copy())
+        rrec["received"].append(env.received_packets.copy())
+        done = False
+        t = 0
+        while not done:
+            p = p_act if t % 13 else 1.0        # every 13th step: everyone attempts (collisions)
+            a = (act_rng.random(N) < p).astype(np.int64)
+            if t % 19 == 4:
+                a[:] = 0                         # nobody attempts
+            if t % 7 == 3:
+                a[:] = 0
+                a[act_rng.integers(0, N)] = 1    # exactly one attempt (decode / channel error)
+            H0 = np.array(env.channel_state, dtype=np.float64).copy()
+            ltt0 = env.last_time_transmitted.copy()
+            obs, state, rew, done, info = env.step(a)
+            H1 = np.array(env.channel_state, dtype=np.float64).copy()
+            rec["actions"].append(a)
+            rec["flips"].append(np.abs(H1 - H0).astype(np.uint8))
+            rec["arrivals"].append(np.array([env.current_buffers[k, d[k] - 1] for k in range(N)]))
+            rec["obs"].append(pad_obs(obs))
+            rec["state"].append(np.asarray(state, dtype=np.float64))
+            rec["rewards"].append(np.asarray(rew, dtype=np.float64))
+            rec["done"].append(done)
+            rec["ack"].append(float(env.last_feedback))
+            rec["buffers"].append(env.current_buffers.copy())
+            rec["chan"].append(H1)
+            rec["received"].append(env.received_packets.copy())
+            rec["discarded"].append(env.discarded_packets.copy())
+            rec["channel_errors"].append(env.channel_errors)
+            rec["n_collisions"].append(env.n_collisions)
+            rec["success"].append((env.last_time_transmitted == 1.0) & (ltt0 + 1 != 1.0))
+            t += 1
+        metrics["jains"].append(env.compute_jains())
+        metrics["urllc"].append(env.compute_urllc())
+        metrics["successful_transmissions"].append(env.successful_transmissions)
+        metrics["channel_errors"].append(env.channel_errors)
+        metrics["n_collisions"].append(env.n_collisions)
+    out = {"params_json": json.dumps({k: _jsonable(v) for k, v in params.items()}), "kind": "single",
+           "episodes": episodes, "obs_len": obs_len, "state_dim": env.state_space.shape[0],
+           "obs_dims": np.array([env.observation_space[k].shape[0] for k in range(N)]),
+           "action_n": np.array([env.action_space[k].n for k in range(N)])}
+    for k, v in rec.items():
+        out[k] = np.array(v)
+    for k, v in rrec.items():
+        out["reset_" + k] = np.array(v)
+    for k, v in metrics.items():
+        out["metric_" + k] = np.array(v)
+    for k in ("buffers", "reset_buffers", "arrivals", "reset_arrivals"):
+        assert out[k].max() < 256
+        out[k] = out[k].astype(np.uint8)
+    for k in ("chan", "reset_chan", "actions"):
+        out[k] = out[k].astype(np.uint8)
+    for k in ("obs", "reset_obs", "state", "reset_state"):
+        out[k] = out[k].astype(np.float32)
+    assert np.all(np.isin(out["ack"], (-1.0, 0.0, 1.0)))
+    out["ack"] = out["ack"].astype(np.int8)
+    np.savez_compressed(os.path.join(OUT, f"d2denv_{name}.npz"), **out)
+    print(f"d2denv_{name}: steps={len(rec['done'])} acks(+1/0/-1)="
+          f"{[(out['ack'] == v).sum() for v in (1, 0, -1)]} urllc={metrics['urllc']} "
+          f"chan_err={metrics['channel_errors']}")
+
+
+def gen_d2denv():
+    for name, params, episodes, p_act in d2denv_configs():
+        run_d2denv(name, params, episodes, p_act)
+
+
 def gen_gae():
     ippo = ref_module("algorithms.ippo")
     d2d = ref_module("algorithms.d2d_ppo")
@@ -428,6 +554,6 @@ def gen_learner():
 
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    which = sys.argv[1:] or ["data", "env", "gae", "learner"]
+    which = sys.argv[1:] or ["data", "env", "d2denv", "gae", "learner"]
     for w in which:
-        {"data": gen_data, "env": gen_env, "gae": gen_gae, "learner": gen_learner}[w]()
+        {"data": gen_data, "env": gen_env, "d2denv": gen_d2denv, "gae": gen_gae, "learner": gen_learner}[w]()
