@@ -238,7 +238,7 @@ class BatchedLearnerBase(DataParallelMixin):
         rew_i32 = torch.empty((T, E), dtype=torch.int32, device=dev)
         val_buf = torch.empty((T, N, E), dtype=torch.float32, device=dev) if want_values else None
         state_buf = torch.empty((T, E, s.state_stride), dtype=torch.float32, device=dev) if want_state else None
-        scores, ep_rewards, jains = [], [], []
+        scores, ep_rewards, jains, ch_errors = [], [], [], []
         tf = self._teacher_tensors(teacher, b, T) if teacher is not None else None
         with torch.no_grad():
             for w in range(waves):
@@ -261,10 +261,13 @@ class BatchedLearnerBase(DataParallelMixin):
                 ep_rewards.extend(rew_i32[t0:t0 + L].double().sum(0).cpu().tolist())
                 if not train:
                     jains.extend(self._jains(b))
+                    if s.kind == "single":  # D2DEnv.channel_errors of the episode (env.py:144-145)
+                        ch_errors.extend(b.sel_quality.cpu().tolist())
         dones = torch.zeros(T, dtype=torch.uint8, device=dev)
         dones[L - 1::L] = 1
         return Rollout(obs=obs_buf, actions=act_buf, logp=logp_buf, rewards=rew_i32.float(), values=val_buf,
-                       states=state_buf, dones=dones, scores=scores, ep_rewards=ep_rewards, jains=jains, T=T, E=E,
+                       states=state_buf, dones=dones, scores=scores, ep_rewards=ep_rewards, jains=jains,
+                       ch_errors=ch_errors, T=T, E=E,
                        waves=waves, L=L)
 
     def _teacher_tensors(self, teacher, b, T):
@@ -283,6 +286,8 @@ class BatchedLearnerBase(DataParallelMixin):
         for i in range(T):
             if s.kind == "comb":
                 f = torch.from_numpy(np.ascontiguousarray(pack_masks(fl[i][None], s.C))).to(dev)
+            elif s.kind == "single":
+                f = torch.from_numpy(np.ascontiguousarray(fl[i].reshape(1, s.N).astype(np.uint8))).to(dev)
             else:
                 word = int((fl[i].astype(np.int64) << np.arange(fl[i].shape[-1])).sum())
                 f = torch.tensor([word], dtype=torch.int32, device=dev)
@@ -335,11 +340,13 @@ class BatchedLearnerBase(DataParallelMixin):
         sc = np.array(ro.scores[:n], dtype=np.float64)
         ja = np.array(ro.jains[:n], dtype=np.float64)
         rw = np.array(ro.ep_rewards[:n], dtype=np.float64)
-        ch = 0  # channel_errors is never incremented by these envs (combinatorial_env.py:97)
-        out = [np.mean(sc), np.mean(ja), np.sum([ch] * n), np.mean(rw)]
+        # channel_errors is never incremented by the comb / chsel envs (combinatorial_env.py:97);
+        # the D2DEnv counts failed single attempts (env.py:144-145), summed over episodes (ippo.py:385-388)
+        ch = float(np.sum(ro.ch_errors[:n])) if ro.ch_errors else 0
+        out = [np.mean(sc), np.mean(ja), ch, np.mean(rw)]
         if getattr(self, "world_size", 1) > 1:  # every rank must take the same save / early-stop branch
             out = [allreduce_mean_scalar(v, self.device, self.process_group) for v in out]
-            out[2] = 0
+            out[2] = out[2] * self.world_size  # channel errors are a sum over every rank's episodes
         return tuple(out)
 
     # --------------------------------------------------------- save/load

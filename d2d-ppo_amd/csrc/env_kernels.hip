@@ -49,6 +49,7 @@ struct EnvArgs {
   int32_t* reward;
   void* ack;
   uint8_t* success;
+  const int32_t* gather;  // single: [N*F + S] obs/state gather codes
   uint64_t draw[kMaxAgents / 64];
 };
 
@@ -631,6 +632,146 @@ __global__ __launch_bounds__(kMaxAgents) void chsel_kernel(EnvArgs a) {
 
 
 // =====================================================================
+// D2DEnv: one shared channel, Discrete(2) actions, neighbourhood observations
+// (/root/reference/envs/env.py: reset 51-99, decode_signal 101-103,
+// evolve_channel 105-107, evolve_buffer 109-113, step 116-213).
+// One lane = one agent; an env is a lane segment (N <= 64) or a workgroup.
+//   n_attempts = #(action != 0 and has a packet).  Exactly one attempt is
+//   decoded with probability channel_state[idx], and that state only ever
+//   flips between 0 and 1 (reset ones, env.py:78; 1 - state, 105-107), so the
+//   decode is the attempter's channel bit.  ack = 1 decoded / 0 channel error
+//   or silence / -1 collision; every agent's reward is ack (207).
+// obs_k = [B'[j,:d_j] for j in nbr(k)] + [H'[j] for j in nbr(k)] + [ack]
+//   (post-evolve channel, 198-202) gathered from the env's rows staged in LDS
+//   and written straight to HBM (full neighbourhoods make rows long:
+//   F = sum d + N + 1); state = [concat_k B'[k,:d_k], H', ack] (204-205).
+// Counters: sel_quality = channel_errors, sel_count = n_collisions.
+// =====================================================================
+template <int DW, bool LARGE>
+__global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Lane L = lane_geometry<LARGE>(a);
+  const int N = a.N, F = a.F;
+  int* cnt = reinterpret_cast<int*>(lds) + L.local_env * 4;
+  uint32_t* rows = reinterpret_cast<uint32_t*>(lds) + a.cnt_words + (size_t)L.local_env * N * (DW + 1);
+  const size_t row = (size_t)L.env * N + L.k;
+  const uint64_t genv = a.env_base + (uint64_t)L.env;
+  const bool env_ok = L.env < a.E;
+
+  Row<DW> b;
+#pragma unroll
+  for (int i = 0; i < DW; ++i) b.w[i] = 0;
+  uint32_t h = 1, act = 0, rc = 0, dc = 0;
+  d2d_agent_entry ag{};
+  if (L.active) {
+    ag = a.agents[L.k];
+    if (!a.reset) {
+      load_row<DW>(b, a.buf + row * DW);
+      h = reinterpret_cast<const uint8_t*>(a.chan)[row] & 1u;
+      act = reinterpret_cast<const uint8_t*>(a.actions)[row];
+      rc = a.recv[row];
+      dc = a.disc[row];
+    }
+  }
+  if (LARGE) {
+    if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
+    __syncthreads();
+  }
+  int ackv = 0, n = 0, ng = 0;
+  bool succ = false;
+  uint32_t h_new = 1;  // reset: channel_state = ones (78)
+  if (!a.reset) {
+    const bool att = L.active && act != 0 && row_any<DW>(b);   // attempts = actions * has_a_packet (124-125)
+    n = env_count<LARGE>(att, L, cnt);                          // n_attempts (126)
+    ng = env_count<LARGE>(att && h != 0, L, cnt + 1);
+    const bool decoded = n == 1 && ng == 1;                     // decode_signal (101-103, 133)
+    ackv = n == 1 ? (decoded ? 1 : 0) : (n > 1 ? -1 : 0);       // 134-152
+    succ = att && decoded;
+    if (succ) row_remove_first<DW>(b);                          // 141-142
+    dc += row_expire_shift<DW>(b);                              // 155-156
+    uint32_t f = 0;                                             // evolve_channel (157, 105-107)
+    if (L.active) {
+      if (a.flips) {
+        f = reinterpret_cast<const uint8_t*>(a.flips)[row] & 1u;
+      } else {
+        const u32x4 r = philox((uint32_t)genv, (uint32_t)L.k, a.rng_step, kStreamFlip << 24, a.seed);
+        f = (uint64_t)r.x < a.flip_thr[L.k] ? 1u : 0u;
+      }
+    }
+    h_new = h ^ f;
+  }
+  // arrivals (reset 56-76, step 160-181)
+  const bool drew = L.active && draws_now(a, L.k);
+  if (drew) {
+    const uint32_t x = arrival_value(a, ag, row, L.k, genv);
+    row_set<DW>(b, (int)ag.deadline - 1, x);
+    rc = (a.reset ? 0u : rc) + x;
+  }
+  if (a.reset) {
+    rc = drew ? rc : 0u;
+    dc = 0;
+  }
+  if (L.active) {
+    store_row<DW>(b, a.buf + row * DW);
+    reinterpret_cast<uint8_t*>(a.chan)[row] = (uint8_t)h_new;
+    a.recv[row] = rc;
+    a.disc[row] = dc;
+    if (a.success && !a.reset) a.success[row] = succ ? 1 : 0;
+  }
+  if (env_ok && L.k == 0) {
+    if (!a.reset) {
+      if (a.reward) a.reward[L.env] = ackv;                          // rewards = ack (207)
+      if (a.ack) reinterpret_cast<int8_t*>(a.ack)[L.env] = (int8_t)ackv;
+      a.selq[L.env] += (n == 1 && ng != 1) ? 1 : 0;                   // channel_errors (144-145)
+      a.seln[L.env] += n > 1 ? 1 : 0;                                 // n_collisions (147-148)
+    } else {
+      a.selq[L.env] = 0;
+      a.seln[L.env] = 0;
+    }
+  }
+  // The env's rows + channel bits go to LDS; the block then writes its envs'
+  // contiguous obs range [epb][N][F] (and state rows) cooperatively, one float
+  // per lane per store (coalesced), each element resolved through the gather
+  // table: j*64+q = byte q of agent j's row, j*64+32 = agent j's channel, -1 ack.
+  if (L.active) {
+#pragma unroll
+    for (int i = 0; i < DW; ++i) rows[L.k * (DW + 1) + i] = b.w[i];
+    rows[L.k * (DW + 1) + DW] = h_new;
+  }
+  if (L.k == 0) cnt[2] = ackv;
+  __syncthreads();
+  const int epb = L.envs_per_block;
+  const int env0 = LARGE ? blockIdx.x : blockIdx.x * epb;
+  const int nenv = min(epb, a.E - env0);
+  const bool nt = a.flags & 1u;
+  const uint32_t* rows0 = reinterpret_cast<const uint32_t*>(lds) + a.cnt_words;
+  const int* cnt0 = reinterpret_cast<const int*>(lds);
+  auto resolve = [&](int le, int code) -> float {
+    if (code == -2) return 0.f;
+    if (code == -1) return (float)cnt0[le * 4 + 2];
+    const int j = code >> 6, q = code & 63;
+    const uint32_t* rj = rows0 + ((size_t)le * N + j) * (DW + 1);
+    if (q == 32) return (float)rj[DW];
+    return (float)((rj[q >> 2] >> ((q & 3) * 8)) & 0xFFu);
+  };
+  if (a.obs && nenv > 0) {
+    const int per = N * F;
+    float* dst = a.obs + (size_t)env0 * per;
+    for (int i = threadIdx.x; i < nenv * per; i += blockDim.x) {
+      const int le = i / per, r = i - le * per;
+      st_stream(dst + i, resolve(le, a.gather[r]), nt);
+    }
+  }
+  if (a.state && nenv > 0) {
+    const int* gs = a.gather + (size_t)N * F;
+    for (int i = threadIdx.x; i < nenv * a.S; i += blockDim.x) {
+      const int le = i / a.S, r = i - le * a.S;
+      st_stream(a.state + (size_t)(env0 + le) * a.state_stride + r, resolve(le, gs[r]), nt);
+    }
+  }
+}
+
+// =====================================================================
 // synthetic actions (env-only benchmark / baseline policies)
 // =====================================================================
 template <typename MaskT>
@@ -641,9 +782,14 @@ __global__ __launch_bounds__(256) void sample_actions_kernel(int E, int N, int C
   if (i >= (int64_t)E * N) return;
   const int env = (int)(i / N), k = (int)(i - (int64_t)env * N);
   const uint32_t genv = (uint32_t)(env_base + (uint64_t)env);
-  if (chsel) {
+  if (chsel == 1) {
     const u32x4 r = philox(genv, (uint32_t)k, rng_step, kStreamAction << 24, seed);
     reinterpret_cast<uint8_t*>(out)[i] = (uint8_t)(((uint64_t)r.x * (uint64_t)(C + 1)) >> 32);
+    return;
+  }
+  if (chsel == 2) {  // single channel: transmit with probability thr / 2^32 (GFAccess.act, baselines.py:121-125)
+    const u32x4 r = philox(genv, (uint32_t)k, rng_step, kStreamAction << 24, seed);
+    reinterpret_cast<uint8_t*>(out)[i] = (uint8_t)((uint64_t)r.x < thr ? 1 : 0);
     return;
   }
   uint32_t m = 0;
@@ -683,7 +829,19 @@ int buffer_words(int D) { return D <= 4 ? 1 : D <= 8 ? 2 : D <= 12 ? 3 : D <= 16
 int check_desc(const d2d_env_desc* d) {
   if (!d) { d2d_set_error("desc is NULL"); return D2D_EINVAL; }
   const bool comb = d->env_kind == D2D_ENV_COMBINATORIAL;
-  if (!comb && d->env_kind != D2D_ENV_CHANNEL_SELECTION) { d2d_set_error("unknown env_kind %d", d->env_kind); return D2D_EINVAL; }
+  const bool single = d->env_kind == D2D_ENV_SINGLE;
+  if (!comb && !single && d->env_kind != D2D_ENV_CHANNEL_SELECTION) { d2d_set_error("unknown env_kind %d", d->env_kind); return D2D_EINVAL; }
+  if (single) {
+    if (d->n_agents < 1 || d->n_agents > kMaxAgents) { d2d_set_error("n_agents=%d outside [1,%d]", d->n_agents, kMaxAgents); return D2D_EUNSUPPORTED; }
+    if (d->n_channels != 1) { d2d_set_error("the single-channel env needs n_channels == 1"); return D2D_EINVAL; }
+    if (d->max_deadline < 1 || d->max_deadline > 32) { d2d_set_error("max_deadline=%d outside [1,32]", d->max_deadline); return D2D_EUNSUPPORTED; }
+    if (d->n_envs < 0) { d2d_set_error("n_envs < 0"); return D2D_EINVAL; }
+    if (d->obs_dim < 2 || d->state_dim != 0 && d->state_stride < d->state_dim) { d2d_set_error("bad obs/state dims"); return D2D_EINVAL; }
+    if (!d->agents || !d->flip_thr || !d->arrival_kind_host || !d->period_host || !d->offset_host || !d->gather) {
+      d2d_set_error("desc tables (incl. the gather map) must be non-NULL"); return D2D_EINVAL;
+    }
+    return D2D_OK;
+  }
   if (d->n_agents < 1 || d->n_agents > kMaxAgents) { d2d_set_error("n_agents=%d outside [1,%d]", d->n_agents, kMaxAgents); return D2D_EUNSUPPORTED; }
   if (d->n_channels < 1 || d->n_channels > (comb ? 32 : 31)) { d2d_set_error("n_channels=%d unsupported", d->n_channels); return D2D_EUNSUPPORTED; }
   if (d->max_deadline < 1 || d->max_deadline > 32) { d2d_set_error("max_deadline=%d outside [1,32]", d->max_deadline); return D2D_EUNSUPPORTED; }
@@ -718,9 +876,14 @@ int set_lds(K kernel, size_t bytes) {
 }
 
 // dynamic LDS of one workgroup (must match the carve in the kernels)
-size_t lds_need(const EnvArgs& a, int block, bool comb) {
+size_t lds_need(const EnvArgs& a, int block, int kind) {
   const bool large = a.N > kWave;
   const bool stage = a.obs || a.state;
+  const bool comb = kind == D2D_ENV_COMBINATORIAL;
+  if (kind == D2D_ENV_SINGLE) {
+    const int epb = large ? 1 : block / a.seg;
+    return sizeof(float) * ((size_t)a.cnt_words + (size_t)epb * a.N * (a.D <= 4 ? 2 : a.D <= 8 ? 3 : a.D <= 12 ? 4 : a.D <= 16 ? 5 : 9));
+  }
   if (comb) {
     const int nwaves = block / kWave;
     const int epw = large ? 1 : kWave / a.seg;
@@ -735,12 +898,12 @@ size_t lds_need(const EnvArgs& a, int block, bool comb) {
 }
 
 template <typename K>
-int launch(K kernel, const EnvArgs& a, int block, hipStream_t s, bool comb) {
+int launch(K kernel, const EnvArgs& a, int block, hipStream_t s, int kind) {
   const bool large = a.N > kWave;
   const int epb = large ? 1 : block / a.seg;
   const int grid = (a.E + epb - 1) / epb;
   if (grid == 0) return D2D_OK;
-  const size_t lds = lds_need(a, block, comb);
+  const size_t lds = lds_need(a, block, kind);
   int rc = set_lds(kernel, lds);
   if (rc) return rc;
   hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), lds, s, a);
@@ -750,8 +913,8 @@ int launch(K kernel, const EnvArgs& a, int block, hipStream_t s, bool comb) {
 
 template <typename MaskT, int DW, int CT, bool RESET>
 int dispatch_comb_ct(const EnvArgs& a, int block, hipStream_t s) {
-  if (a.N > kWave) return launch(comb_kernel<MaskT, DW, true, CT, RESET>, a, block, s, true);
-  return launch(comb_kernel<MaskT, DW, false, CT, RESET>, a, block, s, true);
+  if (a.N > kWave) return launch(comb_kernel<MaskT, DW, true, CT, RESET>, a, block, s, D2D_ENV_COMBINATORIAL);
+  return launch(comb_kernel<MaskT, DW, false, CT, RESET>, a, block, s, D2D_ENV_COMBINATORIAL);
 }
 
 template <int DW>
@@ -771,11 +934,14 @@ int dispatch_comb(const EnvArgs& a, int block, hipStream_t s) {
 }
 
 template <int DW>
-int dispatch_dw(const EnvArgs& a, int block, bool comb, int C, hipStream_t s) {
-  (void)C;
-  if (!comb) {
-    if (a.N > kWave) return launch(chsel_kernel<DW, true>, a, block, s, false);
-    return launch(chsel_kernel<DW, false>, a, block, s, false);
+int dispatch_dw(const EnvArgs& a, int block, int kind, hipStream_t s) {
+  if (kind == D2D_ENV_SINGLE) {
+    if (a.N > kWave) return launch(single_kernel<DW, true>, a, block, s, kind);
+    return launch(single_kernel<DW, false>, a, block, s, kind);
+  }
+  if (kind == D2D_ENV_CHANNEL_SELECTION) {
+    if (a.N > kWave) return launch(chsel_kernel<DW, true>, a, block, s, kind);
+    return launch(chsel_kernel<DW, false>, a, block, s, kind);
   }
   return dispatch_comb<DW>(a, block, s);
 }
@@ -788,7 +954,10 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
     d2d_set_error("state buffers must be non-NULL"); return D2D_EINVAL;
   }
   const bool comb = d->env_kind == D2D_ENV_COMBINATORIAL;
-  if (!comb && (!st->sel_quality || !st->sel_count)) { d2d_set_error("chsel needs sel_quality/sel_count"); return D2D_EINVAL; }
+  const int kind = d->env_kind;
+  if (!comb && (!st->sel_quality || !st->sel_count)) {
+    d2d_set_error("chsel / single need sel_quality / sel_count"); return D2D_EINVAL;
+  }
   if (!reset && !actions) { d2d_set_error("actions is NULL"); return D2D_EINVAL; }
   EnvArgs a;
   memset(&a, 0, sizeof(a));
@@ -798,6 +967,7 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
   a.buf = st->buffers; a.chan = st->channels; a.recv = st->received; a.disc = st->discarded;
   a.selq = st->sel_quality; a.seln = st->sel_count; a.actions = actions;
   if (rp) { a.flips = rp->flips; a.arrivals = rp->arrivals; }
+  a.gather = d->gather;
   if (out) { a.obs = out->obs; a.state = out->state; a.reward = out->reward; a.ack = out->ack; a.success = out->success; }
   draw_mask(d, reset ? 0 : t, a.draw);
   a.flags = store_flags();
@@ -807,20 +977,22 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
   a.seg = large ? ((a.N + kWave - 1) / kWave) * kWave : seg;
   // block: 256 lanes (4 waves) unless the LDS staging of that many envs would
   // exceed 64 KiB (keep >= 2 workgroups per CU); LARGE: one env per block
-  auto cnt_words = [&](int epb) { return comb ? (large ? 80 : 0) : (((epb * 34) + 3) & ~3); };
+  auto cnt_words = [&](int epb) {
+    return kind == D2D_ENV_SINGLE ? epb * 4 : comb ? (large ? 80 : 0) : (((epb * 34) + 3) & ~3);
+  };
   int block = large ? a.seg : 256;
   a.cnt_words = cnt_words(large ? 1 : block / a.seg);
-  while (!large && block > kWave && block > a.seg && lds_need(a, block, comb) > 65536) {
+  while (!large && block > kWave && block > a.seg && lds_need(a, block, kind) > 65536) {
     block >>= 1;
     a.cnt_words = cnt_words(block / a.seg);
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   switch (buffer_words(a.D)) {
-    case 1: return dispatch_dw<1>(a, block, comb, a.C, s);
-    case 2: return dispatch_dw<2>(a, block, comb, a.C, s);
-    case 3: return dispatch_dw<3>(a, block, comb, a.C, s);
-    case 4: return dispatch_dw<4>(a, block, comb, a.C, s);
-    default: return dispatch_dw<8>(a, block, comb, a.C, s);
+    case 1: return dispatch_dw<1>(a, block, kind, s);
+    case 2: return dispatch_dw<2>(a, block, kind, s);
+    case 3: return dispatch_dw<3>(a, block, kind, s);
+    case 4: return dispatch_dw<4>(a, block, kind, s);
+    default: return dispatch_dw<8>(a, block, kind, s);
   }
 }
 
@@ -842,6 +1014,48 @@ extern "C" int d2d_set_option(int32_t option, int32_t value) {
 }
 
 extern "C" int d2d_buffer_words(int32_t max_deadline) { return buffer_words(max_deadline); }
+
+extern "C" int d2d_env_single_gather_map(int32_t n_agents, const int32_t* deadlines, const int32_t* nbr_ptr,
+                                          const int32_t* nbr_idx, int32_t obs_dim, int32_t* out, int64_t out_len) {
+  const int N = n_agents;
+  if (N < 1 || N > d2d::kMaxAgents || !deadlines || !nbr_ptr || !nbr_idx || !out) {
+    d2d_set_error("gather map: bad arguments"); return D2D_EINVAL;
+  }
+  int64_t S = N + 1;
+  for (int k = 0; k < N; ++k) {
+    if (deadlines[k] < 1 || deadlines[k] > 32) { d2d_set_error("gather map: deadline[%d]=%d", k, deadlines[k]); return D2D_EINVAL; }
+    S += deadlines[k];
+  }
+  const int64_t need = (int64_t)N * obs_dim + S;
+  if (obs_dim < 1 || out_len < need) { d2d_set_error("gather map: out_len %lld < %lld", (long long)out_len, (long long)need); return D2D_EINVAL; }
+  if (nbr_ptr[0] != 0) { d2d_set_error("gather map: nbr_ptr[0] != 0"); return D2D_EINVAL; }
+  for (int k = 0; k < N; ++k) {
+    int32_t* o = out + (int64_t)k * obs_dim;
+    const int p0 = nbr_ptr[k], p1 = nbr_ptr[k + 1];
+    if (p1 < p0) { d2d_set_error("gather map: nbr_ptr not monotone"); return D2D_EINVAL; }
+    int64_t len = 1;
+    for (int p = p0; p < p1; ++p) {
+      if (nbr_idx[p] < 0 || nbr_idx[p] >= N) { d2d_set_error("gather map: neighbour %d out of range", nbr_idx[p]); return D2D_EINVAL; }
+      len += deadlines[nbr_idx[p]] + 1;
+    }
+    if (len > obs_dim) { d2d_set_error("gather map: agent %d needs obs_dim >= %lld", k, (long long)len); return D2D_EINVAL; }
+    int off = 0;
+    for (int p = p0; p < p1; ++p) {                 // buffers of the neighbours (env.py:91-92)
+      const int j = nbr_idx[p];
+      for (int q = 0; q < deadlines[j]; ++q) o[off++] = j * 64 + q;
+    }
+    for (int p = p0; p < p1; ++p) o[off++] = nbr_idx[p] * 64 + 32;   // their channel states (93)
+    o[off++] = -1;                                                     // last feedback (94)
+    while (off < obs_dim) o[off++] = -2;
+  }
+  int32_t* st = out + (int64_t)N * obs_dim;        // state (env.py:97-98)
+  int off = 0;
+  for (int k = 0; k < N; ++k)
+    for (int q = 0; q < deadlines[k]; ++q) st[off++] = k * 64 + q;
+  for (int k = 0; k < N; ++k) st[off++] = k * 64 + 32;
+  st[off++] = -1;
+  return (int)need;
+}
 
 extern "C" int d2d_mask_bytes(int32_t n_channels) { return n_channels <= 8 ? 1 : n_channels <= 16 ? 2 : 4; }
 
@@ -865,7 +1079,7 @@ extern "C" int d2d_sample_actions(const d2d_env_desc* d, void* actions, uint64_t
   if (n == 0) return D2D_OK;
   const int grid = (int)((n + 255) / 256);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int chsel = d->env_kind == D2D_ENV_CHANNEL_SELECTION;
+  const int chsel = d->env_kind == D2D_ENV_CHANNEL_SELECTION ? 1 : d->env_kind == D2D_ENV_SINGLE ? 2 : 0;
   const int C = d->n_channels;
   if (chsel || C <= 8)
     hipLaunchKernelGGL(sample_actions_kernel<uint8_t>, dim3(grid), dim3(256), 0, s, d->n_envs, d->n_agents, C, chsel,

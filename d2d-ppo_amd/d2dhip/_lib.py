@@ -14,9 +14,9 @@ import torch  # noqa: F401  (must be imported before the HIP library is loaded)
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libd2dhip.so")
 
-D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION = 0, 1
+D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 1
+ABI_VERSION = 2
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
 
@@ -28,7 +28,7 @@ class EnvDesc(ctypes.Structure):
                 ("max_deadline", ctypes.c_int32), ("obs_dim", ctypes.c_int32), ("state_dim", ctypes.c_int32),
                 ("state_stride", ctypes.c_int32), ("n_envs", ctypes.c_int32), ("env_base", ctypes.c_uint64),
                 ("seed", ctypes.c_uint64), ("agents", _p), ("flip_thr", _p), ("arrival_kind_host", _p),
-                ("period_host", _p), ("offset_host", _p)]
+                ("period_host", _p), ("offset_host", _p), ("gather", _p)]
 
 
 class EnvState(ctypes.Structure):
@@ -59,6 +59,7 @@ _SIGS = {
                                      ctypes.POINTER(EnvOut), ctypes.c_int32, ctypes.c_uint32, _p]),
     "d2d_sample_actions": (ctypes.c_int, [ctypes.POINTER(EnvDesc), _p, ctypes.c_uint64, ctypes.c_uint32, _p]),
     "d2d_mask_bytes": (ctypes.c_int, [ctypes.c_int32]),
+    "d2d_env_single_gather_map": (ctypes.c_int, [ctypes.c_int32, _p, _p, _p, ctypes.c_int32, _p, ctypes.c_int64]),
     "d2d_buffer_words": (ctypes.c_int, [ctypes.c_int32]),
     "d2d_gae_scan": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p, ctypes.c_double,
                                      ctypes.c_double, ctypes.c_int32, _p, _p, _p]),

@@ -9,7 +9,9 @@ import numpy as np
 import torch
 
 from . import _lib
-from .spec import COMB, EnvSpec
+from .spec import COMB, SINGLE, EnvSpec
+
+_KIND_ID = {COMB: _lib.D2D_ENV_COMBINATORIAL, "chsel": _lib.D2D_ENV_CHANNEL_SELECTION, SINGLE: _lib.D2D_ENV_SINGLE}
 
 _MASK_DTYPE = {1: torch.uint8, 2: torch.int16, 4: torch.int32}
 
@@ -36,6 +38,11 @@ class EnvBatch:
         if s.kind == COMB:
             self.channels = torch.zeros((E, s.N), dtype=_MASK_DTYPE[s.mask_bytes], device=dev)
             self.sel_quality = self.sel_count = None
+        elif s.kind == SINGLE:
+            # per-agent channel bit; sel_quality / sel_count hold channel_errors / n_collisions
+            self.channels = torch.zeros((E, s.N), dtype=torch.uint8, device=dev)
+            self.sel_quality = torch.zeros((E,), dtype=torch.int32, device=dev)
+            self.sel_count = torch.zeros((E,), dtype=torch.int32, device=dev)
         else:
             self.channels = torch.zeros((E,), dtype=torch.int32, device=dev)
             self.sel_quality = torch.zeros((E,), dtype=torch.int32, device=dev)
@@ -48,10 +55,12 @@ class EnvBatch:
         self._state = None
         self._ack = None
         self._success = None
+        self.gather = torch.from_numpy(spec.gather_map(self.lib)).to(dev) if s.kind == SINGLE else None
         self.desc = _lib.EnvDesc(
-            0 if s.kind == COMB else 1, s.N, s.C, s.D, s.F, s.S, s.state_stride, E, int(env_base),
+            _KIND_ID[s.kind], s.N, s.C, s.D, s.F, s.S, s.state_stride, E, int(env_base),
             int(seed) & 0xFFFFFFFFFFFFFFFF, self.agents.data_ptr(), self.flip_thr.data_ptr(),
-            self._kinds_host.ctypes.data, self._period_host.ctypes.data, self._offset_host.ctypes.data)
+            self._kinds_host.ctypes.data, self._period_host.ctypes.data, self._offset_host.ctypes.data,
+            None if self.gather is None else self.gather.data_ptr())
         self.st = _lib.EnvState(self.buffers.data_ptr(), self.channels.data_ptr(), self.received.data_ptr(),
                                 self.discarded.data_ptr(),
                                 None if self.sel_quality is None else self.sel_quality.data_ptr(),
@@ -72,6 +81,8 @@ class EnvBatch:
             s = self.spec
             if s.kind == COMB:
                 self._ack = torch.zeros((self.E, s.C), dtype=torch.int8, device=self.device)
+            elif s.kind == SINGLE:
+                self._ack = torch.zeros((self.E,), dtype=torch.int8, device=self.device)
             else:
                 self._ack = torch.zeros((self.E, s.C + 1), dtype=torch.float64, device=self.device)
         return self._ack
@@ -104,8 +115,8 @@ class EnvBatch:
         keep = []
         fp = ap = None
         if flips is not None:
-            want = (self.E, s.N) if s.kind == COMB else (self.E,)
-            dt = _MASK_DTYPE[s.mask_bytes] if s.kind == COMB else torch.int32
+            want = (self.E, s.N) if s.kind in (COMB, SINGLE) else (self.E,)
+            dt = _MASK_DTYPE[s.mask_bytes] if s.kind == COMB else torch.uint8 if s.kind == SINGLE else torch.int32
             self._check_out(flips, want, dt, "replay flips")
             fp = flips.data_ptr()
             keep.append(flips)
@@ -157,7 +168,8 @@ class EnvBatch:
         return res
 
     def sample_actions(self, p=0.1, out=None, stream=None):
-        """Synthetic Philox actions: comb Bernoulli(p) per (agent, channel); chsel uniform id."""
+        """Synthetic Philox actions: comb Bernoulli(p) per (agent, channel); chsel uniform id;
+        single Bernoulli(p) per agent."""
         a = out if out is not None else self.action_buffer()
         thr = int(np.floor(min(max(p, 0.0), 1.0) * 4294967296.0))
         rc = self.lib.d2d_sample_actions(self.desc, a.data_ptr(), thr, self.rng_step, _lib.stream_ptr(stream))
@@ -172,9 +184,11 @@ class EnvBatch:
         return b[:, :, : self.spec.D]
 
     def channels_host(self):
-        """comb: [E][N][C] uint8; chsel: [E][C+1] uint8."""
+        """comb: [E][N][C] uint8; chsel: [E][C+1] uint8; single: [E][N] uint8."""
         s = self.spec
         h = self.channels.cpu().numpy()
+        if s.kind == SINGLE:
+            return h.astype(np.uint8)
         if s.kind == COMB:
             bits = np.unpackbits(h.view(np.uint8).reshape(self.E, s.N, -1), axis=2, bitorder="little")
             return bits[:, :, : s.C]

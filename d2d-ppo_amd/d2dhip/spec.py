@@ -6,11 +6,14 @@ Mirrors how the reference envs interpret their arguments:
   spaces             envs/combinatorial_env.py:47-58, channel_selection_env.py:41-46
   channel_switch     combinatorial_env.py:42-45 (default zeros((N, C)); a 1-D
                      vector broadcasts over agents), channel_selection_env.py:35-38
-                     (C+1 scalar probabilities, channel 0 included)
+                     (C+1 scalar probabilities, channel 0 included),
+                     envs/env.py:33-37, 105-107 (one flip probability per agent, default 0.2)
+  neighbourhoods     envs/env.py:39-49 (obs of agent k = buffers + channel states of
+                     nbr(k), in list order, + the ack; default nbr(k) = [k])
 """
 import numpy as np
 
-COMB, CHSEL = "comb", "chsel"
+COMB, CHSEL, SINGLE = "comb", "chsel", "single"
 
 AGENT_DTYPE = np.dtype([("deadline", "u1"), ("obs_width", "u1"), ("arrival_kind", "u1"), ("reserved", "u1"),
                         ("state_offset", "<i4"), ("lam", "<f8"), ("pois_p0", "<f8"), ("arrival_thr", "<u8")])
@@ -35,7 +38,7 @@ def mask_bytes(C):
 
 class EnvSpec:
     def __init__(self, kind, n_agents, n_channels, deadlines, lbdas, period, arrival_probs, offsets, episode_length,
-                 traffic_model, periodic_devices, homogeneous_size, channel_switch):
+                 traffic_model, periodic_devices, homogeneous_size, channel_switch, neighbourhoods=None):
         self.kind = kind
         N, C = int(n_agents), int(n_channels)
         self.N, self.C = N, C
@@ -70,6 +73,23 @@ class EnvSpec:
             self.switch = np.array(cs, dtype=np.float64)
             self.F = self.D + 2 * C
             self.S = int(d.sum()) + C * (N + 1)
+        elif kind == SINGLE:
+            if C != 1:
+                raise ValueError("the D2DEnv has exactly one channel")
+            cs = 0.2 if channel_switch is None else channel_switch
+            self.switch = np.broadcast_to(np.asarray(cs, dtype=np.float64), (N,)).copy()
+            nbr = [[k] for k in range(N)] if neighbourhoods is None else \
+                [[int(j) for j in np.asarray(nb).reshape(-1)] for nb in neighbourhoods]
+            if len(nbr) != N:
+                raise ValueError(f"neighbourhoods has {len(nbr)} entries for {N} agents")
+            for nb in nbr:
+                if any(j < 0 or j >= N for j in nb):
+                    raise IndexError(f"neighbour index out of range in {nb}")
+            self.nbr = nbr
+            self.nbr_ptr = np.concatenate([[0], np.cumsum([len(nb) for nb in nbr])]).astype(np.int32)
+            self.nbr_idx = np.array([j for nb in nbr for j in nb], dtype=np.int32)
+            self.F = int(max(int(d[nb].sum()) + len(nb) + 1 for nb in nbr))
+            self.S = int(d.sum()) + N + 1
         else:
             cs = np.zeros(N) if channel_switch is None else np.asarray(channel_switch, dtype=np.float64).reshape(-1)
             if cs.shape[0] < C + 1:
@@ -80,13 +100,20 @@ class EnvSpec:
             self.S = int(d.sum()) + C + 1
         self.state_stride = (self.S + 3) // 4 * 4
         self.state_off = np.concatenate([[0], np.cumsum(d)[:-1]]).astype(np.int64)
-        self.obs_len = self.w + 2 * C if kind == COMB else d + C + 1
+        if kind == COMB:
+            self.obs_len = self.w + 2 * C
+        elif kind == SINGLE:
+            self.obs_len = np.array([int(d[nb].sum()) + len(nb) + 1 for nb in self.nbr], dtype=np.int64)
+        else:
+            self.obs_len = d + C + 1
         self.DW = buffer_words(self.D)
         self.mask_bytes = mask_bytes(C) if kind == COMB else 4
         if self.D > 32 or self.D > 255:
             raise NotImplementedError("max deadline > 32 is not supported by the HIP kernels")
         if N > 1024:
             raise NotImplementedError("n_agents > 1024 is not supported by the HIP kernels")
+        if kind == SINGLE and self.F > 1 << 24:
+            raise NotImplementedError("neighbourhood observations longer than 2^24 floats")
         if (kind == COMB and C > 32) or (kind == CHSEL and C > 31):
             raise NotImplementedError("too many channels for the HIP kernels")
 
@@ -121,6 +148,18 @@ class EnvSpec:
         t["pois_p0"] = np.exp(-self.lam)
         t["arrival_thr"] = bernoulli_threshold(self.q)
         return t
+
+    def gather_map(self, lib):
+        """D2DEnv obs/state gather codes (d2d_env_single_gather_map, host-only)."""
+        import ctypes
+        n = self.N * self.F + self.S
+        out = np.zeros(n, dtype=np.int32)
+        dl = np.ascontiguousarray(self.d, dtype=np.int32)
+        rc = lib.d2d_env_single_gather_map(self.N, dl.ctypes.data, self.nbr_ptr.ctypes.data, self.nbr_idx.ctypes.data,
+                                           self.F, out.ctypes.data, ctypes.c_int64(n))
+        if rc != n:
+            raise ValueError(f"d2d_env_single_gather_map: {lib.d2d_last_error().decode()}")
+        return out
 
     def flip_thresholds(self):
         return bernoulli_threshold(self.switch.reshape(-1))

@@ -22,11 +22,15 @@
  *   channels  comb : mask [E][N] (uint8 if C<=8, uint16 if C<=16, uint32 if
  *                    C<=32); bit c = 1 <=> channel c is good for agent k
  *             chsel: uint32 [E], bit j = state of channel j (0..C)
+ *             single: uint8 [E][N], 0/1 = agent k's channel state
  *   actions   comb : mask [E][N] (same width as channels), bit c = attempt on c
  *             chsel: uint8 [E][N], channel id 0..C (0 = idle)
+ *             single: uint8 [E][N], 0/1 (transmit)
  *   obs       float [E][N][obs_dim], agent k's row is prefix-compact:
  *               comb  [B[k,:w_k], channel_row_k (pre-evolve), ack(C), 0 ...]
  *               chsel [B[k,:d_k], ack(C+1), 0 ...]
+ *               single [B[j,:d_j] for j in nbr(k), H[j] for j in nbr(k), ack, 0 ...]
+ *                      (post-evolve channel; ack in {1, 0, -1})
  *             (w_k = D when homogeneous_size else d_k)
  *   state     float [E][state_stride], the reference's np.concatenate(state)
  */
@@ -39,9 +43,9 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 1
+#define D2D_ABI_VERSION 2
 
-enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1 };
+enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
 enum { D2D_OK = 0, D2D_EINVAL = -1, D2D_EUNSUPPORTED = -2, D2D_EHIP = -3 };
 
@@ -76,6 +80,10 @@ typedef struct d2d_env_desc {
     const uint8_t* arrival_kind_host;  /* host [N] */
     const double* period_host;         /* host [N] */
     const double* offset_host;         /* host [N] */
+    /* D2D_ENV_SINGLE only: device int32 [N*obs_dim + state_dim] gather codes of the
+     * neighbourhood obs rows then the state row, built on the host by
+     * d2d_env_single_gather_map (envs/env.py neighbourhoods, :39-49, 91-98) */
+    const int32_t* gather;
 } d2d_env_desc;
 
 typedef struct d2d_env_state {
@@ -83,15 +91,15 @@ typedef struct d2d_env_state {
     void* channels;
     uint32_t* received;     /* [E][N] packets received this episode (received_packets) */
     uint32_t* discarded;    /* [E][N] packets expired (discarded_packets) */
-    uint32_t* sel_quality;  /* chsel [E] selected_channel_qualities; NULL for comb */
-    uint32_t* sel_count;    /* chsel [E] number_selected_channel; NULL for comb */
+    uint32_t* sel_quality;  /* chsel [E] selected_channel_qualities; single [E] channel_errors; NULL for comb */
+    uint32_t* sel_count;    /* chsel [E] number_selected_channel; single [E] n_collisions; NULL for comb */
 } d2d_env_state;
 
 typedef struct d2d_env_out {  /* any field may be NULL */
     float* obs;         /* [E][N][obs_dim] */
     float* state;       /* [E][state_stride] */
-    int32_t* reward;    /* [E]  |successful users| (broadcast to all agents by the host) */
-    void* ack;          /* comb int8 [E][C] in {-1,0,1}; chsel double [E][C+1] */
+    int32_t* reward;    /* [E]  |successful users| (single: the ack); broadcast to all agents by the host */
+    void* ack;          /* comb int8 [E][C] in {-1,0,1}; chsel double [E][C+1]; single int8 [E] */
     uint8_t* success;   /* [E][N] 1 if agent k delivered a packet this slot */
 } d2d_env_out;
 
@@ -100,14 +108,17 @@ typedef struct d2d_env_replay {  /* parity mode; both NULL = Philox production s
     const uint8_t* arrivals;  /* [E][N] arrival value for agents that draw at this call */
 } d2d_env_replay;
 
-/* Replaces CombinatorialEnv.reset (envs/combinatorial_env.py:61-114) and
- * ChannelSelectionEnv.reset (envs/channel_selection_env.py:49-98). */
+/* Replaces CombinatorialEnv.reset (envs/combinatorial_env.py:61-114),
+ * ChannelSelectionEnv.reset (envs/channel_selection_env.py:49-98) and
+ * D2DEnv.reset (envs/env.py:51-99). */
 int d2d_env_reset(const d2d_env_desc* desc, const d2d_env_state* st, const d2d_env_replay* replay,
                   const d2d_env_out* out, uint32_t rng_step, void* stream);
 
 /* Replaces CombinatorialEnv.step (envs/combinatorial_env.py:127-242, with
  * evolve_channel 116-118 and evolve_buffer 120-124) and
- * ChannelSelectionEnv.step (envs/channel_selection_env.py:116-214).
+ * ChannelSelectionEnv.step (envs/channel_selection_env.py:116-214) and
+ * D2DEnv.step (envs/env.py:116-213, with decode_signal 101-103,
+ * evolve_channel 105-107 and evolve_buffer 109-113).
  * `timestep` is the value after the increment (t = 1, 2, ...). */
 int d2d_env_step(const d2d_env_desc* desc, const d2d_env_state* st, const void* actions,
                  const d2d_env_replay* replay, const d2d_env_out* out, int32_t timestep, uint32_t rng_step,
@@ -116,9 +127,19 @@ int d2d_env_step(const d2d_env_desc* desc, const d2d_env_state* st, const void* 
 /* Synthetic actions (env-only benchmark; replaces the per-agent
  * np.random.binomial of baselines.CombinatorialRandomAccess.act,
  * algorithms/baselines.py:181-183): comb mask bit c ~ Bernoulli(thr/2^32);
- * chsel uniform channel id in 0..C. */
+ * chsel uniform channel id in 0..C; single 0/1 ~ Bernoulli(thr/2^32)
+ * (GFAccess.act, algorithms/baselines.py:121-125). */
 int d2d_sample_actions(const d2d_env_desc* desc, void* actions, uint64_t threshold, uint32_t rng_step,
                        void* stream);
+
+/* Host-only: the D2DEnv gather table (envs/env.py:39-49 obs_length / state_length,
+ * 91-98 obs / state concatenation).  Agent k observes agents
+ * nbr_idx[nbr_ptr[k] .. nbr_ptr[k+1]) in that order.  Writes obs_dim*N + S codes
+ * (S = sum d + N + 1): code >= 0 is j*64 + q (byte q of agent j's buffer row,
+ * q < 32) or j*64 + 32 (agent j's channel state); -1 = the ack; -2 = zero padding.
+ * obs_dim must be >= every obs length.  Returns the number of codes written. */
+int d2d_env_single_gather_map(int32_t n_agents, const int32_t* deadlines, const int32_t* nbr_ptr,
+                              const int32_t* nbr_idx, int32_t obs_dim, int32_t* out, int64_t out_len);
 
 /* Bytes of one comb channel/action mask for C channels (1, 2 or 4). */
 int d2d_mask_bytes(int32_t n_channels);

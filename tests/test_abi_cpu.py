@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     for fn in fns:
         assert hasattr(lib, fn), fn
         assert fn in d2dhip.EXPORTED, f"{fn} has no ctypes signature"
-    assert lib.d2d_abi_version() == 1
+    assert lib.d2d_abi_version() == 2
     assert [lib.d2d_mask_bytes(c) for c in (1, 8, 9, 16, 17, 32)] == [1, 1, 2, 2, 4, 4]
     assert [lib.d2d_buffer_words(d) for d in (1, 4, 5, 8, 12, 14, 16, 17, 32)] == [1, 1, 2, 2, 3, 4, 4, 8, 8]
     assert lib.d2d_colstats_workspace(1000, 64) >= 64
@@ -38,7 +38,7 @@ def test_ctypes_structs_match_header_layout():
     from d2dhip import _lib
     from d2dhip.spec import AGENT_DTYPE
     assert AGENT_DTYPE.itemsize == 32
-    assert ctypes.sizeof(_lib.EnvDesc) == 8 * 4 + 8 * 2 + 8 * 5
+    assert ctypes.sizeof(_lib.EnvDesc) == 8 * 4 + 8 * 2 + 8 * 6
     assert ctypes.sizeof(_lib.EnvState) == 6 * 8 and ctypes.sizeof(_lib.EnvOut) == 5 * 8
     assert ctypes.sizeof(_lib.EnvReplay) == 2 * 8
 
@@ -50,7 +50,7 @@ def test_library_validates_arguments_without_gpu():
     lib = d2dhip.load()
     rc = lib.d2d_env_step(None, None, None, None, None, 1, 0, None)
     assert rc == -1 and b"desc" in lib.d2d_last_error()
-    desc = _lib.EnvDesc(0, 2000, 8, 7, 23, 0, 0, 1, 0, 0, None, None, None, None, None)
+    desc = _lib.EnvDesc(0, 2000, 8, 7, 23, 0, 0, 1, 0, 0, None, None, None, None, None, None)
     assert lib.d2d_env_reset(ctypes.byref(desc), None, None, None, 0, None) == -2
     assert lib.d2d_gae_scan(10, 1, 0, 1, None, None, None, 0.9, 0.97, 1, None, None, None) == -1
 
@@ -117,3 +117,71 @@ def test_bernoulli_threshold_edges():
     from d2dhip.spec import bernoulli_threshold
     t = bernoulli_threshold([0.0, 1.0, 0.5, 0.2])
     assert list(t) == [0, 2 ** 32, 2 ** 31, int(np.floor(0.2 * 2 ** 32))]
+
+
+def _apply_gather(codes, buffers, chan, ack):
+    """Resolve d2d_env_single_gather_map codes against one env's buffers [N][D], chan [N], ack."""
+    out = np.zeros(codes.shape[0], dtype=np.float64)
+    for i, c in enumerate(codes):
+        if c == -1:
+            out[i] = ack
+        elif c >= 0:
+            j, q = c >> 6, c & 63
+            out[i] = chan[j] if q == 32 else buffers[j, q]
+    return out
+
+
+def d2denv_fixtures():
+    import glob
+    from conftest import GOLDEN
+    return sorted(glob.glob(os.path.join(GOLDEN, "d2denv_*.npz")))
+
+
+@pytest.mark.parametrize("path", d2denv_fixtures(), ids=os.path.basename)
+def test_single_gather_map_reproduces_reference_obs(path):
+    """The host-built gather table (what the single_kernel's coalesced obs/state writes
+    resolve through) rebuilds every recorded D2DEnv obs / state (env.py:91-98, 198-205)
+    from the recorded buffers, channel states and ACKs."""
+    import d2dhip
+    from conftest import load_params
+    from envs.env import D2DEnv
+    lib = d2dhip.load()
+    z = np.load(path)
+    p = load_params(z)
+    env = D2DEnv(**{k: v for k, v in p.items() if k != "verbose"})
+    s = env.spec
+    assert np.array_equal(s.obs_len, z["obs_dims"]) and s.S == int(z["state_dim"])
+    assert [sp.shape[0] for sp in env.observation_space] == list(z["obs_dims"])     # env.py:43-45
+    assert env.state_space.shape == (s.S,) and [a.n for a in env.action_space] == [2] * s.N
+    codes = s.gather_map(lib)
+    assert codes.shape == (s.N * s.F + s.S,)
+    obs_codes, st_codes = codes[: s.N * s.F].reshape(s.N, s.F), codes[s.N * s.F:]
+    for t in range(z["obs"].shape[0]):
+        b, h, a = z["buffers"][t], z["chan"][t], float(z["ack"][t])
+        for k in range(s.N):
+            want = np.zeros(s.F, dtype=np.float32)
+            want[: z["obs"].shape[2]] = z["obs"][t, k]
+            assert np.array_equal(_apply_gather(obs_codes[k], b, h, a).astype(np.float32), want), (t, k)
+        assert np.array_equal(_apply_gather(st_codes, b, h, a).astype(np.float32), z["state"][t]), t
+    for w in range(z["reset_obs"].shape[0]):
+        st = _apply_gather(st_codes, z["reset_buffers"][w], z["reset_chan"][w], 0.0)
+        assert np.array_equal(st.astype(np.float32), z["reset_state"][w])
+
+
+def test_single_gather_map_rejects_bad_neighbourhoods():
+    import d2dhip
+    lib = d2dhip.load()
+    d = np.array([3, 3], dtype=np.int32)
+    ptr = np.array([0, 1, 2], dtype=np.int32)
+    idx = np.array([1, 5], dtype=np.int32)            # 5 is not an agent
+    out = np.zeros(64, dtype=np.int32)
+    rc = lib.d2d_env_single_gather_map(2, d.ctypes.data, ptr.ctypes.data, idx.ctypes.data, 5, out.ctypes.data, 64)
+    assert rc == -1 and b"out of range" in lib.d2d_last_error()
+    idx = np.array([1, 0], dtype=np.int32)
+    rc = lib.d2d_env_single_gather_map(2, d.ctypes.data, ptr.ctypes.data, idx.ctypes.data, 4, out.ctypes.data, 64)
+    assert rc == -1 and b"obs_dim" in lib.d2d_last_error()  # needs 3 + 1 + 1 = 5
+    rc = lib.d2d_env_single_gather_map(2, d.ctypes.data, ptr.ctypes.data, idx.ctypes.data, 5, out.ctypes.data, 64)
+    assert rc == 2 * 5 + 3 + 3 + 2 + 1
+    from envs.env import D2DEnv
+    with pytest.raises(ValueError, match="0 or 1"):
+        D2DEnv(2, np.array([3, 3]), np.ones(2))._pack_actions([0, 2])
