@@ -24,7 +24,9 @@ More legs are reported in the same JSON line (they do not change `value`):
             at the full 65,536 envs per GPU (ippo.py:406-441);
   configs : BASELINE.json configs[1] (chsel 16x4, 4,096 envs, D2D-PPO) and configs[4]
             (agent sweep 8..256 x 8 channels, 4,096 envs/GPU, D2D-PPO): env-step rates and
-            one D2D-PPO training iteration each.
+            one D2D-PPO training iteration each;
+  d2denv  : the single-channel D2DEnv (envs/env.py): 64 agents with ring
+            neighbourhoods, env-step rate, its kernel's HBM fraction, one iPPO iteration.
 """
 import argparse
 import json
@@ -368,6 +370,78 @@ def configs_leg(args, rank, world, local):
     return out
 
 
+def d2denv_leg(args, rank, world, local):
+    """D2DEnv (envs/env.py): 64 agents on one shared channel, ring
+    neighbourhoods {k-1, k, k+1} (obs = 3 buffers + 3 channel bits + ack = 25 floats), deadlines 7,
+    lambda 1/14 aperiodic, switch 0.2, `--envs` envs per GPU.  Env-step rate with device-sampled
+    Bernoulli(0.05) attempts, the single_kernel's HIP-event time against its algorithmic bytes, and
+    one iPPO iteration (4 epochs) at 4,096 envs."""
+    from envs.env import D2DEnv
+    N, d = 64, 7
+    nb = [[(k - 1) % N, k, (k + 1) % N] for k in range(N)]
+    p = dict(n_agents=N, deadlines=np.full(N, d), lbdas=np.full(N, 1 / 14), episode_length=args.episode_length,
+             channel_switch=0.2, neighbourhoods=nb)
+    env = D2DEnv(**p, n_envs=args.envs, device=f"cuda:{local}", seed=31)
+    env.shard(rank, world)
+    b = env.batch()
+    s = b.spec
+    act = b.action_buffer()
+    b.reset(want_obs=True)
+    for _ in range(10):
+        b.sample_actions(0.05, out=act)
+        b.step(act, want_obs=True)
+    steps = 100
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        if b.timestep >= env.episode_length:
+            b.reset(want_obs=True)
+        b.sample_actions(0.05, out=act)
+        evs[i][0].record()
+        b.step(act, want_obs=True)
+        evs[i][1].record()
+    torch.cuda.synchronize()
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    kern_ms = max_over_ranks(float(np.mean([a.elapsed_time(bb) for a, bb in evs])), world)
+    # algorithmic bytes of one launch: per agent row r+w (buffers 4*DW, channel 1, received 4, discarded 4),
+    # the action byte and the obs row; per env the reward and the two counters (r+w)
+    per_agent = 2 * (4 * s.DW + 1 + 8) + 1 + 4 * s.F
+    per_env = 4 + 16
+    bytes_launch = (per_agent * N + per_env) * b.E
+    achieved = bytes_launch / (kern_ms / 1e3) / 1e9
+    del env, b, act
+    torch.cuda.empty_cache()
+    from algorithms.ippo import iPPO
+    env = D2DEnv(**p, n_envs=4096, device=f"cuda:{local}", seed=32)
+    env.shard(rank, world)
+    torch.manual_seed(3)
+    lr = iPPO(env, hidden_size=64, gamma=0.4, policy_lr=3e-4, value_lr=1e-3, device=env.batch().device,
+              early_stopping=False)
+
+    def it(ne):
+        ro = lr._rollout(4096)
+        upd = lr._update_state(ro)
+        for _ in range(ne):
+            lr._update_epoch(ro, upd)
+
+    it(1)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    it(4)
+    torch.cuda.synchronize()
+    it_s = max_over_ranks(time.perf_counter() - t1, world)
+    out = {"agents": N, "envs_per_gpu": args.envs, "obs_dim": s.F, "neighbourhood": "ring {k-1,k,k+1}",
+           "env_steps_per_s": args.envs * world * steps / wall,
+           "kernel": "d2d::single_kernel<2, false>", "kernel_avg_us": kern_ms * 1e3,
+           "bytes_per_launch": bytes_launch, "achieved_GBps": achieved, "hbm_frac": achieved / HBM_PEAK_GBS,
+           "ippo_iteration_s_4096_envs": it_s, "fused_update": bool(lr._fused_update_ok()),
+           "ippo_env_steps_per_s_end_to_end": 4096 * world * args.episode_length / it_s}
+    del env, lr
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -377,7 +451,7 @@ def main():
     ap.add_argument("--episode-length", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--legs", default="env,rollout,ppo,train,configs")
+    ap.add_argument("--legs", default="env,rollout,ppo,train,configs,d2denv")
     ap.add_argument("--rollout-steps", type=int, default=60)
     ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
     ap.add_argument("--ppo-epochs", type=int, default=6)
@@ -444,6 +518,7 @@ def main():
         ppo = ppo_leg(args, rank, world, local)
     train = train_leg(env, args, rank, world, local) if "train" in legs else None
     configs = configs_leg(args, rank, world, local) if "configs" in legs else None
+    d2denv = d2denv_leg(args, rank, world, local) if "d2denv" in legs else None
 
     if rank == 0:
         res = {
@@ -479,6 +554,8 @@ def main():
             res["train"] = train
         if configs is not None:
             res["configs"] = configs
+        if d2denv is not None:
+            res["d2denv"] = d2denv
         if not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(params, seconds=args.cpu_seconds)
         print(json.dumps(res))
