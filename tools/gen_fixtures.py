@@ -333,6 +333,45 @@ def gen_d2denv():
         run_d2denv(name, params, episodes, p_act)
 
 
+def gen_baselines():
+    """act() of the four reference baselines (baselines.py) on seeded buffer matrices: EDF's
+    earliest-deadline choice (ties, empty rows, the random pick when nobody has a packet) and the
+    global-numpy-stream draws of GF / RandomAccess / CombinatorialRandomAccess, re-seeded per case."""
+    bl = ref_module("algorithms.baselines")
+
+    class _Env:
+        def __init__(self, n, c, d):
+            self.n_agents, self.n_channels, self.deadlines = n, c, np.asarray(d)
+
+    rng = np.random.default_rng(11)
+    out = {}
+    cases = []
+    for i in range(40):
+        n = int(rng.integers(1, 9))
+        D = int(rng.integers(1, 9))
+        dens = [0.0, 0.05, 0.2, 0.6][i % 4]
+        buf = (rng.random((n, D)) < dens) * rng.integers(1, 4, (n, D))
+        if i % 5 == 0 and n > 1:          # ties on the earliest column
+            buf[:, :] = 0
+            buf[[0, n - 1], min(1, D - 1)] = 1
+        cases.append(buf.astype(np.float64))
+    for i, buf in enumerate(cases):
+        n, D = buf.shape
+        env = _Env(n, 3, np.full(n, D))
+        out[f"case{i}/buffers"] = buf
+        np.random.seed(1000 + i)
+        out[f"case{i}/edf"] = bl.EarliestDeadlineFirstScheduler(env).act(buf)
+        np.random.seed(2000 + i)
+        out[f"case{i}/gf"] = bl.GFAccess(env, transmission_prob=0.4).act(buf)
+        np.random.seed(3000 + i)
+        out[f"case{i}/ra"] = bl.RandomAccess(env).act(buf.reshape(-1))
+        np.random.seed(4000 + i)
+        out[f"case{i}/cra"] = bl.CombinatorialRandomAccess(env, transmission_prob=0.3).act(buf)
+    out["n_cases"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(OUT, "baselines_act.npz"), **out)
+    print(f"baselines_act: {len(cases)} cases")
+
+
 def gen_gae():
     ippo = ref_module("algorithms.ippo")
     d2d = ref_module("algorithms.d2d_ppo")
@@ -554,6 +593,7 @@ def gen_learner():
 
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    which = sys.argv[1:] or ["data", "env", "d2denv", "gae", "learner"]
+    which = sys.argv[1:] or ["data", "env", "d2denv", "gae", "learner", "baselines"]
     for w in which:
-        {"data": gen_data, "env": gen_env, "d2denv": gen_d2denv, "gae": gen_gae, "learner": gen_learner}[w]()
+        {"data": gen_data, "env": gen_env, "d2denv": gen_d2denv, "gae": gen_gae, "learner": gen_learner,
+         "baselines": gen_baselines}[w]()
