@@ -415,46 +415,43 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   float(*zb)[16][20] = dzt[wave];
 
   const int stride = a.G * 4;
-  int tile = blockIdx.y * 4 + wave;
-  // one tile of look-ahead: the next tile's loads are issued as soon as this tile's obs are
-  // staged (the registers are reused), so they fly during the whole tile's compute
-  ActorIn<KC, PAIR> in;
-  if (tile < a.n_tiles) load_actor_in<KC, PAIR>(in, a, tile, k, g, i);
-  for (; tile < a.n_tiles; tile += stride) {
+  const int tile0 = blockIdx.y * 4 + wave;
+  int e0 = 0;
+  ActorIn<KC, PAIR> cur;  // per-sample scalars of the tile being computed
+  bf16x8 xh[2][KC];
+  // ---- inputs: bias column, zeros past it; bf16 high parts; the tile to LDS for dW1.
+  // Returns whether every input of the tile is bf16-exact (wave-uniform).
+  auto stage = [&](const ActorIn<KC, PAIR>& src, int tile) -> bool {
     const int t = tile / a.tiles_per_t;
-    const int e0 = (tile - t * a.tiles_per_t) * 32;
-    ActorIn<KC, PAIR> cur;
+    e0 = (tile - t * a.tiles_per_t) * 32;
 #pragma unroll
     for (int s = 0; s < (PAIR ? 1 : 2); ++s) {
-      cur.act[s] = in.act[s];
-      cur.lo[s] = in.lo[s];
-      cur.w[s] = in.w[s];
+      cur.act[s] = src.act[s];
+      cur.lo[s] = src.lo[s];
+      cur.w[s] = src.w[s];
     }
-
-    // ---- inputs: bias column, zeros past it; bf16 high parts; the tile to LDS for dW1
-    float xr[2][KC][8];
     uint32_t low = 0;
-    bf16x8 xh[2][KC];
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int c = 0; c < KC; ++c) {
+        float xr[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int col = 32 * c + 8 * g + j;
-          xr[s][c][j] = col < F ? in.x[s][c][j] : col == F ? 1.f : 0.f;
-          low |= fbits(xr[s][c][j]) & 0xFFFFu;
+          xr[j] = col < F ? src.x[s][c][j] : col == F ? 1.f : 0.f;
+          low |= fbits(xr[j]) & 0xFFFFu;
         }
-        xh[s][c] = hi_frag(xr[s][c]);
-        *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g]) = f32x4{xr[s][c][0], xr[s][c][1], xr[s][c][2], xr[s][c][3]};
-        *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g + 4]) = f32x4{xr[s][c][4], xr[s][c][5], xr[s][c][6], xr[s][c][7]};
+        xh[s][c] = hi_frag(xr);
+        *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g]) = f32x4{xr[0], xr[1], xr[2], xr[3]};
+        *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g + 4]) = f32x4{xr[4], xr[5], xr[6], xr[7]};
       }
-    const bool x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;  // wave-uniform
-    if (tile + stride < a.n_tiles) load_actor_in<KC, PAIR>(in, a, tile + stride, k, g, i);
+    return __builtin_amdgcn_ballot_w64(low != 0) == 0;
+  };
 
-    // the tile body; XE = true would specialise it on bf16-exact inputs (no branch inside), but
-    // carrying both bodies spills at 2 waves/SIMD, so the general body with wave-uniform runtime
-    // branches on x_exact runs (exact-only measured 5 % faster)
+  {
+    // the tile body, XE: every input bf16-exact (env observations: one MFMA per split part of
+    // W1), else the residual parts of x too
     auto body = [&](auto xe) {
       constexpr bool XE = decltype(xe)::value;
       // ---- forward (transposed): HT = W1 . X^T (bf16 split), Z^T = W2 . relu(HT) + b2 (fp32)
@@ -473,7 +470,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
             ht[t2] = mfma_bf16(w1p[t2][c].h, xh[s][c], ht[t2]);
           }
         }
-        if (!(XE || x_exact)) {  // rare (fractional observations): residual parts, x re-read from LDS
+        if constexpr (!XE) {  // rare (fractional observations): residual parts, x re-read from LDS
 #pragma unroll
           for (int c = 0; c < KC; ++c) {
             float xv[8];
@@ -545,7 +542,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
           float xc[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) xc[r] = xw[16 * s + 4 * g + r][16 * q + i];
-          if (XE || x_exact) {
+          if constexpr (XE) {
             const uint32_t xh2[2] = {pack_hi(xc[0], xc[1]), pack_hi(xc[2], xc[3])};
             bx1[q] = cat(xh2, xh2);  // (dH_h + dH_m) x
           } else {
@@ -567,7 +564,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
             hn = mfma_bf16(xh[s][c], w1p[t2][c].m, hn);
             hn = mfma_bf16(xh[s][c], w1p[t2][c].h, hn);
           }
-          if (!(XE || x_exact)) {
+          if constexpr (!XE) {
 #pragma unroll
             for (int c = 0; c < KC; ++c) {
               float xv[8];
@@ -604,14 +601,35 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
           const bf16x8 d_hm = cat(dp.h, dp.m);
 #pragma unroll
           for (int q = 0; q < QT; ++q) {
-            if (!(XE || x_exact)) dw1[t2][q] = mfma_bf16(d_hm, bx2[q], dw1[t2][q]);
+            if constexpr (!XE) dw1[t2][q] = mfma_bf16(d_hm, bx2[q], dw1[t2][q]);
             dw1[t2][q] = mfma_bf16(d_hm, bx1[q], dw1[t2][q]);
           }
         }
       }
     };
-    body(std::false_type{});  // runtime x_exact branches (a deferred-tile XE=true mode: DESIGN.md)
-    lds_order();
+    // Exact tiles run the branch-free XE body as they stream by (one tile of look-ahead: the
+    // next tile's loads are issued as soon as this tile is staged); a tile with fractional inputs
+    // is deferred to a second pass over the wave's tiles with the general body, so neither body
+    // carries the other's live ranges or branches.
+    ActorIn<KC, PAIR> in;
+    bool deferred = false;
+    if (tile0 < a.n_tiles) load_actor_in<KC, PAIR>(in, a, tile0, k, g, i);
+    for (int tile = tile0; tile < a.n_tiles; tile += stride) {
+      const bool x_exact = stage(in, tile);
+      if (tile + stride < a.n_tiles) load_actor_in<KC, PAIR>(in, a, tile + stride, k, g, i);
+      if (x_exact)
+        body(std::true_type{});
+      else
+        deferred = true;
+      lds_order();
+    }
+    if (deferred) {
+      for (int tile = tile0; tile < a.n_tiles; tile += stride) {
+        load_actor_in<KC, PAIR>(in, a, tile, k, g, i);
+        if (!stage(in, tile)) body(std::false_type{});
+        lds_order();
+      }
+    }
   }
 
   // ---- workgroup partial
@@ -748,19 +766,18 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
   float(*xw)[XS] = xs[wave];
 
   const int stride = a.G * 4;
-  int tile = blockIdx.y * 4 + wave;
-  CriticIn<KC> in;
-  if (tile < a.n_tiles) load_critic_in<KC>(in, a, tile, k, g, i);
-  for (; tile < a.n_tiles; tile += stride) {
+  const int tile0 = blockIdx.y * 4 + wave;
+  int e0 = 0;
+  float R[2][4];
+  bf16x8 xh[2][KC];
+  auto stage = [&](const CriticIn<KC>& src, int tile) -> bool {
     const int t = tile / a.tiles_per_t;
-    const int e0 = (tile - t * a.tiles_per_t) * 32;
-    float R[2][4];
+    e0 = (tile - t * a.tiles_per_t) * 32;
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) R[s][r] = in.R[s][r];
+      for (int r = 0; r < 4; ++r) R[s][r] = src.R[s][r];
     uint32_t low = 0;
-    bf16x8 xh[2][KC];
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -769,20 +786,17 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int col = 32 * c + 8 * g + j;
-          xr[j] = col < F ? in.x[s][c][j] : col == F ? 1.f : 0.f;
+          xr[j] = col < F ? src.x[s][c][j] : col == F ? 1.f : 0.f;
           low |= fbits(xr[j]) & 0xFFFFu;
         }
         xh[s][c] = hi_frag(xr);
         *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g]) = f32x4{xr[0], xr[1], xr[2], xr[3]};
         *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g + 4]) = f32x4{xr[4], xr[5], xr[6], xr[7]};
       }
-    const bool x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;
-    if (tile + stride < a.n_tiles) load_critic_in<KC>(in, a, tile + stride, k, g, i);
-    lds_order();
-
-    // the tile body; XE = true would specialise it on bf16-exact inputs (no branch inside), but
-    // carrying both bodies spills at 2 waves/SIMD, so the general body with wave-uniform runtime
-    // branches on x_exact runs (exact-only measured 5 % faster)
+    return __builtin_amdgcn_ballot_w64(low != 0) == 0;
+  };
+  {
+    // the tile body (XE: bf16-exact inputs), deferred tiles as in the actor kernel
     auto body = [&](auto xe) {
       constexpr bool XE = decltype(xe)::value;
 #pragma unroll
@@ -799,7 +813,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
             acc = mfma_bf16(xh[s][c], v1p[t2][c].m, acc);
             acc = mfma_bf16(xh[s][c], v1p[t2][c].h, acc);
           }
-          if (!(XE || x_exact)) {
+          if constexpr (!XE) {
 #pragma unroll
             for (int c = 0; c < KC; ++c) {
               float xv[8];
@@ -833,7 +847,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
           float xc[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) xc[r] = xw[16 * s + 4 * g + r][16 * q + i];
-          if (XE || x_exact) {
+          if constexpr (XE) {
             const uint32_t xh2[2] = {pack_hi(xc[0], xc[1]), pack_hi(xc[2], xc[3])};
             bx1[q] = cat(xh2, xh2);
           } else {
@@ -855,14 +869,34 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
           const bf16x8 d_hm = cat(dp.h, dp.m);
 #pragma unroll
           for (int q = 0; q < QT; ++q) {
-            if (!(XE || x_exact)) dv1[t2][q] = mfma_bf16(d_hm, bx2[q], dv1[t2][q]);
+            if constexpr (!XE) dv1[t2][q] = mfma_bf16(d_hm, bx2[q], dv1[t2][q]);
             dv1[t2][q] = mfma_bf16(d_hm, bx1[q], dv1[t2][q]);
           }
         }
       }
     };
-    body(std::false_type{});  // runtime x_exact branches (a deferred-tile XE=true mode: DESIGN.md)
-    lds_order();
+    CriticIn<KC> in;
+    bool deferred = false;
+    if (tile0 < a.n_tiles) load_critic_in<KC>(in, a, tile0, k, g, i);
+    for (int tile = tile0; tile < a.n_tiles; tile += stride) {
+      const bool x_exact = stage(in, tile);
+      if (tile + stride < a.n_tiles) load_critic_in<KC>(in, a, tile + stride, k, g, i);
+      lds_order();
+      if (x_exact)
+        body(std::true_type{});
+      else
+        deferred = true;
+      lds_order();
+    }
+    if (deferred) {
+      for (int tile = tile0; tile < a.n_tiles; tile += stride) {
+        load_critic_in<KC>(in, a, tile, k, g, i);
+        const bool x_exact = stage(in, tile);
+        lds_order();
+        if (!x_exact) body(std::false_type{});
+        lds_order();
+      }
+    }
   }
 
   float acc[NV];
