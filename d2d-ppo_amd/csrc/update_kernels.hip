@@ -349,7 +349,9 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   // half per hidden tile) in LDS, shared by the workgroup's four waves
   Parts w1p[HT][KC];
   f32x4 b2i;
-  __shared__ __attribute__((aligned(16))) uint32_t w2b_s[HT][3][64][2];  // dH's B operand parts h, m, l
+  // dH's three B operands [l|h], [m|h], [h|m], stored whole so one ds_read_b128 lands each in
+  // the four consecutive registers the MFMA reads (no operand assembly moves)
+  __shared__ __attribute__((aligned(16))) bf16x8 w2b_s[HT][3][64];
   __shared__ __attribute__((aligned(16))) float w2f_s[HT][64][4];        // Z^T's fp32 A operand
   {
     const float* W1 = a.w1 + (size_t)k * H * F;
@@ -377,12 +379,9 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
 #pragma unroll
       for (int j = 0; j < 4; ++j) wb[j] = (hok && 4 * g + j < A) ? W2[(size_t)(4 * g + j) * H + hrow] : 0.f;
       const Parts4 p4 = split3_4(wb);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        w2b_s[t][0][lane][q] = p4.h[q];
-        w2b_s[t][1][lane][q] = p4.m[q];
-        w2b_s[t][2][lane][q] = p4.l[q];
-      }
+      w2b_s[t][0][lane] = cat(p4.l, p4.h);
+      w2b_s[t][1][lane] = cat(p4.m, p4.h);
+      w2b_s[t][2][lane] = cat(p4.h, p4.m);
       // A operand of Z^T = W2 . relu(HT) (fp32 16x16x4): row = action i, k = hidden 16t + 4g + r
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -576,16 +575,9 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
             }
           }
           // the 4 live k-slots of each fragment half carry a second split part: 6 terms, 3 MFMAs
-          uint32_t wh[2], wm[2], wl[2];
-#pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            wh[q] = w2b_s[t2][0][lane][q];
-            wm[q] = w2b_s[t2][1][lane][q];
-            wl[q] = w2b_s[t2][2][lane][q];
-          }
-          f32x4 acc = mfma_bf16(a_hl, cat(wl, wh), f32x4{0.f, 0.f, 0.f, 0.f});
-          acc = mfma_bf16(a_hm, cat(wm, wh), acc);
-          acc = mfma_bf16(a_hm, cat(wh, wm), acc);
+          f32x4 acc = mfma_bf16(a_hl, w2b_s[t2][0][lane], f32x4{0.f, 0.f, 0.f, 0.f});
+          acc = mfma_bf16(a_hm, w2b_s[t2][1][lane], acc);
+          acc = mfma_bf16(a_hm, w2b_s[t2][2][lane], acc);
           float dh[4], hr[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
