@@ -457,7 +457,6 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
       f32x4 zt[2];
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        __builtin_amdgcn_sched_barrier(0);  // bound live ranges: phases do not interleave
         f32x4 ht[HT];
 #pragma unroll
         for (int t2 = 0; t2 < HT; ++t2) {
@@ -493,7 +492,6 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
         zt[s] = z;
       }
 
-      __builtin_amdgcn_sched_barrier(0);  // bound live ranges: phases do not interleave
       // ---- epilogue -> dZ (lane (g, i): sample 16s + i, actions 4g + r), written transposed to LDS
       f32x4 dz[2];
       if constexpr (PAIR) {
@@ -527,7 +525,6 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
       //      from LDS, bf16-exact on env observations, else split too)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        __builtin_amdgcn_sched_barrier(0);  // bound live ranges: phases do not interleave
         float dzn[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) dzn[r] = zb[s][4 * g + r][i];
@@ -793,7 +790,6 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
       constexpr bool XE = decltype(xe)::value;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        __builtin_amdgcn_sched_barrier(0);  // bound live ranges: phases do not interleave
         // HV = X . V1^T (sample 16s + 4g + r on rows, hidden 16t + i on lanes)
         f32x4 hv[HT];
 #pragma unroll
