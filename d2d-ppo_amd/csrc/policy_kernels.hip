@@ -612,7 +612,10 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const float* obs, cons
   a.E = d->n_envs; a.N = d->n_agents; a.F = d->obs_dim; a.H = d->hidden; a.A = d->n_out; a.kind = d->kind;
   a.deterministic = deterministic ? 1 : 0;
   a.inv_A = 1.f / (float)a.A;
+  // 256 envs (16 tiles) per wave amortise the per-wave weight split; a small batch takes fewer,
+  // down to 32 (the tile loop runs tiles in pairs), so that >= 2048 waves (2 per SIMD) fill the chip
   a.envs_per_wave = 256;
+  while (a.envs_per_wave > 32 && (int64_t)d->n_envs * d->n_agents / a.envs_per_wave < 2048) a.envs_per_wave >>= 1;
   a.rng_step = rng_step; a.seed = d->seed; a.env_base = d->env_base;
   a.w1 = d->w1; a.b1 = d->b1; a.w2 = d->w2; a.b2 = d->b2; a.v1 = d->v1; a.c1 = d->c1; a.v2 = d->v2; a.c2 = d->c2;
   a.obs = obs; a.forced = forced; a.act_out = actions; a.logp_out = logp; a.value_out = value;
