@@ -182,6 +182,7 @@ class BatchedLearnerBase(DataParallelMixin):
             from d2dhip import _lib
             lib = _lib.require_gpu()
             desc = self._mlp_desc(b.E, b.desc.env_base)
+            desc.rng_offset = b.rng_off.data_ptr()
             fz = None
             if forced is not None:
                 fz = self._env_actions(forced).contiguous()
@@ -227,19 +228,36 @@ class BatchedLearnerBase(DataParallelMixin):
         the policy still computes probs/log-probs/values, of the forced actions."""
         b = self._bind_env()
         env = self.env
-        s = b.spec
-        E, L, N, Fd = b.E, env.episode_length, s.N, s.F
+        E, L = b.E, env.episode_length
         waves = max(1, math.ceil(num_episodes / E))
+        if teacher is None and self._graph_ok(train, b, waves * L):
+            return self._collect_graph(b, waves, want_values, want_state)
+        bufs = self._rollout_buffers(b, waves, want_values, want_state)
+        tf = self._teacher_tensors(teacher, b, waves * L) if teacher is not None else None
+        self._waves(bufs, b, waves, train, tf)
+        return self._rollout_result(bufs, b, waves, train)
+
+    # ------------------------------------------------- rollout body (eager or captured)
+    def _rollout_buffers(self, b, waves, want_values, want_state):
+        s, E, L, dev = b.spec, b.E, self.env.episode_length, self.device
         T = waves * L
-        dev = self.device
-        obs_buf = torch.empty((T, E, N, Fd), dtype=torch.float32, device=dev)
-        act_buf = torch.empty((T, E, N), dtype=b.action_buffer().dtype, device=dev)
-        logp_buf = torch.empty((T, N, E), dtype=torch.float32, device=dev)
-        rew_i32 = torch.empty((T, E), dtype=torch.int32, device=dev)
-        val_buf = torch.empty((T, N, E), dtype=torch.float32, device=dev) if want_values else None
-        state_buf = torch.empty((T, E, s.state_stride), dtype=torch.float32, device=dev) if want_state else None
-        scores, ep_rewards, jains, ch_errors = [], [], [], []
-        tf = self._teacher_tensors(teacher, b, T) if teacher is not None else None
+        f64 = lambda: torch.zeros((waves, E), dtype=torch.float64, device=dev)  # noqa: E731
+        return dict(obs=torch.empty((T, E, s.N, s.F), dtype=torch.float32, device=dev),
+                    act=torch.empty((T, E, s.N), dtype=b.action_buffer().dtype, device=dev),
+                    logp=torch.empty((T, s.N, E), dtype=torch.float32, device=dev),
+                    rew=torch.empty((T, E), dtype=torch.int32, device=dev),
+                    val=torch.empty((T, s.N, E), dtype=torch.float32, device=dev) if want_values else None,
+                    state=torch.empty((T, E, s.state_stride), dtype=torch.float32, device=dev) if want_state else None,
+                    recv=f64(), disc=f64(), eprew=f64(), jains=f64(), ch=f64())
+
+    def _waves(self, bufs, b, waves, train, tf):
+        """The rollout proper: per wave one reset and L slots of (policy kernel, env kernel), then
+        the wave's episode statistics as device reductions (no host synchronisation)."""
+        env, s = self.env, b.spec
+        L = env.episode_length
+        obs_buf, act_buf, logp_buf, rew_i32 = bufs["obs"], bufs["act"], bufs["logp"], bufs["rew"]
+        val_buf, state_buf = bufs["val"], bufs["state"]
+        want_state = state_buf is not None
         with torch.no_grad():
             for w in range(waves):
                 t0 = w * L
@@ -249,26 +267,84 @@ class BatchedLearnerBase(DataParallelMixin):
                 for t in range(L):
                     i = t0 + t
                     act = self._policy_slot(obs_buf, t0, i, train, act_buf[i], logp_buf[i],
-                                            val_buf[i] if want_values else None, tf, b)
+                                            val_buf[i] if val_buf is not None else None, tf, b)
                     last = t + 1 == L
                     env.step_batched(act, want_obs=not last, want_state=want_state and not last,
                                      out_obs=None if last else obs_buf[i + 1],
                                      out_state=None if (last or not want_state) else state_buf[i + 1],
                                      out_reward=rew_i32[i], replay=None if tf is None else tf["replay"][i])
-                recv = b.received.sum(1).double()
-                disc = b.discarded.sum(1).double()
-                scores.extend((1 - disc / recv).cpu().tolist())
-                ep_rewards.extend(rew_i32[t0:t0 + L].double().sum(0).cpu().tolist())
+                bufs["recv"][w].copy_(b.received.sum(1))
+                bufs["disc"][w].copy_(b.discarded.sum(1))
+                bufs["eprew"][w].copy_(rew_i32[t0:t0 + L].sum(0))
                 if not train:
-                    jains.extend(self._jains(b))
+                    bufs["jains"][w].copy_(self._jains_dev(b))
                     if s.kind == "single":  # D2DEnv.channel_errors of the episode (env.py:144-145)
-                        ch_errors.extend(b.sel_quality.cpu().tolist())
-        dones = torch.zeros(T, dtype=torch.uint8, device=dev)
+                        bufs["ch"][w].copy_(b.sel_quality)
+
+    def _rollout_result(self, bufs, b, waves, train):
+        L = self.env.episode_length
+        T = waves * L
+        recv, disc = bufs["recv"].cpu(), bufs["disc"].cpu()
+        scores = (1 - disc / recv).reshape(-1).tolist()
+        ep_rewards = bufs["eprew"].cpu().reshape(-1).tolist()
+        jains = bufs["jains"].cpu().reshape(-1).tolist() if not train else []
+        ch_errors = bufs["ch"].cpu().reshape(-1).tolist() if (not train and b.spec.kind == "single") else []
+        dones = torch.zeros(T, dtype=torch.uint8, device=self.device)
         dones[L - 1::L] = 1
-        return Rollout(obs=obs_buf, actions=act_buf, logp=logp_buf, rewards=rew_i32.float(), values=val_buf,
-                       states=state_buf, dones=dones, scores=scores, ep_rewards=ep_rewards, jains=jains,
-                       ch_errors=ch_errors, T=T, E=E,
-                       waves=waves, L=L)
+        return Rollout(obs=bufs["obs"], actions=bufs["act"], logp=bufs["logp"], rewards=bufs["rew"].float(),
+                       values=bufs["val"], states=bufs["state"], dones=dones, scores=scores, ep_rewards=ep_rewards,
+                       jains=jains, ch_errors=ch_errors, T=T, E=b.E, waves=waves, L=L)
+
+    # ------------------------------------------------------- HIP-graph rollout
+    graph_rollout = os.environ.get("D2D_GRAPH_ROLLOUT", "1") != "0"
+    GRAPH_ROLLOUT_MAX_BYTES = 4 << 30
+
+    def _graph_ok(self, train, b, T):
+        """Training rollouts of the fused MLP policy replay one captured HIP graph (reset + L x
+        (policy kernel, env kernel) per wave + the statistics): at small batches the slot loop is
+        bound by per-launch host work, not the GPU.  Large rollouts (obs buffer > 4 GiB, where the
+        kernels dominate) stay eager rather than pinning a second copy of the buffers."""
+        if not (self.graph_rollout and train and not self.useRNN and self._fused_ok()
+                and (self.kind == "comb") == bool(self.combinatorial)):
+            return False
+        s = b.spec
+        return T * b.E * s.N * s.F * 4 <= self.GRAPH_ROLLOUT_MAX_BYTES
+
+    def _collect_graph(self, b, waves, want_values, want_state):
+        """Capture once per rollout shape, replay afterwards.  The kernels add the device word
+        b.rng_off to their launch's rng_step, so a replay draws the Philox counters an eager rollout
+        from the current b.rng_step would (bit-identical results); its buffers are reused by the next
+        training rollout of the same shape."""
+        env = self.env
+        L = env.episode_length
+        key = (b.E, L, waves, bool(want_values), bool(want_state))
+        cache = self.__dict__.setdefault("_rollout_graphs", {})
+        G = cache.get(key)
+        if G is None:
+            cache.clear()  # one live graph (and its buffers) per learner
+            bufs = self._rollout_buffers(b, waves, want_values, want_state)
+            side = torch.cuda.Stream(device=self.device)
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):  # warm-up: a real rollout (allocations, kernel attributes)
+                self._waves(bufs, b, waves, True, None)
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize(self.device)
+            result = self._rollout_result(bufs, b, waves, True)
+            base = b.rng_step
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._waves(bufs, b, waves, True, None)
+            G = dict(graph=g, bufs=bufs, base=base, delta=b.rng_step - base)
+            b.rng_step = base  # capturing ran nothing
+            cache[key] = G
+            return result
+        b.rng_off.fill_(b.rng_step - G["base"])
+        G["graph"].replay()
+        b.rng_off.zero_()
+        b.rng_step += G["delta"]
+        b.timestep = L
+        env.timestep = L
+        return self._rollout_result(G["bufs"], b, waves, True)
 
     def _teacher_tensors(self, teacher, b, T):
         from d2dhip.envbatch import pack_masks
@@ -296,12 +372,11 @@ class BatchedLearnerBase(DataParallelMixin):
         return {"actions": a, "replay": replay, "reset_arrivals": ra}
 
     @staticmethod
-    def _jains(b):
+    def _jains_dev(b):
         recv = b.received.double()
         disc = b.discarded.double()
         u = torch.where(recv > 0, 1 - disc / recv.clamp(min=1), torch.ones_like(recv))
-        j = u.sum(1) ** 2 / recv.shape[1] / (u ** 2).sum(1)
-        return j.cpu().tolist()
+        return u.sum(1) ** 2 / recv.shape[1] / (u ** 2).sum(1)
 
     # ------------------------------------------------------ update inputs
     def _seq(self, x_tne):

@@ -50,6 +50,7 @@ struct EnvArgs {
   void* ack;
   uint8_t* success;
   const int32_t* gather;  // single: [N*F + S] obs/state gather codes
+  const uint32_t* rng_off;  // optional device word added to rng_step (graph replays)
   uint64_t draw[kMaxAgents / 64];
 };
 
@@ -144,6 +145,9 @@ __device__ __forceinline__ float row_byte(const Row<DW>& r, int j) {
   return (float)((r.w[j >> 2] >> ((j & 3) * 8)) & 0xFFu);
 }
 
+// Philox step of this launch: the call's rng_step plus the optional device offset (one scalar load)
+__device__ __forceinline__ uint32_t rng_of(const EnvArgs& a) { return a.rng_step + (a.rng_off ? *a.rng_off : 0u); }
+
 // ------------------------------------------------------------------ draws
 __device__ __forceinline__ bool draws_now(const EnvArgs& a, int k) {
   return (a.draw[k >> 6] >> (k & 63)) & 1ull;
@@ -152,7 +156,7 @@ __device__ __forceinline__ bool draws_now(const EnvArgs& a, int k) {
 __device__ __forceinline__ uint32_t arrival_value(const EnvArgs& a, const d2d_agent_entry& ag, size_t row, int k,
                                                   uint64_t genv) {
   if (a.arrivals) return a.arrivals[row];
-  const u32x4 r = philox((uint32_t)genv, (uint32_t)k, a.rng_step, kStreamArrival << 24, a.seed);
+  const u32x4 r = philox((uint32_t)genv, (uint32_t)k, rng_of(a), kStreamArrival << 24, a.seed);
   if (ag.arrival_kind == D2D_ARRIVAL_POISSON) return poisson_inv(r.x, ag.lam, ag.pois_p0);
   return (uint64_t)r.x < ag.arrival_thr ? 1u : 0u;
 }
@@ -380,7 +384,7 @@ __global__ __launch_bounds__(kMaxAgents) void comb_kernel(EnvArgs a) {
       } else {
         const uint64_t* thr = a.flip_thr + (size_t)L.k * C;
         auto flip_block = [&](int blk) {
-          const u32x4 r = philox((uint32_t)genv, (uint32_t)L.k, a.rng_step, (kStreamFlip << 24) | (uint32_t)blk, a.seed);
+          const u32x4 r = philox((uint32_t)genv, (uint32_t)L.k, rng_of(a), (kStreamFlip << 24) | (uint32_t)blk, a.seed);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int c = blk * 4 + i;
@@ -548,7 +552,7 @@ __global__ __launch_bounds__(kMaxAgents) void chsel_kernel(EnvArgs a) {
         f = reinterpret_cast<const uint32_t*>(a.flips)[L.env];
       } else {
         for (int blk = 0; blk * 4 < C + 1; ++blk) {
-          const u32x4 r = philox((uint32_t)genv, kPerEnv, a.rng_step, (kStreamFlip << 24) | (uint32_t)blk, a.seed);
+          const u32x4 r = philox((uint32_t)genv, kPerEnv, rng_of(a), (kStreamFlip << 24) | (uint32_t)blk, a.seed);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int j = blk * 4 + i;
@@ -694,7 +698,7 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
       if (a.flips) {
         f = reinterpret_cast<const uint8_t*>(a.flips)[row] & 1u;
       } else {
-        const u32x4 r = philox((uint32_t)genv, (uint32_t)L.k, a.rng_step, kStreamFlip << 24, a.seed);
+        const u32x4 r = philox((uint32_t)genv, (uint32_t)L.k, rng_of(a), kStreamFlip << 24, a.seed);
         f = (uint64_t)r.x < a.flip_thr[L.k] ? 1u : 0u;
       }
     }
@@ -997,6 +1001,7 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
   a.selq = st->sel_quality; a.seln = st->sel_count; a.actions = actions;
   if (rp) { a.flips = rp->flips; a.arrivals = rp->arrivals; }
   a.gather = d->gather;
+  a.rng_off = d->rng_offset;
   if (out) { a.obs = out->obs; a.state = out->state; a.reward = out->reward; a.ack = out->ack; a.success = out->success; }
   draw_mask(d, reset ? 0 : t, a.draw);
   a.flags = store_flags();

@@ -30,6 +30,7 @@ struct MlpArgs {
   int E, N, F, H, A, kind, deterministic, envs_per_wave;
   float inv_A;
   uint32_t rng_step;
+  const uint32_t* rng_off;  // optional device word added to rng_step (graph replays)
   uint64_t seed, env_base;
   const float *w1, *b1, *w2, *b2, *v1, *c1, *v2, *c2;
   const float* obs;      // [E][N][F]
@@ -142,7 +143,7 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
 #pragma unroll
       for (int r = 0; r < 4; ++r) taken |= (uint32_t)(p[r] > 0.5f) << r;  // dist.probs > 0.5 (ippo.py:166)
     } else {
-      const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step, (kStreamPolicy << 24) | (uint32_t)ga, a.seed);
+      const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step + (a.rng_off ? *a.rng_off : 0u), (kStreamPolicy << 24) | (uint32_t)ga, a.seed);
 #pragma unroll
       for (int r = 0; r < 4; ++r) taken |= (uint32_t)((float)(pick(rr, r) >> 8) * (1.f / 16777216.f) < p[r]) << r;
     }
@@ -184,7 +185,7 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
       chosen = bi;
     } else {
       // prefix over lane groups: exclusive sum of psum for groups < g
-      const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step, (kStreamPolicy << 24), a.seed);
+      const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step + (a.rng_off ? *a.rng_off : 0u), (kStreamPolicy << 24), a.seed);
       const float u = (float)(rr.x >> 8) * (1.f / 16777216.f) * tot;
       const float s16 = uf(partner16(fu(psum), g));  // partner in pair (g ^ 1)
       const float pair = psum + s16;
@@ -616,7 +617,7 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const float* obs, cons
   // down to 32 (the tile loop runs tiles in pairs), so that >= 2048 waves (2 per SIMD) fill the chip
   a.envs_per_wave = 256;
   while (a.envs_per_wave > 32 && (int64_t)d->n_envs * d->n_agents / a.envs_per_wave < 2048) a.envs_per_wave >>= 1;
-  a.rng_step = rng_step; a.seed = d->seed; a.env_base = d->env_base;
+  a.rng_step = rng_step; a.rng_off = d->rng_offset; a.seed = d->seed; a.env_base = d->env_base;
   a.w1 = d->w1; a.b1 = d->b1; a.w2 = d->w2; a.b2 = d->b2; a.v1 = d->v1; a.c1 = d->c1; a.v2 = d->v2; a.c2 = d->c2;
   a.obs = obs; a.forced = forced; a.act_out = actions; a.logp_out = logp; a.value_out = value;
   a.mask_bytes = d->n_out <= 8 ? 1 : d->n_out <= 16 ? 2 : 4;

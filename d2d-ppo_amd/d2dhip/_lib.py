@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libd2dhip.so")
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
 
@@ -28,7 +28,7 @@ class EnvDesc(ctypes.Structure):
                 ("max_deadline", ctypes.c_int32), ("obs_dim", ctypes.c_int32), ("state_dim", ctypes.c_int32),
                 ("state_stride", ctypes.c_int32), ("n_envs", ctypes.c_int32), ("env_base", ctypes.c_uint64),
                 ("seed", ctypes.c_uint64), ("agents", _p), ("flip_thr", _p), ("arrival_kind_host", _p),
-                ("period_host", _p), ("offset_host", _p), ("gather", _p)]
+                ("period_host", _p), ("offset_host", _p), ("gather", _p), ("rng_offset", _p)]
 
 
 class EnvState(ctypes.Structure):
@@ -48,7 +48,7 @@ class MlpDesc(ctypes.Structure):
     _fields_ = [("n_agents", ctypes.c_int32), ("n_envs", ctypes.c_int32), ("obs_dim", ctypes.c_int32),
                 ("hidden", ctypes.c_int32), ("n_out", ctypes.c_int32), ("kind", ctypes.c_int32),
                 ("w1", _p), ("b1", _p), ("w2", _p), ("b2", _p), ("v1", _p), ("c1", _p), ("v2", _p), ("c2", _p),
-                ("seed", ctypes.c_uint64), ("env_base", ctypes.c_uint64)]
+                ("seed", ctypes.c_uint64), ("env_base", ctypes.c_uint64), ("rng_offset", _p)]
 
 
 # name -> (restype, argtypes)

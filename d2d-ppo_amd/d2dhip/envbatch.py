@@ -56,11 +56,14 @@ class EnvBatch:
         self._ack = None
         self._success = None
         self.gather = torch.from_numpy(spec.gather_map(self.lib)).to(dev) if s.kind == SINGLE else None
+        # device word added to rng_step by every kernel of this batch (and by the learner's policy
+        # kernel): 0 for eager calls, set before replaying a captured rollout graph
+        self.rng_off = torch.zeros(1, dtype=torch.int32, device=dev)
         self.desc = _lib.EnvDesc(
             _KIND_ID[s.kind], s.N, s.C, s.D, s.F, s.S, s.state_stride, E, int(env_base),
             int(seed) & 0xFFFFFFFFFFFFFFFF, self.agents.data_ptr(), self.flip_thr.data_ptr(),
             self._kinds_host.ctypes.data, self._period_host.ctypes.data, self._offset_host.ctypes.data,
-            None if self.gather is None else self.gather.data_ptr())
+            None if self.gather is None else self.gather.data_ptr(), self.rng_off.data_ptr())
         self.st = _lib.EnvState(self.buffers.data_ptr(), self.channels.data_ptr(), self.received.data_ptr(),
                                 self.discarded.data_ptr(),
                                 None if self.sel_quality is None else self.sel_quality.data_ptr(),

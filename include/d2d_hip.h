@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 2
+#define D2D_ABI_VERSION 3
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -84,6 +84,10 @@ typedef struct d2d_env_desc {
      * neighbourhood obs rows then the state row, built on the host by
      * d2d_env_single_gather_map (envs/env.py neighbourhoods, :39-49, 91-98) */
     const int32_t* gather;
+    /* optional device uint32 added to every call's rng_step when the kernel runs (NULL = 0):
+     * a captured HIP graph of reset/step calls replays with fresh Philox counters by
+     * updating this one word instead of the baked launch arguments */
+    const uint32_t* rng_offset;
 } d2d_env_desc;
 
 typedef struct d2d_env_state {
@@ -206,6 +210,7 @@ typedef struct d2d_mlp_desc {
     const float *w1, *b1, *w2, *b2;
     const float *v1, *c1, *v2, *c2;
     uint64_t seed, env_base;
+    const uint32_t* rng_offset;  /* optional device uint32 added to rng_step (graph replays), as in d2d_env_desc */
 } d2d_mlp_desc;
 
 int d2d_policy_mlp_step(const d2d_mlp_desc* desc, const float* obs, const void* forced, uint32_t rng_step,

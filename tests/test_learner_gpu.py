@@ -161,3 +161,48 @@ def test_batched_train_and_test_run_at_scale():
     assert all(np.isfinite(pl)) and all(np.isfinite(vl))
     sc, ja, ch, rw = lr.test(300)
     assert 0 <= sc <= 1 and 0 < ja <= 1 and ch == 0 and rw >= 0
+
+
+@pytest.mark.parametrize("algo,kind", [("ippo", "comb"), ("d2d", "chsel")])
+def test_graph_rollout_equals_eager(algo, kind):
+    """The HIP-graph rollout (captured once, replayed with the device rng offset) reproduces the
+    eager slot loop bit for bit over consecutive rollouts: obs, states, actions, log-probs,
+    values, rewards and the episode statistics."""
+    from algorithms.d2d_ppo import D2DPPO
+    from algorithms.ippo import iPPO
+    from envs.channel_selection_env import ChannelSelectionEnv
+    from envs.combinatorial_env import CombinatorialEnv
+    N, C = 6, 4
+    if kind == "comb":
+        mk = lambda: CombinatorialEnv(N, C, np.array([4, 7] * 3), np.full(N, 0.3), episode_length=12,  # noqa: E731
+                                      channel_switch=np.full((N, C), 0.3), n_envs=40, device="cuda", seed=3)
+    else:
+        mk = lambda: ChannelSelectionEnv(N, C, np.full(N, 5), np.full(N, 0.3), episode_length=12,  # noqa: E731
+                                         channel_switch=np.full(C + 1, 0.3), n_envs=40, device="cuda", seed=3)
+    outs = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        env = mk()
+        common = dict(hidden_size=32, gamma=0.5, device="cuda", combinatorial=kind == "comb", early_stopping=False)
+        lr = iPPO(env, **common) if algo == "ippo" else D2DPPO(env, **common)
+        lr.graph_rollout = graph
+        res = []
+        for _ in range(3):  # 2 waves each; capture on the first, replay after (buffers are reused)
+            ro = lr._rollout(60)
+            res.append((ro.obs.clone(), ro.actions.clone(), ro.logp.clone(), ro.rewards.clone(),
+                        None if ro.values is None else ro.values.clone(),
+                        None if ro.states is None else ro.states[..., :env.state_space.shape[0]].clone(),  # no pad
+                        list(ro.scores), list(ro.ep_rewards)))
+        outs.append(res)
+        if graph:
+            assert getattr(lr, "_rollout_graphs", None), "graph path not taken"
+    for a, b in zip(*outs):
+        for x, y in zip(a, b):
+            if x is None:
+                assert y is None
+            elif isinstance(x, list):
+                assert x == y
+            else:
+                assert torch.equal(x, y)
+    # consecutive rollouts differ (fresh Philox counters on replay)
+    assert not torch.equal(outs[1][1][1], outs[1][2][1])
