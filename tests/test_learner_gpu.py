@@ -2,7 +2,8 @@
 
 For each golden learner fixture (tools/gen_fixtures.py gen_learner: iPPO and
 D2D-PPO x {MLP, GRU} x {Bernoulli/combinatorial, Categorical/channel
-selection}) the reference was run on CPU with fixed seeds:
+selection}, plus iPPO x {MLP, GRU} on the D2DEnv with neighbourhood observations) the reference
+was run on CPU with fixed seeds:
   1. create_rollouts(2) on its env, recording the actions it sampled and the
      env's random draws;
   2. one train() iteration (2 epochs) on exactly that rollout.
@@ -53,7 +54,9 @@ def build(z):
     from envs.combinatorial_env import CombinatorialEnv
     kind = str(z["kind"])
     params = _params(z)
-    env = (CombinatorialEnv if kind == "comb" else ChannelSelectionEnv)(**params, n_envs=1, device="cuda", seed=0)
+    from envs.env import D2DEnv
+    cls = {"comb": CombinatorialEnv, "chsel": ChannelSelectionEnv, "single": D2DEnv}[kind]
+    env = cls(**params, n_envs=1, device="cuda", seed=0)
     common = dict(hidden_size=int(z["hidden"]), gamma=float(z["gamma"]), policy_lr=3e-3, value_lr=1e-2,
                   device="cuda", useRNN=bool(z["useRNN"]), combinatorial=bool(z["combinatorial"]),
                   history_len=int(z["history_len"]), early_stopping=False)

@@ -482,6 +482,8 @@ LEARNER_VARIANTS = {
     "rnn_comb": ("comb", True, True, 4),
     "mlp_cat": ("chsel", False, False, 3),
     "rnn_cat": ("chsel", True, False, 3),
+    "mlp_d2denv": ("single", False, False, 3),   # iPPO only: the reference D2DPPO cannot run on D2DEnv
+    "rnn_d2denv": ("single", True, False, 3),
 }
 
 
@@ -498,6 +500,12 @@ def _learner_env(kind, episode_length=20):
             period=np.array([2] * 6), arrival_probs=setup8["arrival_probs"], offsets=setup8["offsets"],
             episode_length=episode_length, traffic_model="heterogeneous", homogeneous_size=False,
             periodic_devices=[0, 1, 2], channel_switch=setup8["channel_switch"])
+    if kind == "single":
+        mod = ref_module("envs.env")
+        p = dict(n_agents=5, deadlines=np.array([3, 5, 4, 3, 4]), lbdas=np.array([0.5] * 5),
+                 episode_length=episode_length, traffic_model="aperiodic", channel_switch=0.3,
+                 neighbourhoods=[[0, 1], [1, 2, 0], [2], [3, 4, 2], [4, 0]])
+        return mod.D2DEnv(**p), p
     mod = ref_module("envs.channel_selection_env")
     p = dict(n_agents=4, n_channels=3, deadlines=np.array([4, 6, 4, 5]), lbdas=np.array([0.6] * 4),
              episode_length=episode_length, traffic_model="aperiodic", channel_switch=np.array([0.5, 0.3, 0.7, 0.2]))
@@ -508,8 +516,12 @@ def gen_learner():
     import torch
     ippo = ref_module("algorithms.ippo")
     d2d = ref_module("algorithms.d2d_ppo")
+    import sys as _sys
+    only = [a for a in _sys.argv[2:]]
     for vname, (kind, useRNN, comb, hl) in LEARNER_VARIANTS.items():
-        for algo in ("ippo", "d2d"):
+        if only and vname not in only:
+            continue
+        for algo in (("ippo",) if kind == "single" else ("ippo", "d2d")):
             out = {"kind": kind, "useRNN": useRNN, "combinatorial": comb, "history_len": hl, "hidden": 16,
                    "gamma": 0.6, "episode_length": 20}
             env, params = _learner_env(kind)
@@ -593,7 +605,9 @@ def gen_learner():
 
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    which = sys.argv[1:] or ["data", "env", "d2denv", "gae", "learner", "baselines"]
-    for w in which:
-        {"data": gen_data, "env": gen_env, "d2denv": gen_d2denv, "gae": gen_gae, "learner": gen_learner,
-         "baselines": gen_baselines}[w]()
+    table = {"data": gen_data, "env": gen_env, "d2denv": gen_d2denv, "gae": gen_gae, "learner": gen_learner,
+             "baselines": gen_baselines}
+    # `learner <variant> ...` regenerates only the named learner variants
+    which = sys.argv[1:2] if sys.argv[1:2] == ["learner"] else sys.argv[1:]
+    for w in which or list(table):
+        table[w]()
