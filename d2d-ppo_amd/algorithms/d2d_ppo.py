@@ -217,10 +217,8 @@ class D2DPPO(BatchedLearnerBase):
         adv, _ = self._gae(ro.rewards, v_te, ro.dones, normalize_adv=True, normalize_ret=False)
         T, E, N = ro.T, ro.E, self.n_agents
         A = adv[:, :, 0].reshape(-1)                                                   # [T*E]
-        logp_old = ro.logp.permute(1, 0, 2).reshape(N, T * E)
         with torch.no_grad():
-            ratio = torch.exp(self._logp_forced(ro) - logp_old)                        # [N][T*E]
-            M = happo_chain(A, ratio, cycle)
+            M = self._chain_dev(A, self._logp_forced(ro), ro.logp, cycle, T, E)         # [N][T*E]
         pp = self.policy.params
         kind = "comb" if self.combinatorial else "chsel"
         beta = float(self.beta_entropy)
@@ -239,6 +237,20 @@ class D2DPPO(BatchedLearnerBase):
         self.value_optimizer.step()
         pl = ploss.detach().cpu().numpy()
         return [float(pl[i]) for i in cycle], value_loss.detach()
+
+    def _chain_dev(self, A, logp_new, logp_old_tne, cycle, T, E):
+        """happo_chain on the GPU (d2d_happo_chain): ratios and the sequential fp32 products in one
+        kernel, logp_old read in the rollout's [T][N][E] layout."""
+        from d2dhip import _lib
+        lib = _lib.require_gpu()
+        N = self.n_agents
+        perm = torch.as_tensor(np.asarray(cycle, dtype=np.int32), device=self.device)
+        M = torch.empty((N, T * E), dtype=torch.float32, device=self.device)
+        A = A.contiguous()
+        rc = lib.d2d_happo_chain(N, T, E, A.data_ptr(), logp_new.data_ptr(), logp_old_tne.data_ptr(), perm.data_ptr(),
+                                 M.data_ptr(), _lib.stream_ptr())
+        _lib.check(rc, "d2d_happo_chain")
+        return M
 
     def _update_epoch(self, ro, upd):
         if upd is None:

@@ -160,6 +160,41 @@ static int gae_scan(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, con
   return D2D_OK;
 }
 
+// ---------------------------------------------------------------- D2D-PPO agent chain
+// M[sigma_j][b] = adv[b] * r_sigma_0[b] * ... * r_sigma_{j-1}[b], multiplied left to right in fp32
+// like the reference's sequential loop over the permuted agents (d2d_ppo.py:405-433), with
+// r_k[b] = exp(logp_new[k][b] - logp_old[k][b]) of the epoch-start policy.  One thread per sample
+// b = t*E + e; logp_old is read in the rollout's [T][N][E] layout (no agent-major copy).
+__global__ __launch_bounds__(256) void happo_chain_kernel(int N, int T, int E, const float* __restrict__ adv,
+                                                          const float* __restrict__ logp_new,
+                                                          const float* __restrict__ logp_old,
+                                                          const int32_t* __restrict__ perm, float* __restrict__ M) {
+  const int64_t B = (int64_t)T * E;
+  const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int t = (int)(b / E), e = (int)(b - (int64_t)t * E);
+  float cur = adv[b];
+  for (int j = 0; j < N; ++j) {
+    const int k = perm[j];
+    M[(int64_t)k * B + b] = cur;
+    if (j + 1 < N) cur = expf(logp_new[(int64_t)k * B + b] - logp_old[((int64_t)t * N + k) * E + e]) * cur;
+  }
+}
+
+extern "C" int d2d_happo_chain(int32_t n_agents, int32_t T, int32_t E, const float* adv, const float* logp_new,
+                               const float* logp_old, const int32_t* perm, float* M, void* stream) {
+  if (n_agents < 1 || T < 0 || E < 0 || !adv || !logp_new || !logp_old || !perm || !M) {
+    d2d_set_error("d2d_happo_chain: bad arguments");
+    return D2D_EINVAL;
+  }
+  const int64_t B = (int64_t)T * E;
+  if (B == 0) return D2D_OK;
+  hipLaunchKernelGGL(happo_chain_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), n_agents, T, E, adv, logp_new, logp_old, perm, M);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
 extern "C" int d2d_gae_scan(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards, const float* values,
                             const uint8_t* dones, double gamma, double lam, int32_t last_shard, float* adv, float* ret,
                             void* stream) {

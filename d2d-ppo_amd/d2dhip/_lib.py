@@ -73,6 +73,7 @@ _SIGS = {
                                               _p]),
     "d2d_normalize_columns": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, _p, _p, _p, _p, _p]),
     "d2d_set_option": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),
+    "d2d_happo_chain": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p, _p, _p, _p]),
     "d2d_policy_mlp_step": (ctypes.c_int, [ctypes.POINTER(MlpDesc), _p, _p, ctypes.c_uint32, ctypes.c_int32, _p, _p,
                                             _p, _p]),
     "d2d_ppo_workspace": (ctypes.c_int64, [ctypes.c_int32] * 6),

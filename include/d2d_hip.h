@@ -194,6 +194,13 @@ int d2d_normalize_columns(int64_t rows, int32_t cols, float* x, const double* me
 int d2d_normalize_columns_tce(int32_t T, int32_t cols, int32_t E, float* x, const double* mean, const double* scale,
                               const int32_t* gate, void* stream);
 
+/* D2D-PPO's sequential agent update chain (algorithms/d2d_ppo.py:405-433): for the agent
+ * permutation perm[0..N), M[perm[j]][b] = adv[b] * prod_{l<j} exp(logp_new[perm[l]][b] -
+ * logp_old(perm[l], b)), multiplied left to right in fp32.  b = t*E + e over T*E samples;
+ * adv [T*E], logp_new [N][T*E], logp_old [T][N][E] (the rollout layout), M [N][T*E]; perm device int32. */
+int d2d_happo_chain(int32_t n_agents, int32_t T, int32_t E, const float* adv, const float* logp_new,
+                    const float* logp_old, const int32_t* perm, float* M, void* stream);
+
 /* ---- fused behaviour-policy slot (MLP learners) ----
  * Replaces Policy/Value.forward + PPO.select_action for every agent of every env
  * (algorithms/ippo.py:54-90, 154-176; d2d_ppo.py:62-98, 159-181).  Weights are the

@@ -304,3 +304,24 @@ def test_fused_epoch_matches_torch_epoch(kind, algo):
             for k in pf:
                 err = (pf[k].data - pr[k].data).abs().max().item()
                 assert err < 0.02 * lr, (ep, k, err)
+
+
+def test_happo_chain_kernel_matches_torch_loop():
+    """d2d_happo_chain == the sequential torch loop of happo_chain (d2d_ppo.py:405-433 semantics):
+    ratios exp(logp_new - logp_old) and left-to-right fp32 products over the agent permutation."""
+    from algorithms.d2d_ppo import happo_chain
+    from d2dhip import _lib
+    lib = _lib.require_gpu()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for N, T, E in ((1, 3, 5), (7, 20, 33), (64, 50, 128)):
+        adv = torch.randn(T * E, device="cuda", generator=g)
+        lp_old = -torch.rand((T, N, E), device="cuda", generator=g) * 3
+        lp_new = lp_old.permute(1, 0, 2).reshape(N, T * E) + 0.3 * torch.randn((N, T * E), device="cuda", generator=g)
+        perm = np.random.default_rng(N).permutation(N)
+        ratio = torch.exp(lp_new - lp_old.permute(1, 0, 2).reshape(N, T * E))
+        ref = happo_chain(adv, ratio, perm)
+        M = torch.empty_like(ref)
+        pt = torch.as_tensor(perm.astype(np.int32), device="cuda")
+        assert lib.d2d_happo_chain(N, T, E, adv.data_ptr(), lp_new.contiguous().data_ptr(), lp_old.data_ptr(),
+                                   pt.data_ptr(), M.data_ptr(), _lib.stream_ptr()) == 0
+        torch.testing.assert_close(M, ref, rtol=2e-6, atol=0)
