@@ -147,29 +147,45 @@ def rollout_leg(env, args, world):
     val = torch.empty_like(logp)
     b.reset(want_obs=True, out_obs=ring[0])
 
-    def slot(k):
+    K = args.rollout_steps
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+
+    def slot(k, e=None):
         if b.timestep >= env.episode_length:
             b.reset(want_obs=True, out_obs=ring[k % 2])
         with torch.no_grad():
+            if e is not None:
+                e[0].record()
             lr._policy_slot(ring, 0, k % 2, True, act, logp, val, None, b)
+            if e is not None:
+                e[1].record()
             b.step(act, want_obs=True, out_obs=ring[(k + 1) % 2], out_reward=rew)
+            if e is not None:
+                e[2].record()
 
     for k in range(10):
         slot(k)
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
-    K = args.rollout_steps
     for k in range(K):
-        slot(k)
+        slot(k, ev[k])
     torch.cuda.synchronize()
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world)
     v = b.E * world * K / el
     path = ("fused HIP policy kernel (exact 3-way bf16 split MFMA, fp32-accurate)" if lr._fused_ok()
             else "torch agent-stacked bmm")
+    pol_ms = max_over_ranks(float(np.mean([e[0].elapsed_time(e[1]) for e in ev])), world)
+    env_ms = max_over_ranks(float(np.mean([e[1].elapsed_time(e[2]) for e in ev])), world)
+    F, H, A = lr.policy.F, lr.policy.H, lr.policy.A
+    flop = 2 * (F * H + H * A) + 2 * (F * H + H)  # actor + critic forward per agent-step
+    tflops = flop * b.E * b.spec.N / (pol_ms / 1e3) / 1e12
     return {"env_steps_per_s": v, "agent_steps_per_s": v * b.spec.N, "ms_per_step": el / K * 1e3, "steps": K,
-            "policy": f"iPPO MLP H=64 actor+critic, 64 agents, Bernoulli sampling, fp32; {path}"}
+            "policy": f"iPPO MLP H=64 actor+critic, 64 agents, Bernoulli sampling, fp32; {path}",
+            "policy_kernel_us": pol_ms * 1e3, "env_kernel_us": env_ms * 1e3,
+            "policy_flop_per_agent_step": flop, "policy_tflops_fp32_equiv": tflops,
+            "policy_frac_of_fp32_matrix_peak": tflops / 157.3}
 
 
 def ppo_leg(args, rank, world, local):

@@ -103,7 +103,7 @@ __device__ __forceinline__ void load_obs_tile(float (&xf)[KS], const float* __re
 // prefetch), or kModeRuntime (tested per launch from a.forced / a.deterministic).
 template <int KIND, bool CRITIC, bool HALF = false, int MODE = kModeRuntime>
 __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, float value, int env, bool env_ok,
-                                                int k, int g) {
+                                                int k, int g, uint32_t rng) {
   const int N = a.N, A = a.A;
   constexpr bool critic = CRITIC;
   const int ga = HALF ? (g & 1) : g;
@@ -143,7 +143,7 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
 #pragma unroll
       for (int r = 0; r < 4; ++r) taken |= (uint32_t)(p[r] > 0.5f) << r;  // dist.probs > 0.5 (ippo.py:166)
     } else {
-      const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step + (a.rng_off ? *a.rng_off : 0u), (kStreamPolicy << 24) | (uint32_t)ga, a.seed);
+      const u32x4 rr = philox(genv, (uint32_t)k, rng, (kStreamPolicy << 24) | (uint32_t)ga, a.seed);
 #pragma unroll
       for (int r = 0; r < 4; ++r) taken |= (uint32_t)((float)(pick(rr, r) >> 8) * (1.f / 16777216.f) < p[r]) << r;
     }
@@ -185,7 +185,7 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
       chosen = bi;
     } else {
       // prefix over lane groups: exclusive sum of psum for groups < g
-      const u32x4 rr = philox(genv, (uint32_t)k, a.rng_step + (a.rng_off ? *a.rng_off : 0u), (kStreamPolicy << 24), a.seed);
+      const u32x4 rr = philox(genv, (uint32_t)k, rng, (kStreamPolicy << 24), a.seed);
       const float u = (float)(rr.x >> 8) * (1.f / 16777216.f) * tot;
       const float s16 = uf(partner16(fu(psum), g));  // partner in pair (g ^ 1)
       const float pair = psum + s16;
@@ -231,6 +231,8 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
 // KIND 0 Bernoulli / 1 Categorical, CRITIC: iPPO per-agent critic present
 template <int KS, int HT, int KIND, bool CRITIC>
 __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
+  // Philox step of the launch, read once (the optional device offset of graph replays)
+  const uint32_t rng = a.rng_off ? a.rng_step + *a.rng_off : a.rng_step;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;   // lane group: k-slot of A/B operands, row group of C/D
   const int i = lane & 15;   // row of A / column of B, C/D (the env of the tile)
@@ -321,7 +323,7 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) lg[r] *= kLog2e;
-    policy_epilogue<KIND, CRITIC>(a, lg, value, env, env_ok, k, g);
+    policy_epilogue<KIND, CRITIC>(a, lg, value, env, env_ok, k, g, rng);
   }
 }
 
@@ -363,6 +365,9 @@ __device__ __forceinline__ void stage_inputs(float (&x)[KC][8], const float* slo
 template <int KC, int HT, int KIND, bool CRITIC, int MODE>
 __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpArgs a) {  // waves / SIMD
   static_assert(HT % 2 == 0, "layer 2 consumes hidden tiles in pairs");
+  // Philox step of the launch, read once before the obs pipeline starts (the optional device
+  // offset of graph replays; a load inside the epilogue would add a wait to every tile pair)
+  const uint32_t rng = (MODE == kModeSample && a.rng_off) ? a.rng_step + *a.rng_off : a.rng_step;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int i = lane & 15;
@@ -547,10 +552,10 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
 #pragma unroll
       for (int r = 0; r < 4; ++r) lgc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(lg0[r]), fu(lg1[r]), false, false)[0]);
       const int envc = g < 2 ? env0 : env1;
-      policy_epilogue<KIND, CRITIC, true, MODE>(a, lgc, g < 2 ? v0 : v1, envc, envc < a.E, k, g);
+      policy_epilogue<KIND, CRITIC, true, MODE>(a, lgc, g < 2 ? v0 : v1, envc, envc < a.E, k, g, rng);
     } else {
-      policy_epilogue<KIND, CRITIC, false, MODE>(a, lg0, v0, env0, env0 < a.E, k, g);
-      policy_epilogue<KIND, CRITIC, false, MODE>(a, lg1, v1, env1, env1 < a.E, k, g);
+      policy_epilogue<KIND, CRITIC, false, MODE>(a, lg0, v0, env0, env0 < a.E, k, g, rng);
+      policy_epilogue<KIND, CRITIC, false, MODE>(a, lg1, v1, env1, env1 < a.E, k, g, rng);
     }
   }
   wait_vmem<0>();  // no LDS-DMA may land after the wave (and its LDS allocation) is gone
