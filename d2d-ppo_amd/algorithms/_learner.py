@@ -330,10 +330,18 @@ class BatchedLearnerBase(DataParallelMixin):
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize(self.device)
             result = self._rollout_result(bufs, b, waves, True)
-            base = b.rng_step
+            base, ts = b.rng_step, b.timestep
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._waves(bufs, b, waves, True, None)
+            try:
+                # thread_local: other threads' runtime calls (e.g. a process group's watchdog
+                # querying its events) do not invalidate this thread's capture
+                with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                    self._waves(bufs, b, waves, True, None)
+            except RuntimeError as err:  # capture unsupported here: keep the eager slot loop
+                b.rng_step, b.timestep = base, ts
+                self.graph_rollout = False
+                print(f"[d2d] rollout graph capture failed ({err}); eager rollouts from now on")
+                return result
             G = dict(graph=g, bufs=bufs, base=base, delta=b.rng_step - base)
             b.rng_step = base  # capturing ran nothing
             cache[key] = G
