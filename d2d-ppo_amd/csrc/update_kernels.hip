@@ -40,6 +40,16 @@
 
 #include "mlp_common.h"
 
+#ifndef D2D_UPD_ABLATE
+#define D2D_UPD_ABLATE 0  // != 0 only in tools/gpu/ablate_update.py's timing builds
+#endif
+#ifndef D2D_LOGITS_BF16
+// logits Z^T = W2 . relu(HT) on bf16 MFMAs: W2's three-way split against a two-way RNE split of
+// relu(HT) (<= 2^-17 relative per product), 3 x 16 instead of 4 x 32 MFMA cycles per hidden tile
+// (actor kernel 2.55 -> 2.44 ms per 26 M agent-samples); 0 = v_mfma_f32_16x16x4_f32 (exact fmaf chain)
+#define D2D_LOGITS_BF16 1
+#endif
+
 namespace d2d {
 
 struct UpdArgs {
@@ -353,6 +363,9 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   // the four consecutive registers the MFMA reads (no operand assembly moves)
   __shared__ __attribute__((aligned(16))) bf16x8 w2b_s[HT][3][64];
   __shared__ __attribute__((aligned(16))) float w2f_s[HT][64][4];        // Z^T's fp32 A operand
+#if D2D_LOGITS_BF16
+  __shared__ __attribute__((aligned(16))) bf16x8 w2z_s[HT][3][64];       // Z^T's bf16 A operands [h|h], [m|m], [l|0]
+#endif
   {
     const float* W1 = a.w1 + (size_t)k * H * F;
     const float* W2 = a.w2 + (size_t)k * A * H;
@@ -388,6 +401,18 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
         const int hid = 16 * t + 4 * g + r;
         w2f_s[t][lane][r] = (i < A && hid < H) ? W2[(size_t)i * H + hid] : 0.f;
       }
+#if D2D_LOGITS_BF16
+      {
+        float wz[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wz[r] = w2f_s[t][lane][r];
+        const Parts4 pz = split3_4(wz);
+        const uint32_t zero2[2] = {0u, 0u};
+        w2z_s[t][0][lane] = cat(pz.h, pz.h);
+        w2z_s[t][1][lane] = cat(pz.m, pz.m);
+        w2z_s[t][2][lane] = cat(pz.l, zero2);
+      }
+#endif
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) b2i[r] = 4 * g + r < A ? a.b2[(size_t)k * A + 4 * g + r] : 0.f;
@@ -487,7 +512,26 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
         for (int t2 = 0; t2 < HT; ++t2) {
           const f32x4 w2f = *reinterpret_cast<const f32x4*>(&w2f_s[t2][lane][0]);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) z = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[r], relu(ht[t2][r]), z, 0, 0, 0);
+          for (int r = 0; r < 4; ++r)
+#if D2D_UPD_ABLATE == 2  // timing ablation: logits without the fp32 MFMAs
+            z[r] += w2f[r] * relu(ht[t2][r]);
+#elif D2D_LOGITS_BF16
+            (void)w2f;
+#else
+            z = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[r], relu(ht[t2][r]), z, 0, 0, 0);
+#endif
+#if D2D_LOGITS_BF16
+          {  // relu(HT) on a two-way RNE split in the k-slots [h_h | h_m] against W2's h, m, l parts
+            float hv[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hv[r] = relu(ht[t2][r]);
+            const Parts2x4 hp = split2_4(hv);
+            const bf16x8 bh = cat(hp.h, hp.m);
+            z = mfma_bf16(w2z_s[t2][2][lane], bh, z);
+            z = mfma_bf16(w2z_s[t2][1][lane], bh, z);
+            z = mfma_bf16(w2z_s[t2][0][lane], bh, z);
+          }
+#endif
         }
         zt[s] = z;
       }
@@ -499,7 +543,11 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
 #pragma unroll
         for (int r = 0; r < 4; ++r) zc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(zt[0][r]), fu(zt[1][r]), false, false)[0]);
         const int e = e0 + 16 * (g >> 1) + i;
+#if D2D_UPD_ABLATE == 1  // timing ablation: no epilogue (dz = z)
+        const f32x4 dzc = zc;
+#else
         const f32x4 dzc = ppo_dz<KIND, true>(a, zc, cur.act[0], cur.lo[0], cur.w[0], e < a.E, g & 1, surr_acc, ent_acc);
+#endif
         db2 += dzc;
         *reinterpret_cast<f32x4*>(&zb[g >> 1][i][4 * (g & 1)]) = dzc;
 #pragma unroll
@@ -591,7 +639,9 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
 #pragma unroll
           for (int q = 0; q < QT; ++q) {
             if constexpr (!XE) dw1[t2][q] = mfma_bf16(d_hm, bx2[q], dw1[t2][q]);
+#if D2D_UPD_ABLATE != 3  // timing ablation 3: no dW1 products
             dw1[t2][q] = mfma_bf16(d_hm, bx1[q], dw1[t2][q]);
+#endif
           }
         }
       }

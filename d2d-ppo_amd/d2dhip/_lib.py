@@ -13,6 +13,9 @@ import torch  # noqa: F401  (must be imported before the HIP library is loaded)
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libd2dhip.so")
+# A/B timing builds only (tools/gpu/ablate_update.py): another in-tree build of the same library
+if os.environ.get("D2D_LIB_VARIANT"):
+    LIB_PATH = os.path.join(PKG_DIR, "lib", f"libd2dhip_{os.environ['D2D_LIB_VARIANT']}.so")
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
