@@ -231,7 +231,9 @@ __device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, uint32_t act,
       lsum += valid[r] ? (bit ? l1 : l0) : 0.f;
       esum += valid[r] ? -(p[r] * l1 + (1.f - p[r]) * l0) : 0.f;
       logit[r] = l1 - l0;
-      dsur[r] = (valid[r] && inside) ? (bit ? __builtin_amdgcn_rcpf(pc) : -__builtin_amdgcn_rcpf(1.f - pc)) : 0.f;
+      // d log_prob / dp: 1/pc or -1/(1-pc) -- one reciprocal of the selected denominator
+      const float rden = __builtin_amdgcn_rcpf(bit ? pc : 1.f - pc);
+      dsur[r] = (valid[r] && inside) ? (bit ? rden : -rden) : 0.f;
     }
     logp = group_sum<HALF>(lsum) * a.inv_A;
     ent = group_sum<HALF>(esum) * a.inv_A;
