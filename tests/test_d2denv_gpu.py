@@ -133,7 +133,7 @@ def test_philox_matches_oracle(name):
     _philox_case(params, E=129, steps=12, seed=20261016)
 
 
-@pytest.mark.parametrize("N,full", [(65, False), (96, True), (200, False)])
+@pytest.mark.parametrize("N,full", [(65, False), (96, True), (200, False), (1024, False)])
 def test_philox_large_agent_counts(N, full):
     """N > 64: one env per workgroup, LDS-accumulated attempt counts; full neighbourhoods
     make obs rows N*(d+1)+1 long (gathered from the env's rows staged in LDS)."""

@@ -155,8 +155,10 @@ def test_philox_matches_c_oracle(name):
     _philox_case(str(z["kind"]), params, E=257, steps=15, seed=20261015)
 
 
-@pytest.mark.parametrize("N,C,D", [(65, 8, 7), (128, 8, 14), (256, 8, 7), (100, 16, 20), (96, 32, 3)])
+@pytest.mark.parametrize("N,C,D", [(65, 8, 7), (128, 8, 14), (256, 8, 7), (100, 16, 20), (96, 32, 3),
+                                   (512, 8, 7), (1024, 2, 4)])  # N > 64 stages an env's obs + state in LDS
 def test_philox_large_agent_counts(N, C, D):
+    """N > 64: one env per workgroup (up to 1,024 agents, 16 waves)."""
     params = dict(n_agents=N, n_channels=C, deadlines=np.array([D, max(1, D // 2)] * (N // 2) + [D] * (N % 2)),
                   lbdas=np.full(N, 0.3), episode_length=6, traffic_model="aperiodic",
                   channel_switch=np.full((N, C), 0.4))
@@ -290,3 +292,13 @@ def test_full_size_episode_invariants():
     buf = torch.from_numpy(b.buffers_host().astype(np.int64)).to(b.device).sum((1, 2))
     assert bool((recv == disc + delivered + buf).all())
     assert int(delivered.sum()) > 0 and int(disc.sum()) > 0
+
+
+def test_oversized_env_rejected_loudly():
+    """An env whose obs + state rows exceed the workgroup's LDS (N > 64 stages the whole env) is
+    refused with NotImplementedError before any launch, not computed wrongly."""
+    N, C, D = 1024, 32, 32
+    env = make_env("comb", dict(n_agents=N, n_channels=C, deadlines=np.full(N, D), lbdas=np.full(N, 0.1),
+                                episode_length=4, channel_switch=np.full((N, C), 0.4)), n_envs=2, device="cuda", seed=1)
+    with pytest.raises(NotImplementedError, match="LDS"):
+        env.reset_batched(want_obs=True, want_state=True)
