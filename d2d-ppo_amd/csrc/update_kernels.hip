@@ -873,7 +873,11 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
           float pv = 0.f;
 #pragma unroll
           for (int t2 = 0; t2 < HT; ++t2) pv = fmaf(relu(hv[t2][r]), v2f[t2], pv);
+#if D2D_UPD_ABLATE == 4  // timing ablation: no cross-lane value reduction
+          const float v = pv + c2;
+#else
           const float v = row_sum16(pv) + c2;
+#endif
           const bool ok = e0 + 16 * s + 4 * g + r < a.E;
           const float d = v - R[s][r];
           dvs[r] = ok ? 2.f * a.scale * d : 0.f;
@@ -910,7 +914,9 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
 #pragma unroll
           for (int q = 0; q < QT; ++q) {
             if constexpr (!XE) dv1[t2][q] = mfma_bf16(d_hm, bx2[q], dv1[t2][q]);
+#if D2D_UPD_ABLATE != 5  // timing ablation 5: no dV1 products
             dv1[t2][q] = mfma_bf16(d_hm, bx1[q], dv1[t2][q]);
+#endif
           }
         }
       }

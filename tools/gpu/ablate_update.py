@@ -21,28 +21,37 @@ net = {{"w1": torch.randn(N, H, F, device="cuda", generator=g) * 0.1, "b1": torc
        "w2": torch.randn(N, A, H, device="cuda", generator=g) * 0.1, "b2": torch.zeros(N, A, device="cuda")}}
 obs = torch.randint(0, 3, (T, E, N, F), device="cuda", generator=g).float()
 acts = pack_masks_torch(torch.randint(0, 2, (T, E, N, A), device="cuda", generator=g)).contiguous()
-lo = -torch.rand(T, E, N, device="cuda", generator=g)
-W = torch.randn(T, E, N, device="cuda", generator=g)
-for _ in range(2):
-    actor_grads(net, obs, acts, lo, W, "comb")
-torch.cuda.synchronize()
-ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-ev[0].record()
-for _ in range(5):
-    actor_grads(net, obs, acts, lo, W, "comb")
-ev[1].record()
-torch.cuda.synchronize()
-print(json.dumps({{"ms": ev[0].elapsed_time(ev[1]) / 5}}))
+# per-sample scalars in the learner's [T][N][E] layout, viewed as [T][E][N] (coalesced over envs)
+lo = -torch.rand(T, N, E, device="cuda", generator=g).permute(0, 2, 1)
+W = torch.randn(T, N, E, device="cuda", generator=g).permute(0, 2, 1)
+from d2dhip.update import critic_grads
+vnet = {{"w1": net["w1"].clone(), "b1": net["b1"].clone(), "w2": torch.randn(N, 1, H, device="cuda", generator=g) * 0.1,
+        "b2": torch.zeros(N, 1, device="cuda")}}
+R = torch.randn(T, N, E, device="cuda", generator=g).permute(0, 2, 1)
+res = {{}}
+for name, fn in (("actor", lambda: actor_grads(net, obs, acts, lo, W, "comb")),
+                 ("critic", lambda: critic_grads(vnet, obs, R))):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(5):
+        fn()
+    ev[1].record()
+    torch.cuda.synchronize()
+    res[name] = ev[0].elapsed_time(ev[1]) / 5
+print(json.dumps(res))
 '''
 
 if __name__ == "__main__":
     out = {}
-    for v in ["", "abl1", "abl2", "abl3", "lf32"]:
+    for v in ["", "abl1", "abl2", "abl3", "abl4", "abl5", "lf32"]:
         env = dict(os.environ)
         if v:
             env["D2D_LIB_VARIANT"] = v
         r = subprocess.run([sys.executable, "-c", CODE.format(root=ROOT)], env=env, capture_output=True, text=True,
                            timeout=300)
         line = [l for l in r.stdout.splitlines() if l.startswith("{")]
-        out[v or "base"] = json.loads(line[-1])["ms"] if line else r.stderr[-500:]
+        out[v or "base"] = json.loads(line[-1]) if line else r.stderr[-500:]
     print(json.dumps(out, indent=1))

@@ -2,7 +2,7 @@
 set -e
 cd "$(dirname "$0")/../../d2d-ppo_amd"
 mkdir -p build/abl lib
-for n in 1 2 3; do
+for n in 1 2 3 4 5; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize --offload-arch=gfx950 -I../include -Icsrc \
     -DD2D_UPD_ABLATE=$n -c csrc/update_kernels.hip -o build/abl/update_kernels_$n.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib/libd2dhip_abl$n.so build/env_kernels.o \
