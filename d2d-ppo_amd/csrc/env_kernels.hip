@@ -1016,7 +1016,9 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
   };
   // single: 512-lane blocks amortise each gather-code load over more envs (measured 256: 130 us,
   // 512: 125 us, 1024: 134 us per 65,536 x 64-agent step)
-  int block = large ? a.seg : kind == D2D_ENV_SINGLE ? 512 : 256;
+  // 512-lane blocks (8 envs of 64 agents): comb 64 x 8 x 65,536 141 -> 137 us against 256-lane
+  // blocks; single: 8 envs per gather-table read (256: 130 us, 512: 125 us, 1024: 134 us)
+  int block = large ? a.seg : 512;
   a.cnt_words = cnt_words(large ? 1 : block / a.seg);
   while (!large && block > kWave && block > a.seg && lds_need(a, block, kind) > 65536) {
     block >>= 1;
