@@ -317,7 +317,10 @@ class BatchedLearnerBase(DataParallelMixin):
         training rollout of the same shape."""
         env = self.env
         L = env.episode_length
-        key = (b.E, L, waves, bool(want_values), bool(want_state))
+        # the graph bakes in the env batch's state buffers and the stacked parameters' addresses
+        key = (id(b), b.E, L, waves, bool(want_values), bool(want_state),
+               tuple(t.data_ptr() for t in self.policy.params.values()),
+               tuple(t.data_ptr() for t in getattr(self.value, "params", {}).values()) if hasattr(self, "value") else ())
         cache = self.__dict__.setdefault("_rollout_graphs", {})
         G = cache.get(key)
         if G is None:
