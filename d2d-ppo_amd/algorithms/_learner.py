@@ -448,6 +448,7 @@ class BatchedLearnerBase(DataParallelMixin):
         for i, agent in enumerate(self.agents):
             sd = torch.load(f"{checkpoint_path}/agent_{i}.pth", map_location=self.device, weights_only=True)
             agent.policy_network.load_state_dict(sd)
+        self._policy_version = getattr(self, "_policy_version", 0) + 1  # rollouts before this are stale
         print("Models loaded!")
 
     def preprocess_input_for_rnn(self, obs_agent):

@@ -143,6 +143,7 @@ class D2DPPO(BatchedLearnerBase):
     # ------------------------------------------------------------ rollouts
     def _rollout(self, num_episodes, teacher=None):
         ro = self._collect(num_episodes, train=True, want_state=True, teacher=teacher)
+        ro.policy_version = getattr(self, "_policy_version", 0)  # actor parameters the rollout used
         S = self.env.state_space.shape[0]
         ro.state_seq = ro.states[:, :, :S].transpose(0, 1).reshape(ro.E * ro.T, S)     # [E*T][S]
         # returns = discount_rewards(rewards (T,N)).mean(1) (d2d_ppo.py:333,339): every agent has the
@@ -193,6 +194,7 @@ class D2DPPO(BatchedLearnerBase):
         self._reduce_grads(self.policy.parameters())
         self.policy.grad_norm_clip_(20)
         self.policy_optimizer.step()
+        self._policy_version = getattr(self, "_policy_version", 0) + 1
         # 4) critic update (d2d_ppo.py:440-446)
         value_loss = F.mse_loss(values, ro.ret_mean, reduction='mean')
         self.value_optimizer.zero_grad()
@@ -218,7 +220,13 @@ class D2DPPO(BatchedLearnerBase):
         T, E, N = ro.T, ro.E, self.n_agents
         A = adv[:, :, 0].reshape(-1)                                                   # [T*E]
         with torch.no_grad():
-            M = self._chain_dev(A, self._logp_forced(ro), ro.logp, cycle, T, E)         # [N][T*E]
+            if getattr(ro, "policy_version", -1) == getattr(self, "_policy_version", 0):
+                # first epoch on this rollout: the epoch-start actors ARE the rollout's, and the
+                # policy kernel's forced log-probs equal the sampled ones bit for bit, so every
+                # ratio is exactly 1 and the chain is A for every agent (no forced pass needed)
+                M = A.expand(N, T * E)
+            else:
+                M = self._chain_dev(A, self._logp_forced(ro), ro.logp, cycle, T, E)     # [N][T*E]
         pp = self.policy.params
         kind = "comb" if self.combinatorial else "chsel"
         beta = float(self.beta_entropy)
@@ -228,6 +236,7 @@ class D2DPPO(BatchedLearnerBase):
         self._reduce_grads(self.policy.parameters())
         self.policy.grad_norm_clip_(20)
         self.policy_optimizer.step()
+        self._policy_version = getattr(self, "_policy_version", 0) + 1
         ploss = -(sa[:, 0] + beta * sa[:, 1]) / (T * E)
         value_loss = F.mse_loss(values, ro.ret_mean, reduction='mean')
         self.value_optimizer.zero_grad()
