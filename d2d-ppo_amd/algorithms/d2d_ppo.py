@@ -214,7 +214,8 @@ class D2DPPO(BatchedLearnerBase):
         cycle = np.arange(self.n_agents)
         np.random.shuffle(cycle)
         cycle = self._sync_perm(cycle)
-        values = self.value_network(ro.state_seq).squeeze()
+        crit = self._critic_split_forward(ro)
+        values = crit[0] if crit is not None else self.value_network(ro.state_seq).squeeze()
         v_te = values.detach().view(ro.E, ro.T).t().unsqueeze(2).contiguous()
         adv, _ = self._gae(ro.rewards, v_te, ro.dones, normalize_adv=True, normalize_ret=False)
         T, E, N = ro.T, ro.E, self.n_agents
@@ -238,14 +239,75 @@ class D2DPPO(BatchedLearnerBase):
         self.policy_optimizer.step()
         self._policy_version = getattr(self, "_policy_version", 0) + 1
         ploss = -(sa[:, 0] + beta * sa[:, 1]) / (T * E)
-        value_loss = F.mse_loss(values, ro.ret_mean, reduction='mean')
-        self.value_optimizer.zero_grad()
-        value_loss.backward()
+        if crit is not None:
+            value_loss = self._critic_split_backward(ro, crit)
+        else:
+            value_loss = F.mse_loss(values, ro.ret_mean, reduction='mean')
+            self.value_optimizer.zero_grad()
+            value_loss.backward()
         self._reduce_grads(list(self.value_network.parameters()))
         torch.nn.utils.clip_grad_norm_(self.value_network.parameters(), 20)
         self.value_optimizer.step()
         pl = ploss.detach().cpu().numpy()
         return [float(pl[i]) for i in cycle], value_loss.detach()
+
+    # ------------------------------------------------ central critic on bf16 split GEMMs
+    critic_split = True
+    CRITIC_SPLIT_MIN_DIM = 256  # below this state width the fp32 GEMMs are launch-bound anyway
+
+    def _critic_split_forward(self, ro):
+        """Value(state) = linear2(relu(linear1(state))) (d2d_ppo.py:95-98) for all T*E states with the
+        first layer as ONE bf16 GEMM with fp32 output: the states are small integers (buffer counts,
+        channel bits, ACKs) and so exact in bf16, and W1 is split three ways (h + m + l, exact), so
+        the product is fp32-accurate at the bf16 matrix rate.  Returns (values, pre-activation,
+        hidden) or None when the fp32 torch path applies (small states or non-integer states)."""
+        S = ro.state_seq.shape[1]
+        if not self.critic_split or S < self.CRITIC_SPLIT_MIN_DIM:
+            return None
+        xb = getattr(ro, "state_bf16", None)
+        if xb is None:
+            # the env kernels' states are integer-valued by construction (buffer counts <= 255,
+            # channel bits, ACKs in {-1, 0, 1}); a spot check of the first rows guards the rest
+            head = ro.state_seq[:4096]
+            if not torch.equal(head.to(torch.bfloat16).float(), head):
+                self.critic_split = False  # fractional states: keep torch fp32
+                return None
+            xb = ro.state_bf16 = ro.state_seq.to(torch.bfloat16)
+        l1, l2 = self.value_network.linear1, self.value_network.linear2
+        H = l1.weight.shape[0]
+        with torch.no_grad():
+            w = l1.weight
+            wh = w.to(torch.bfloat16)
+            r = w - wh.float()
+            wm = r.to(torch.bfloat16)
+            wl = (r - wm.float()).to(torch.bfloat16)
+            z3 = torch.mm(xb, torch.cat([wh, wm, wl], 0).t(), out_dtype=torch.float32)   # [B][3H]
+            pre = (z3[:, :H] + z3[:, H:2 * H]) + z3[:, 2 * H:] + l1.bias
+            hid = torch.relu(pre)
+            v = torch.addmm(l2.bias, hid, l2.weight.t())[:, 0]
+        return v, pre, hid
+
+    def _critic_split_backward(self, ro, crit):
+        """Gradients of mse(V, returns) into the critic's .grad (what value_loss.backward() leaves):
+        dW1 = dPreᵀ X on a two-way RNE bf16 split of dPre (≤ 2^-17 relative per product term, as in
+        the fused update kernels) against the exact bf16 states."""
+        v, pre, hid = crit
+        l1, l2 = self.value_network.linear1, self.value_network.linear2
+        H = l1.weight.shape[0]
+        with torch.no_grad():
+            d = v - ro.ret_mean
+            value_loss = (d * d).mean()
+            dv = d * (2.0 / d.numel())                                                  # [B]
+            g_w2 = (dv[None, :] @ hid)                                                  # [1][H]
+            g_b2 = dv.sum().reshape(1)
+            dpre = torch.where(pre > 0, dv[:, None] * l2.weight, torch.zeros_like(pre))  # [B][H]
+            dh = dpre.to(torch.bfloat16)
+            dm = (dpre - dh.float()).to(torch.bfloat16)
+            g = torch.mm(torch.cat([dh, dm], 1).t(), ro.state_bf16, out_dtype=torch.float32)  # [2H][S]
+            grads = {l1.weight: g[:H] + g[H:], l1.bias: dpre.sum(0), l2.weight: g_w2, l2.bias: g_b2}
+            for prm, gr in grads.items():
+                prm.grad = gr.reshape(prm.shape).contiguous()
+        return value_loss
 
     def _chain_dev(self, A, logp_new, logp_old_tne, cycle, T, E):
         """happo_chain on the GPU (d2d_happo_chain): ratios and the sequential fp32 products in one

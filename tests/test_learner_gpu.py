@@ -209,3 +209,33 @@ def test_graph_rollout_equals_eager(algo, kind):
                 assert torch.equal(x, y)
     # consecutive rollouts differ (fresh Philox counters on replay)
     assert not torch.equal(outs[1][1][1], outs[1][2][1])
+
+
+def test_d2d_central_critic_split_gemm_matches_fp32():
+    """The central critic on bf16 split GEMMs (exact bf16 states x three-way split W1; dPre two-way
+    split) == torch fp32 autograd of mse(Value(state), returns): values to 1e-5 relative,
+    gradients to 2e-5 of their largest entry."""
+    from algorithms.d2d_ppo import D2DPPO
+    from envs.combinatorial_env import CombinatorialEnv
+    N, C = 12, 8
+    env = CombinatorialEnv(N, C, np.array([7, 14] * 6), np.full(N, 0.4), episode_length=20,
+                           channel_switch=np.full((N, C), 0.3), n_envs=64, device="cuda", seed=4)
+    torch.manual_seed(2)
+    lr = D2DPPO(env, hidden_size=64, gamma=0.5, device="cuda", combinatorial=True, early_stopping=False)
+    lr.CRITIC_SPLIT_MIN_DIM = 0
+    ro = lr._rollout(64)
+    crit = lr._critic_split_forward(ro)
+    assert crit is not None
+    loss = lr._critic_split_backward(ro, crit)
+    got = {n: p.grad.clone() for n, p in lr.value_network.named_parameters()}
+    for p in lr.value_network.parameters():
+        p.grad = None
+    v = lr.value_network(ro.state_seq).squeeze()
+    ref_loss = torch.nn.functional.mse_loss(v, ro.ret_mean)
+    ref_loss.backward()
+    torch.testing.assert_close(crit[0], v.detach(), rtol=1e-5, atol=1e-5)
+    assert abs(loss.item() - ref_loss.item()) <= 1e-5 * abs(ref_loss.item()) + 1e-7
+    for n, p in lr.value_network.named_parameters():
+        scale = p.grad.abs().max().item()
+        err = (got[n] - p.grad).abs().max().item()
+        assert err <= 2e-5 * scale + 1e-8, (n, err, scale)
