@@ -46,12 +46,13 @@ print(json.dumps(res))
 
 if __name__ == "__main__":
     out = {}
-    for v in ["", "abl1", "abl2", "abl3", "abl4", "abl5", "lf32"]:
+    variants = sys.argv[1:] or ["", "abl1", "abl2", "abl3", "abl4", "abl5", "lf32"]
+    for n, v in enumerate(variants):
         env = dict(os.environ)
         if v:
             env["D2D_LIB_VARIANT"] = v
         r = subprocess.run([sys.executable, "-c", CODE.format(root=ROOT)], env=env, capture_output=True, text=True,
                            timeout=300)
         line = [l for l in r.stdout.splitlines() if l.startswith("{")]
-        out[v or "base"] = json.loads(line[-1]) if line else r.stderr[-500:]
+        out[f"{n}:{v or 'base'}"] = json.loads(line[-1]) if line else r.stderr[-500:]
     print(json.dumps(out, indent=1))
