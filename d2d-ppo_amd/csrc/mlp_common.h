@@ -52,6 +52,20 @@ __device__ __forceinline__ uint32_t partner32(uint32_t v, int g) {
 
 // relu as one v_max_i32 on the bit pattern (negative floats are negative ints, -0 -> +0);
 // fmaxf(x, 0) costs a NaN-quieting canonicalize plus the max under the IEEE mode
+// XCD-aware block mapping.  MI355X dispatches workgroups round-robin over its 8 XCDs, each with
+// its own L2, so in an agent-fast grid (x = agent) the agents of one env chunk -- whose obs rows
+// ([env][agent][F] floats) share cache lines -- land on eight different L2s and every line is
+// fetched by about two of them.  The remap gives XCD j the j-th contiguous eighth of the
+// x-fast block order (a bijection on the first 8 * floor(total / 8) blocks, identity on the
+// rest), so an env chunk's agents run on one XCD.  bx, by are wave-uniform.
+__device__ __forceinline__ void xcd_block(int& bx, int& by) {
+  const uint32_t nx = gridDim.x, total = nx * gridDim.y, per = total / 8;
+  uint32_t b = blockIdx.x + nx * blockIdx.y;
+  if (b < per * 8) b = (b % 8) * per + b / 8;
+  bx = (int)(b % nx);
+  by = (int)(b / nx);
+}
+
 __device__ __forceinline__ float relu(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
 
 // channel masks of 1 / 2 / 4 bytes (d2d_mask_bytes): one typed access, no byte loop

@@ -101,9 +101,11 @@ __device__ __forceinline__ void load_obs_tile(float (&xf)[KS], const float* __re
 // MODE: kModeSample / kModeDeterministic / kModeForced as a compile-time constant (the split
 // kernel: no forced-mask load exists in the sampling kernel, so nothing in it can drain the obs
 // prefetch), or kModeRuntime (tested per launch from a.forced / a.deterministic).
-template <int KIND, bool CRITIC, bool HALF = false, int MODE = kModeRuntime>
+// PRE (forced mode): the forced mask / id was loaded ahead by the caller and arrives in `fpre`
+// (the split kernel's paired epilogue); otherwise the epilogue loads it itself.
+template <int KIND, bool CRITIC, bool HALF = false, int MODE = kModeRuntime, bool PRE = false>
 __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, float value, int env, bool env_ok,
-                                                int k, int g, uint32_t rng) {
+                                                int k, int g, uint32_t rng, uint32_t fpre = 0) {
   const int N = a.N, A = a.A;
   constexpr bool critic = CRITIC;
   const int ga = HALF ? (g & 1) : g;
@@ -134,11 +136,12 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
   int out_id = 0;
   if constexpr (KIND == 0) {
     // ---- Bernoulli per channel (combinatorial): u < p, one Philox block per lane group
-    // bit r of `taken` = action 4g + r.  Each mode computes it inside its own wave-uniform branch,
-    // so the forced-mask load is waited for there and never drains the obs prefetch in flight.
+    // bit r of `taken` = action 4g + r.  An in-epilogue forced-mask load (PRE false) is waited for
+    // with vmcnt(0), which also drains any obs prefetch in flight; the split kernel's paired
+    // epilogue therefore takes the mask preloaded (PRE).
     uint32_t taken = 0;
     if (forced) {
-      taken = (load_mask(a.forced, env_ok ? cell : 0, a.mask_bytes) >> (4 * ga)) & 0xFu;
+      taken = ((PRE ? fpre : load_mask(a.forced, env_ok ? cell : 0, a.mask_bytes)) >> (4 * ga)) & 0xFu;
     } else if (deterministic) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) taken |= (uint32_t)(p[r] > 0.5f) << r;  // dist.probs > 0.5 (ippo.py:166)
@@ -168,7 +171,7 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
     tot = group_sum<HALF>(tot);
     int chosen = 0;
     if (forced) {
-      chosen = env_ok ? reinterpret_cast<const unsigned char*>(a.forced)[cell] : 0;
+      chosen = PRE ? (int)fpre : env_ok ? reinterpret_cast<const unsigned char*>(a.forced)[cell] : 0;
     } else if (deterministic) {
       // first index of the maximum (torch.argmax)
       float bv = -INFINITY;
@@ -371,9 +374,28 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int i = lane & 15;
-  const int k = blockIdx.x;
+  int k, by;
+  xcd_block(k, by);  // k = agent, by = env chunk
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
   const int N = a.N, F = a.F, H = a.H, A = a.A;
+  const int tiles = a.envs_per_wave / 16;
+  const int wave_env0 = (by * (blockDim.x >> 6) + wave) * a.envs_per_wave;
+
+  // ---- forced mode with the paired epilogue (A <= 8: one forced byte per cell): every forced
+  // byte this lane's epilogues will read, loaded before the weight split so their latency hides
+  // under it.  A load inside the tile loop would be waited for with vmcnt(0) and drain the obs
+  // DMA ring every tile pair.  Pair p of lane (g, i) is env wave_env0 + 32 p + 16 (g >> 1) + i,
+  // byte p & 3 of word p >> 2 (envs_per_wave <= 256: at most 8 pairs).
+  // Branch-free: all eight loads are issued (clamped to cell 0), and packed after the split.
+  uint32_t fpk[2] = {0u, 0u}, fv[8];
+  if constexpr (MODE == kModeForced) {
+    const unsigned char* fb = reinterpret_cast<const unsigned char*>(a.forced);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int env = wave_env0 + 32 * p + 16 * (g >> 1) + i;
+      fv[p] = fb[(A <= 8 && 2 * p < tiles && env < a.E) ? (size_t)env * N + k : 0];
+    }
+  }
 
   // ---- weight fragments of agent k, split once per workgroup
   Parts w1p[HT][KC], v1p[CRITIC ? HT : 1][KC], w2p[HT / 2];
@@ -424,9 +446,14 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
     }
   }
   const float c2 = CRITIC ? a.c2[k] : 0.f;
+  if constexpr (MODE == kModeForced) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int env = wave_env0 + 32 * p + 16 * (g >> 1) + i;
+      fpk[p >> 2] |= (2 * p < tiles && env < a.E ? fv[p] : 0u) << (8 * (p & 3));
+    }
+  }
 
-  const int tiles = a.envs_per_wave / 16;
-  const int wave_env0 = (blockIdx.y * (blockDim.x >> 6) + wave) * a.envs_per_wave;
   // Two obs register sets alternate (loop unrolled by two), so each tile's loads are issued two
   // tiles ahead of their use without a register copy that would wait on them early.
   constexpr int RING = ring_tiles<KC>();
@@ -552,7 +579,10 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
 #pragma unroll
       for (int r = 0; r < 4; ++r) lgc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(lg0[r]), fu(lg1[r]), false, false)[0]);
       const int envc = g < 2 ? env0 : env1;
-      policy_epilogue<KIND, CRITIC, true, MODE>(a, lgc, g < 2 ? v0 : v1, envc, envc < a.E, k, g, rng);
+      const int pair = tt >> 1;  // wave-uniform
+      const uint32_t fpre = ((pair < 4 ? fpk[0] : fpk[1]) >> (8 * (pair & 3))) & 0xFFu;
+      policy_epilogue<KIND, CRITIC, true, MODE, MODE == kModeForced>(a, lgc, g < 2 ? v0 : v1, envc, envc < a.E, k,
+                                                                      g, rng, fpre);
     } else {
       policy_epilogue<KIND, CRITIC, false, MODE>(a, lg0, v0, env0, env0 < a.E, k, g, rng);
       policy_epilogue<KIND, CRITIC, false, MODE>(a, lg1, v1, env1, env1 < a.E, k, g, rng);

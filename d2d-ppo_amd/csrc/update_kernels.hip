@@ -353,7 +353,8 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   constexpr int QT = 2 * KC;  // input tiles of 16 in dW1
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, i = lane & 15;
-  const int k = blockIdx.x;
+  int k, by;
+  xcd_block(k, by);  // k = agent, by = sample-chunk group
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, A = a.A, F = a.F;
 
@@ -441,7 +442,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   float(*zb)[16][20] = dzt[wave];
 
   const int stride = a.G * 4;
-  const int tile0 = blockIdx.y * 4 + wave;
+  const int tile0 = by * 4 + wave;
   int e0 = 0;
   ActorIn<KC, PAIR> cur;  // per-sample scalars of the tile being computed
   bf16x8 xh[2][KC];
@@ -694,7 +695,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   }
   reduce_waves<NV>(acc, red, wave, lane);
   if (wave != 0) return;
-  float* out = a.partial + ((size_t)blockIdx.y * a.N + k) * a.P;
+  float* out = a.partial + ((size_t)by * a.N + k) * a.P;
   const int OB1 = H * F, OW2 = OB1 + H, OB2 = OW2 + A * H, OST = OB2 + A;
   int n = 0;
 #pragma unroll
@@ -764,7 +765,8 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
   constexpr int QT = 2 * KC;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, i = lane & 15;
-  const int k = blockIdx.x;
+  int k, by;
+  xcd_block(k, by);  // k = agent, by = sample-chunk group
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, F = a.F;
 
@@ -807,7 +809,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
   float(*xw)[XS] = xs[wave];
 
   const int stride = a.G * 4;
-  const int tile0 = blockIdx.y * 4 + wave;
+  const int tile0 = by * 4 + wave;
   int e0 = 0;
   float R[2][4];
   bf16x8 xh[2][KC];
@@ -961,7 +963,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
   }
   reduce_waves<NV>(acc, red, wave, lane);
   if (wave != 0) return;
-  float* out = a.partial + ((size_t)blockIdx.y * a.N + k) * a.P;
+  float* out = a.partial + ((size_t)by * a.N + k) * a.P;
   const int OB1 = H * F, OW2 = OB1 + H, OB2 = OW2 + H, OST = OB2 + 1;
   int n = 0;
 #pragma unroll

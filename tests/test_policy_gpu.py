@@ -125,3 +125,28 @@ def test_sampling_uses_philox_stream3(kind, F, H, A, in_dims):
     # the log-prob returned with a sample equals the forced evaluation of that sample
     _, lp2, _ = policy_mlp_step(actor, obs, kind, None, forced=acts)
     torch.testing.assert_close(lp, lp2, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("kind,F,H,A,in_dims", [CASES[0], CASES[4], CASES[3]])
+def test_forced_full_waves_equal_sampled_logp(kind, F, H, A, in_dims):
+    """Batches large enough for 256 envs per wave (8 epilogue pairs, the forced bytes preloaded
+    per wave) with a ragged tail: the forced evaluation of sampled actions reproduces their
+    log-probs bit for bit (the D2D first-epoch identity), and matches torch (1e-5, well-conditioned)."""
+    from torch.distributions import Bernoulli, Categorical
+    from d2dhip.policy import policy_mlp_step
+    from d2dhip.envbatch import pack_masks_torch
+    N, E = 8, 65536 + 1000 + 7
+    actor, _, obs = make(kind, N, E, F, H, A, in_dims, seed=4, critic=False)
+    acts, lp, _ = policy_mlp_step(actor, obs, kind, None, rng_step=2, seed=99)
+    acts2, lp2, _ = policy_mlp_step(actor, obs, kind, None, forced=acts)
+    assert torch.equal(acts2, acts)
+    torch.testing.assert_close(lp2, lp, rtol=0, atol=0)
+    probs, _ = torch_ref(actor, None, obs)
+    if kind == "comb":
+        bits = torch.stack([(acts.long() >> j) & 1 for j in range(A)], -1).transpose(0, 1).float()  # [N][E][A]
+        assert torch.equal(pack_masks_torch(bits.transpose(0, 1)), acts)
+        ref_lp = Bernoulli(probs=probs, validate_args=False).log_prob(bits).mean(-1)
+    else:
+        ref_lp = Categorical(probs=probs, validate_args=False).log_prob(acts.t().long())
+    well = ((probs > 1e-3) & (probs < 1 - 1e-3)).all(-1)
+    torch.testing.assert_close(lp2[well], ref_lp[well], rtol=0, atol=1e-5)
