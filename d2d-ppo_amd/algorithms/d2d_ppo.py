@@ -259,8 +259,8 @@ class D2DPPO(BatchedLearnerBase):
         """Value(state) = linear2(relu(linear1(state))) (d2d_ppo.py:95-98) for all T*E states with the
         first layer as ONE bf16 GEMM with fp32 output: the states are small integers (buffer counts,
         channel bits, ACKs) and so exact in bf16, and W1 is split three ways (h + m + l, exact), so
-        the product is fp32-accurate at the bf16 matrix rate.  Returns (values, pre-activation,
-        hidden) or None when the fp32 torch path applies (small states or non-integer states)."""
+        the product is fp32-accurate at the bf16 matrix rate.  Returns (values [B], pre-activation [H][B],
+        hidden [H][B]) or None when the fp32 torch path applies (small states or non-integer states)."""
         S = ro.state_seq.shape[1]
         if not self.critic_split or S < self.CRITIC_SPLIT_MIN_DIM:
             return None
@@ -281,10 +281,13 @@ class D2DPPO(BatchedLearnerBase):
             r = w - wh.float()
             wm = r.to(torch.bfloat16)
             wl = (r - wm.float()).to(torch.bfloat16)
-            z3 = torch.mm(xb, torch.cat([wh, wm, wl], 0).t(), out_dtype=torch.float32)   # [B][3H]
-            pre = (z3[:, :H] + z3[:, H:2 * H]) + z3[:, 2 * H:] + l1.bias
+            # computed transposed ([3H] x B): the 3H = 192 output rows are one GEMM tile, so the
+            # [B][S] states are streamed once (as [B][3H] the 192 columns took two 128-wide tiles
+            # and read the states twice)
+            z3 = torch.mm(torch.cat([wh, wm, wl], 0), xb.t(), out_dtype=torch.float32)   # [3H][B]
+            pre = (z3[:H] + z3[H:2 * H]) + z3[2 * H:] + l1.bias[:, None]                # [H][B]
             hid = torch.relu(pre)
-            v = torch.addmm(l2.bias, hid, l2.weight.t())[:, 0]
+            v = torch.addmm(l2.bias[:, None], l2.weight, hid)[0]                           # [B]
         return v, pre, hid
 
     def _critic_split_backward(self, ro, crit):
@@ -298,13 +301,13 @@ class D2DPPO(BatchedLearnerBase):
             d = v - ro.ret_mean
             value_loss = (d * d).mean()
             dv = d * (2.0 / d.numel())                                                  # [B]
-            g_w2 = (dv[None, :] @ hid)                                                  # [1][H]
+            g_w2 = torch.mv(hid, dv)                                                    # [H]
             g_b2 = dv.sum().reshape(1)
-            dpre = torch.where(pre > 0, dv[:, None] * l2.weight, torch.zeros_like(pre))  # [B][H]
+            dpre = torch.where(pre > 0, l2.weight.t() * dv[None, :], torch.zeros_like(pre))  # [H][B]
             dh = dpre.to(torch.bfloat16)
             dm = (dpre - dh.float()).to(torch.bfloat16)
-            g = torch.mm(torch.cat([dh, dm], 1).t(), ro.state_bf16, out_dtype=torch.float32)  # [2H][S]
-            grads = {l1.weight: g[:H] + g[H:], l1.bias: dpre.sum(0), l2.weight: g_w2, l2.bias: g_b2}
+            g = torch.mm(torch.cat([dh, dm], 0), ro.state_bf16, out_dtype=torch.float32)  # [2H][S]
+            grads = {l1.weight: g[:H] + g[H:], l1.bias: dpre.sum(1), l2.weight: g_w2, l2.bias: g_b2}
             for prm, gr in grads.items():
                 prm.grad = gr.reshape(prm.shape).contiguous()
         return value_loss
