@@ -92,14 +92,33 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-def cpu_baseline(params, seconds=12.0, max_envs=8192):  # bounded: ~`seconds` of host work
-    """C oracle ("port") on the host cores, Philox mode, same workload, bounded sample."""
-    from oracle.c_oracle import COracle
+def host_cores():
+    """CPUs this process may run on: the affinity set, capped by a cgroup CPU quota when one is set
+    (a container's share of a large host).  Returns (cores, affinity, quota or None)."""
     try:
-        cores = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, 16))
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // period)
+        except (OSError, ValueError):
+            pass
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
+def cpu_baseline_c(params, seconds=8.0, max_envs=16384):  # bounded: ~`seconds` of host work
+    """C oracle ("port") on every host core (OpenMP), Philox mode, same workload, bounded sample."""
+    from oracle.c_oracle import COracle
+    threads, aff, quota = host_cores()
     E = max_envs
     c = COracle("comb", params, n_envs=E, seed=42, nthreads=threads)
     c.reset(rng_step=0, want_state=False)
@@ -119,8 +138,74 @@ def cpu_baseline(params, seconds=12.0, max_envs=8192):  # bounded: ~`seconds` of
     v = E * steps / el
     return {"value": v, "unit": "env-steps/s", "cores": threads, "kind": "port",
             "agent_steps_per_s": v * params["n_agents"],
-            "sample": f"oracle/c/d2d_oracle.c (OpenMP, {threads} threads): {E} envs x {steps} slots of the same "
+            "sample": f"oracle/c/d2d_oracle.c (OpenMP, {threads} threads = affinity {aff}"
+                      f"{'' if quota is None else f', cgroup quota {quota}'}): {E} envs x {steps} slots of the same "
                       f"64x8 workload incl. action sampling and fp32 obs, {el:.1f} s"}
+
+
+def _numpy_worker(args):
+    """One host process of the NumPy leg: the oracle's per-env restatement of the reference step
+    (oracle/env_oracle.py, one env at a time like CombinatorialEnv.step) for `seconds`."""
+    params, proc, seconds, E = args
+    from oracle.env_oracle import EnvOracle
+    o = EnvOracle("comb", params, n_envs=E, seed=42, env_base=proc * E)
+    rng = np.random.default_rng(proc)
+    o.reset(rng_step=0)
+    rs, steps = 1, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        a = (rng.random((E, params["n_agents"], params["n_channels"])) < 0.1).astype(np.int64)
+        o.step(a, rng_step=rs)
+        rs += 1
+        steps += 1
+        if o.timestep >= params["episode_length"]:
+            o.reset(rng_step=rs)
+            rs += 1
+    return E * steps, time.perf_counter() - t0
+
+
+def cpu_baseline_numpy(params, seconds=8.0, E=4):
+    """The NumPy restatement, one process per host core.  Runs BEFORE the GPU is
+    touched (fork of a process without a HIP context).  Aggregate env-steps/s = sum over processes."""
+    import multiprocessing as mp
+    cores, aff, quota = host_cores()
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(cores) as pool:
+        res = pool.map(_numpy_worker, [(params, p, seconds, E) for p in range(cores)])
+    wall = time.perf_counter() - t0
+    v = sum(n / el for n, el in res)
+    return {"value": v, "unit": "env-steps/s", "cores": cores, "kind": "port",
+            "agent_steps_per_s": v * params["n_agents"],
+            "sample": f"oracle/env_oracle.py (NumPy, per-env loop mirroring CombinatorialEnv.step), {cores} processes "
+                      f"(affinity {aff}{'' if quota is None else f', cgroup quota {quota}'}) x {E} envs x ~{seconds:.0f} s "
+                      f"of the same 64x8 workload, fp32 obs; {wall:.1f} s wall"}
+
+
+class PhaseTimer:
+    """Splits learner work into phases with HIP events on the current stream (the learners call
+    _phase(name) after each phase; the time since the previous mark is charged to `name`)."""
+
+    def __init__(self):
+        self.marks = []
+        self.start()
+
+    def start(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.prev = e
+
+    def mark(self, name):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.marks.append((name, self.prev, e))
+        self.prev = e
+
+    def totals_ms(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, a, b in self.marks:
+            out[name] = out.get(name, 0.0) + a.elapsed_time(b)
+        return out
 
 
 def load_pmc_traffic():
@@ -290,15 +375,24 @@ def train_leg(env, args, rank, world, local):
     iteration(1)  # warm-up: allocations, kernels
     torch.cuda.synchronize()
     barrier(world)
+    lr.phase_timer = PhaseTimer()
     t0 = time.perf_counter()
     iteration(args.train_epochs)
     torch.cuda.synchronize()
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world)
+    phases = {k: max_over_ranks(v, world) for k, v in lr.phase_timer.totals_ms().items()}
+    lr.phase_timer = None
     T = env.episode_length
+    epoch_ms = sum(v for k, v in phases.items() if k not in ("rollout", "gae")) / args.train_epochs
     return {"s_per_iteration": el, "n_epoch": args.train_epochs, "envs_per_gpu": E, "slots": T,
             "agent_samples_per_epoch": E * world * T * env.n_agents,
             "env_steps_per_s_end_to_end": E * world * T / el,
+            "phase_ms": phases,
+            "ppo_ms_per_update": epoch_ms,
+            "ppo_updates_per_s": 1e3 / epoch_ms,
+            "ppo_batch": f"{E} envs/GPU x {T} slots x {env.n_agents} agents (the headline batch; one update = "
+                         f"one epoch: actor + critic gradients, all-reduce, Adam)",
             "path": "fused policy kernel + env kernel rollout, HIP GAE, fused PPO gradient kernels + Adam"}
 
 
@@ -466,7 +560,7 @@ def main():
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--episode-length", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--legs", default="env,rollout,ppo,train,configs,d2denv")
     ap.add_argument("--rollout-steps", type=int, default=60)
     ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
@@ -474,10 +568,17 @@ def main():
     ap.add_argument("--train-epochs", type=int, default=4, help="n_epoch of the train leg")
     args = ap.parse_args()
 
+    params = config3_params(args.episode_length)
+    world0 = int(os.environ.get("WORLD_SIZE", "1"))
+    cpu = None
+    if not args.no_cpu_baseline and world0 == 1:
+        # before any GPU call: the NumPy leg forks one worker per host core
+        cpu = cpu_baseline_numpy(params, seconds=args.cpu_seconds)
+        cpu["c_openmp"] = cpu_baseline_c(params, seconds=args.cpu_seconds)
+
     rank, world, local = setup_dist(args.gpus)
     from envs.combinatorial_env import CombinatorialEnv
 
-    params = config3_params(args.episode_length)
     E = args.envs
     env = CombinatorialEnv(**params, n_envs=E, device=f"cuda:{local}", seed=42)
     env.shard(rank, world)
@@ -572,8 +673,8 @@ def main():
             res["configs"] = configs
         if d2denv is not None:
             res["d2denv"] = d2denv
-        if not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(params, seconds=args.cpu_seconds)
+        if cpu is not None:
+            res["cpu_baseline"] = cpu
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

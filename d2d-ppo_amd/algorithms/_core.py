@@ -142,14 +142,16 @@ class StackedNets:
         self.params = {}
         with torch.no_grad():
             for name, shp in shapes.items():
-                t = torch.zeros((self.N,) + shp, dtype=torch.float32, device=dev)
+                # stacked where the modules live (host after construction), then ONE copy to the device
+                # (per-agent copies were 2 x N x 4 hipMemcpy calls per network)
+                t = torch.zeros((self.N,) + shp, dtype=torch.float32)
                 for k, m in enumerate(modules):
-                    src = srcs(m)[name].detach().to(dev)
+                    src = srcs(m)[name].detach().to("cpu", torch.float32)
                     if name in ("w1", "w_ih") and not (kind == "rnn" and name == "w1"):
                         t[k, :, : self.in_dims[k]] = src
                     else:
                         t[k] = src
-                self.params[name] = nn.Parameter(t)
+                self.params[name] = nn.Parameter(t.to(dev))
         for k, m in enumerate(modules):
             self._bind(m, k)
 

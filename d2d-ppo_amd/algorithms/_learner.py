@@ -177,7 +177,7 @@ class BatchedLearnerBase(DataParallelMixin):
 
     def _policy_slot(self, obs_buf, t0, i, train, act_out, logp_out, val_out, tf, b):
         """Actions for slot i of every env (written to act_out [E][N]), log-probs [N][E], values [N][E]."""
-        forced = None if tf is None else tf["actions"][i]
+        forced = None if (tf is None or tf["actions"] is None) else tf["actions"][i]
         if self._fused_ok() and (self.kind == "comb") == bool(self.combinatorial):
             from d2dhip import _lib
             lib = _lib.require_gpu()
@@ -223,9 +223,10 @@ class BatchedLearnerBase(DataParallelMixin):
 
     # ------------------------------------------------------------ rollout
     def _collect(self, num_episodes, train=True, want_values=False, want_state=False, teacher=None):
-        """teacher (parity testing, n_envs == 1): recorded reference actions and env draws,
-        dict(actions [T][N][C|1], reset_arrivals [W][N], flips [T][..], arrivals [T][N]);
-        the policy still computes probs/log-probs/values, of the forced actions."""
+        """teacher (parity testing): a recorded reference rollout of E * waves episodes,
+        dict(actions [E*T][N][C|1] or None, reset_arrivals [E*W][N], flips [E*T][..], arrivals [E*T][N]);
+        the env replays the draws, the policy computes probs/log-probs/values of the forced actions
+        (or, with actions None, acts itself)."""
         b = self._bind_env()
         env = self.env
         E, L = b.E, env.episode_length
@@ -233,7 +234,7 @@ class BatchedLearnerBase(DataParallelMixin):
         if teacher is None and self._graph_ok(train, b, waves * L):
             return self._collect_graph(b, waves, want_values, want_state)
         bufs = self._rollout_buffers(b, waves, want_values, want_state)
-        tf = self._teacher_tensors(teacher, b, waves * L) if teacher is not None else None
+        tf = self._teacher_tensors(teacher, b, waves) if teacher is not None else None
         self._waves(bufs, b, waves, train, tf)
         return self._rollout_result(bufs, b, waves, train)
 
@@ -284,11 +285,14 @@ class BatchedLearnerBase(DataParallelMixin):
     def _rollout_result(self, bufs, b, waves, train):
         L = self.env.episode_length
         T = waves * L
-        recv, disc = bufs["recv"].cpu(), bufs["disc"].cpu()
-        scores = (1 - disc / recv).reshape(-1).tolist()
-        ep_rewards = bufs["eprew"].cpu().reshape(-1).tolist()
-        jains = bufs["jains"].cpu().reshape(-1).tolist() if not train else []
-        ch_errors = bufs["ch"].cpu().reshape(-1).tolist() if (not train and b.spec.kind == "single") else []
+        # per-episode statistics are [waves][E] on the device; episodes are listed env-major
+        # (env 0's waves, then env 1's, ...) like the samples (module docstring)
+        em = lambda t: t.t().reshape(-1)  # noqa: E731
+        recv, disc = em(bufs["recv"]).cpu(), em(bufs["disc"]).cpu()
+        scores = (1 - disc / recv).tolist()
+        ep_rewards = em(bufs["eprew"]).cpu().tolist()
+        jains = em(bufs["jains"]).cpu().tolist() if not train else []
+        ch_errors = em(bufs["ch"]).cpu().tolist() if (not train and b.spec.kind == "single") else []
         dones = torch.zeros(T, dtype=torch.uint8, device=self.device)
         dones[L - 1::L] = 1
         return Rollout(obs=bufs["obs"], actions=bufs["act"], logp=bufs["logp"], rewards=bufs["rew"].float(),
@@ -357,29 +361,42 @@ class BatchedLearnerBase(DataParallelMixin):
         env.timestep = L
         return self._rollout_result(G["bufs"], b, waves, True)
 
-    def _teacher_tensors(self, teacher, b, T):
+    def _teacher_tensors(self, teacher, b, waves):
+        """Per-slot device tensors of a recorded reference rollout of E * waves sequential episodes.
+        Reference episode q = e * waves + w is replayed by env e in wave w (the env-major sample order
+        of _collect), so slot i = w * L + t of env e takes reference step (e * waves + w) * L + t.
+        teacher["actions"] may be None (test(): the policy acts deterministically on its own)."""
         from d2dhip.envbatch import pack_masks
-        if b.E != 1:
-            raise ValueError("teacher forcing needs n_envs == 1")
-        s, dev = b.spec, b.device
-        acts = np.asarray(teacher["actions"], dtype=np.float64)[:T]
-        if self.combinatorial:
-            a = torch.from_numpy(acts.reshape(T, s.N, 1, -1).astype(np.float32)).to(dev)       # [T][N][1][C]
-        else:
-            a = torch.from_numpy(acts.reshape(T, s.N, 1).astype(np.int64)).to(dev)             # [T][N][1]
-        fl = np.asarray(teacher["flips"])[:T]
-        arr = np.asarray(teacher["arrivals"])[:T].astype(np.uint8)
+        s, dev, E, L = b.spec, b.device, b.E, self.env.episode_length
+        T = waves * L
+        need = E * T
+        fl_all = np.asarray(teacher["flips"])
+        if fl_all.shape[0] < need or len(teacher["reset_arrivals"]) < E * waves:
+            raise ValueError(f"teacher holds {fl_all.shape[0]} steps; {E} envs x {waves} waves need {need}")
+        # reference step index of (slot i, env e)
+        ref = (np.arange(E)[None, :] * waves + (np.arange(T) // L)[:, None]) * L + (np.arange(T) % L)[:, None]
+        a = None
+        if teacher.get("actions") is not None:
+            acts = np.asarray(teacher["actions"], dtype=np.float64)[ref]                   # [T][E][...]
+            if self.combinatorial:
+                a = torch.from_numpy(acts.reshape(T, E, s.N, -1).transpose(0, 2, 1, 3).astype(np.float32))
+            else:
+                a = torch.from_numpy(acts.reshape(T, E, s.N).transpose(0, 2, 1).astype(np.int64))
+            a = a.contiguous().to(dev)                                                      # [T][N][E](...)
+        fl = fl_all[ref]                                                                    # [T][E][...]
+        arr = np.asarray(teacher["arrivals"])[ref].astype(np.uint8)                         # [T][E][N]
         replay = []
         for i in range(T):
             if s.kind == "comb":
-                f = torch.from_numpy(np.ascontiguousarray(pack_masks(fl[i][None], s.C))).to(dev)
+                f = torch.from_numpy(np.ascontiguousarray(pack_masks(fl[i], s.C))).to(dev)
             elif s.kind == "single":
-                f = torch.from_numpy(np.ascontiguousarray(fl[i].reshape(1, s.N).astype(np.uint8))).to(dev)
+                f = torch.from_numpy(np.ascontiguousarray(fl[i].reshape(E, s.N).astype(np.uint8))).to(dev)
             else:
-                word = int((fl[i].astype(np.int64) << np.arange(fl[i].shape[-1])).sum())
-                f = torch.tensor([word], dtype=torch.int32, device=dev)
-            replay.append((f, torch.from_numpy(arr[i][None].copy()).to(dev)))
-        ra = [torch.from_numpy(np.asarray(r, dtype=np.uint8)[None].copy()).to(dev) for r in teacher["reset_arrivals"]]
+                words = (fl[i].astype(np.int64) << np.arange(fl[i].shape[-1])).sum(-1)
+                f = torch.from_numpy(words.astype(np.int32)).to(dev)
+            replay.append((f, torch.from_numpy(np.ascontiguousarray(arr[i])).to(dev)))
+        ra_all = np.asarray(teacher["reset_arrivals"], dtype=np.uint8)
+        ra = [torch.from_numpy(np.ascontiguousarray(ra_all[np.arange(E) * waves + w])).to(dev) for w in range(waves)]
         return {"actions": a, "replay": replay, "reset_arrivals": ra}
 
     @staticmethod
@@ -421,7 +438,14 @@ class BatchedLearnerBase(DataParallelMixin):
 
     # ------------------------------------------------------------- test
     def test(self, num_episodes):
-        ro = self._collect(num_episodes, train=False)
+        """Deterministic evaluation (ippo.py:345-388, d2d_ppo.py:341-383): argmax / p > 0.5 actions,
+        returns (mean URLLC score, mean Jain's index, summed channel errors, mean episode reward)."""
+        return self._test(num_episodes)
+
+    def _test(self, num_episodes, teacher=None):
+        """test() body; `teacher` (parity tests) replays recorded env draws, actions stay the policy's."""
+        ro = self._collect(num_episodes, train=False, teacher=teacher)
+        self._last_test_rollout = ro if teacher is not None else None
         n = num_episodes
         sc = np.array(ro.scores[:n], dtype=np.float64)
         ja = np.array(ro.jains[:n], dtype=np.float64)
@@ -448,7 +472,6 @@ class BatchedLearnerBase(DataParallelMixin):
         for i, agent in enumerate(self.agents):
             sd = torch.load(f"{checkpoint_path}/agent_{i}.pth", map_location=self.device, weights_only=True)
             agent.policy_network.load_state_dict(sd)
-        self._policy_version = getattr(self, "_policy_version", 0) + 1  # rollouts before this are stale
         print("Models loaded!")
 
     def preprocess_input_for_rnn(self, obs_agent):
@@ -462,3 +485,12 @@ class BatchedLearnerBase(DataParallelMixin):
                            last_shard=self._last_shard(), n_envs_total=self._n_envs_total())
 
     process_group = None  # set by DataParallelMixin._setup_data_parallel when world_size > 1
+
+    # ------------------------------------------------------------ phase marks
+    phase_timer = None  # bench.py installs one to split an iteration into phases (stream events)
+
+    def _phase(self, name):
+        """Attribute the GPU time since the previous mark to `name` (no-op unless timed)."""
+        t = self.phase_timer
+        if t is not None:
+            t.mark(name)

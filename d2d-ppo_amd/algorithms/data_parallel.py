@@ -61,22 +61,6 @@ def allreduce_mean_scalar(x, device, group=None):
     return float(t.item()) / dist.get_world_size(group)
 
 
-def combine_column_stats(local_sum, local_m2_fn, n_local, ddof, group=None):
-    """Reference implementation of the two-pass global statistics used by
-    d2dhip.gae.normalize_columns_: returns (mean, std) over all ranks' rows.
-    local_m2_fn(mean) -> local centred sum of squares."""
-    s = local_sum.clone()
-    n = torch.tensor([float(n_local)], dtype=torch.float64, device=s.device)
-    if group is not None or (dist.is_available() and dist.is_initialized()):
-        dist.all_reduce(s, group=group)
-        dist.all_reduce(n, group=group)
-    mean = s / n
-    m2 = local_m2_fn(mean).clone()
-    if group is not None or (dist.is_available() and dist.is_initialized()):
-        dist.all_reduce(m2, group=group)
-    return mean, torch.sqrt(m2 / (n - ddof))
-
-
 class DataParallelMixin:
     """Hooks used by BatchedLearnerBase when torch.distributed is initialised."""
 
@@ -86,8 +70,27 @@ class DataParallelMixin:
             return
         self.process_group = dist.group.WORLD
         env = self.env
-        if getattr(env, "_batch", None) is None and getattr(env, "env_base", 0) == 0:
-            env.shard(self.rank, self.world_size)
+        want = self.rank * env.n_envs
+        err = None
+        if getattr(env, "_batch", None) is None:
+            if getattr(env, "env_base", 0) not in (0, want):
+                err = f"env was sharded with env_base {env.env_base}, expected {want} (= rank * n_envs)"
+            else:
+                env.shard(self.rank, self.world_size)
+        elif env._batch.desc.env_base != want:
+            # an env batch built before the learner (e.g. by env.reset()) draws the Philox streams of
+            # envs [env_base, env_base + n_envs): unsharded, every rank would roll out identical
+            # episodes and the all-reduced gradient would be one rank's gradient
+            err = (f"the env batch already exists with env_base {env._batch.desc.env_base}; call "
+                   f"env.shard({self.rank}, {self.world_size}) before the first reset, or build the "
+                   f"learner before using the env")
+        # every rank learns whether any rank is misconfigured, so all of them raise (no rank is left
+        # waiting in the weight broadcast below)
+        bad = torch.tensor([0 if err is None else 1], dtype=torch.int64,
+                           device=self.device if dist.get_backend(self.process_group) == "nccl" else "cpu")
+        dist.all_reduce(bad, group=self.process_group)
+        if int(bad.item()):
+            raise RuntimeError(f"rank {self.rank}: " + (err or "another rank's env is not sharded for it"))
         broadcast_params_(params, 0, self.process_group)
 
     def _reduce_grads(self, params):

@@ -166,8 +166,10 @@ class iPPO(BatchedLearnerBase):
     # ------------------------------------------------------------ rollouts
     def _rollout(self, num_episodes, teacher=None):
         ro = self._collect(num_episodes, train=True, want_values=True, teacher=teacher)
+        self._phase("rollout")
         # values [T][N][E] as the policy kernel wrote them; adv / ret in the same layout (ippo.py:337-338)
         ro.adv_tne, ro.ret_tne = self._gae(ro.rewards, ro.values, ro.dones, layout="tce")
+        self._phase("gae")
         return ro
 
     def create_rollouts(self, num_episodes=4):
@@ -222,12 +224,18 @@ class iPPO(BatchedLearnerBase):
         _, sa = actor_grads({k: v.data for k, v in pp.items()}, ro.obs, ro.actions, ro.logp.permute(0, 2, 1),
                             ro.adv_tne.permute(0, 2, 1), kind, clip=cliprange, beta=beta,
                             grads=self._grad_buffers(pp))
+        self._phase("actor_grad")
         self._reduce_grads(self.policy.parameters())
+        self._phase("allreduce")
         self.policy_optimizer.step()
+        self._phase("adam")
         _, sv = critic_grads({k: v.data for k, v in vp.items()}, ro.obs, ro.ret_tne.permute(0, 2, 1),
                              grads=self._grad_buffers(vp))
+        self._phase("critic_grad")
         self._reduce_grads(self.value.parameters())
+        self._phase("allreduce")
         self.value_optimizer.step()
+        self._phase("adam")
         return -(sa[:, 0] + beta * sa[:, 1]) / B, sv[:, 0] / B
 
     def _update_epoch(self, ro, upd):
@@ -237,6 +245,8 @@ class iPPO(BatchedLearnerBase):
         return self._epoch(x, acts, logp_old, ro.adv, ro.ret)
 
     def train(self, num_iter, n_epoch=4, num_episodes=4, test_freq=100):
+        from d2dhip import _lib
+        _lib.refuse_ablation("iPPO.train()")
         scores_episode = []
         score_test_list = []
         policy_loss_list = []

@@ -50,8 +50,6 @@ __device__ __forceinline__ uint32_t partner32(uint32_t v, int g) {
   return (g & 2) ? p[0] : p[1];
 }
 
-// relu as one v_max_i32 on the bit pattern (negative floats are negative ints, -0 -> +0);
-// fmaxf(x, 0) costs a NaN-quieting canonicalize plus the max under the IEEE mode
 // XCD-aware block mapping.  MI355X dispatches workgroups round-robin over its 8 XCDs, each with
 // its own L2, so in an agent-fast grid (x = agent) the agents of one env chunk -- whose obs rows
 // ([env][agent][F] floats) share cache lines -- land on eight different L2s and every line is
@@ -66,6 +64,8 @@ __device__ __forceinline__ void xcd_block(int& bx, int& by) {
   by = (int)(b / nx);
 }
 
+// relu as one v_max_i32 on the bit pattern (negative floats are negative ints, -0 -> +0);
+// fmaxf(x, 0) costs a NaN-quieting canonicalize plus the max under the IEEE mode
 __device__ __forceinline__ float relu(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
 
 // channel masks of 1 / 2 / 4 bytes (d2d_mask_bytes): one typed access, no byte loop

@@ -8,14 +8,29 @@ every entry point raises if the library cannot be loaded or no GPU is present.
 """
 import ctypes
 import os
+import sys
 
 import torch  # noqa: F401  (must be imported before the HIP library is loaded)
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libd2dhip.so")
-# A/B timing builds only (tools/gpu/ablate_update.py): another in-tree build of the same library
-if os.environ.get("D2D_LIB_VARIANT"):
-    LIB_PATH = os.path.join(PKG_DIR, "lib", f"libd2dhip_{os.environ['D2D_LIB_VARIANT']}.so")
+# A/B timing builds only (tools/gpu/ablate_update.py): another in-tree build of the same library.
+# Those builds drop parts of the update on purpose (wrong gradients), so the variable is honoured
+# only together with an explicit D2D_ALLOW_ABLATION=1, loudly, and the learners refuse to train on it.
+VARIANT = os.environ.get("D2D_LIB_VARIANT") or None
+if VARIANT:
+    if os.environ.get("D2D_ALLOW_ABLATION") != "1":
+        raise RuntimeError(f"D2D_LIB_VARIANT={VARIANT} selects an ablation build of libd2dhip (wrong results "
+                           f"by design); set D2D_ALLOW_ABLATION=1 as well to load it, or unset it")
+    LIB_PATH = os.path.join(PKG_DIR, "lib", f"libd2dhip_{VARIANT}.so")
+    print(f"[d2dhip] WARNING: loading ablation build {LIB_PATH} (results are NOT correct)", file=sys.stderr,
+          flush=True)
+
+
+def refuse_ablation(what):
+    """Product entry points (training, smoke) must not run on an ablation build."""
+    if VARIANT:
+        raise RuntimeError(f"{what} refuses the ablation build libd2dhip_{VARIANT}.so (D2D_LIB_VARIANT)")
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2

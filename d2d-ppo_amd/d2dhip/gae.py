@@ -18,6 +18,22 @@ def _all_reduce(t, group):
     return t
 
 
+def two_pass_column_stats(colsum, finalize, group=None):
+    """The cross-rank protocol behind normalize_columns_ (data-parallel shards of envs normalise with
+    the GLOBAL column mean / std):
+        s1 = Σ x per column (local)            -> all-reduce -> mean = finalize(s1, None)
+        m2 = Σ (x - mean)^2 per column (local) -> all-reduce -> (mean, scale, gate) = finalize(s1, m2)
+    colsum(center) returns a fresh float64 [cols] tensor of local sums (center None: plain sums);
+    finalize(s1, m2) returns (mean, scale, gate).  Two deterministic passes instead of a one-pass
+    Σx / Σx² keep the variance of large-mean columns exact to float64."""
+    s1 = colsum(None)
+    _all_reduce(s1, group)
+    mean = finalize(s1, None)[0]
+    m2 = colsum(mean)
+    _all_reduce(m2, group)
+    return finalize(s1, m2)
+
+
 def normalize_columns_(x2d, ddof, group=None, n_total=None, tce=None):
     """In place: x = (x - mean) / std per column iff every column's std > 0.
     x2d: contiguous float32 [rows][cols] on the GPU, or (tce = (T, cols, E)) a contiguous
@@ -31,29 +47,29 @@ def normalize_columns_(x2d, ddof, group=None, n_total=None, tce=None):
     dev = x2d.device
     st = _lib.stream_ptr()
     ws = torch.empty(int(lib.d2d_colstats_workspace(rows, cols)), dtype=torch.float64, device=dev)
-    s1 = torch.empty(cols, dtype=torch.float64, device=dev)
-    m2 = torch.empty(cols, dtype=torch.float64, device=dev)
     mean = torch.empty(cols, dtype=torch.float64, device=dev)
     scale = torch.empty(cols, dtype=torch.float64, device=dev)
     gate = torch.zeros(1, dtype=torch.int32, device=dev)
     n = float(rows if n_total is None else n_total)
 
-    def colstats(center, out):
+    def colsum(center):
+        out = torch.empty(cols, dtype=torch.float64, device=dev)
+        c = None if center is None else center.data_ptr()
         if tce is None:
-            _lib.check(lib.d2d_colstats(rows, cols, x2d.data_ptr(), center, ws.data_ptr(), out.data_ptr(), st),
+            _lib.check(lib.d2d_colstats(rows, cols, x2d.data_ptr(), c, ws.data_ptr(), out.data_ptr(), st),
                        "d2d_colstats")
         else:
-            _lib.check(lib.d2d_colstats_tce(T, cols, E, x2d.data_ptr(), center, ws.data_ptr(), out.data_ptr(), st),
+            _lib.check(lib.d2d_colstats_tce(T, cols, E, x2d.data_ptr(), c, ws.data_ptr(), out.data_ptr(), st),
                        "d2d_colstats_tce")
+        return out
 
-    colstats(None, s1)
-    _all_reduce(s1, group)
-    _lib.check(lib.d2d_colstats_finalize(cols, s1.data_ptr(), None, n, ddof, mean.data_ptr(), None, None, st),
-               "d2d_colstats_finalize")
-    colstats(mean.data_ptr(), m2)
-    _all_reduce(m2, group)
-    _lib.check(lib.d2d_colstats_finalize(cols, s1.data_ptr(), m2.data_ptr(), n, ddof, mean.data_ptr(),
-                                         scale.data_ptr(), gate.data_ptr(), st), "d2d_colstats_finalize")
+    def finalize(s1, m2):
+        _lib.check(lib.d2d_colstats_finalize(cols, s1.data_ptr(), None if m2 is None else m2.data_ptr(), n, ddof,
+                                             mean.data_ptr(), None if m2 is None else scale.data_ptr(),
+                                             None if m2 is None else gate.data_ptr(), st), "d2d_colstats_finalize")
+        return mean, scale, gate
+
+    two_pass_column_stats(colsum, finalize, group)
     if tce is None:
         _lib.check(lib.d2d_normalize_columns(rows, cols, x2d.data_ptr(), mean.data_ptr(), scale.data_ptr(),
                                              gate.data_ptr(), st), "d2d_normalize_columns")

@@ -60,3 +60,16 @@ def gae_returns_batched(rewards, values, dones, gamma, lbda):
     ret = discount_rewards_seq(seq(r), gamma, d, True, exact_stats=True)
     back = lambda x: np.transpose(x.reshape(E, T, cols), (1, 0, 2))  # noqa: E731
     return back(adv), back(ret)
+
+
+def colstats_finalize(s1, m2, n, ddof):
+    """Restatement of d2d_colstats_finalize (csrc/gae_kernels.hip): mean = Σx / n; with the centred
+    sums m2: scale = 1 / std (std with ddof, as np.std / torch.std in ippo.py:100, 114), gate = every
+    column's std > 0 (the reference normalises only then, quirk Q2).  torch float64 in and out."""
+    import torch
+    mean = s1 / n
+    if m2 is None:
+        return mean, None, None
+    sd = torch.sqrt(m2 / (n - ddof))
+    gate = torch.tensor([int(bool((sd > 0).all()))], dtype=torch.int32)
+    return mean, 1.0 / sd, gate

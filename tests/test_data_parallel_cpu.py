@@ -80,12 +80,19 @@ def _worker(rank, ws, port, outdir):
             _d2d_epoch(st, opt, x[:, sl], acts[:, sl], adv[sl], logp_old[:, sl], perm, dp.allreduce_grads_)
         torch.save({k: v.detach().clone() for k, v in st.params.items()}, os.path.join(outdir, f"w{rank}.pt"))
         np.save(os.path.join(outdir, f"perm{rank}.npy"), perm)
-        # global column statistics from shard-local sums
+        # global column statistics: the product's cross-rank protocol (d2dhip.gae.two_pass_column_stats,
+        # the one normalize_columns_ runs between its HIP kernels) driven with the oracle's arithmetic
+        from d2dhip.gae import two_pass_column_stats
+        from oracle.gae_oracle import colstats_finalize
         rng = np.random.default_rng(7)
         full = torch.from_numpy(rng.normal(size=(1000, 4)) * [1, 2, 3, 4] + [0, 1, 2, 3])
         loc = full[rank * 500:(rank + 1) * 500]
-        mean, std = dp.combine_column_stats(loc.sum(0), lambda m: ((loc - m) ** 2).sum(0), 500, 1)
-        np.save(os.path.join(outdir, f"stats{rank}.npy"), torch.stack([mean, std]).numpy())
+        for ddof in (0, 1):
+            mean, scale, gate = two_pass_column_stats(
+                lambda c: (loc.sum(0) if c is None else ((loc - c) ** 2).sum(0)).clone(),
+                lambda s1, m2: colstats_finalize(s1, m2, 1000.0, ddof), dp.dist.group.WORLD)
+            np.save(os.path.join(outdir, f"stats{rank}_{ddof}.npy"),
+                    torch.stack([mean, 1.0 / scale, gate.double().expand(4)]).numpy())
     finally:
         dist.destroy_process_group()
 
@@ -105,12 +112,14 @@ def test_two_rank_update_equals_full_batch(tmp_path):
     for k, v in st.params.items():
         torch.testing.assert_close(w0[k], w1[k], rtol=0, atol=0)
         torch.testing.assert_close(w0[k], v.detach(), rtol=0, atol=1e-6)
-    s0, s1 = np.load(tmp_path / "stats0.npy"), np.load(tmp_path / "stats1.npy")
     rng = np.random.default_rng(7)
     full = rng.normal(size=(1000, 4)) * [1, 2, 3, 4] + [0, 1, 2, 3]
-    np.testing.assert_allclose(s0, s1, rtol=0, atol=0)
-    np.testing.assert_allclose(s0[0], full.mean(0), rtol=0, atol=1e-12)
-    np.testing.assert_allclose(s0[1], full.std(0, ddof=1), rtol=0, atol=1e-12)
+    for ddof in (0, 1):
+        s0, s1 = np.load(tmp_path / f"stats0_{ddof}.npy"), np.load(tmp_path / f"stats1_{ddof}.npy")
+        np.testing.assert_allclose(s0, s1, rtol=0, atol=0)
+        np.testing.assert_allclose(s0[0], full.mean(0), rtol=0, atol=1e-12)
+        np.testing.assert_allclose(s0[1], full.std(0, ddof=ddof), rtol=0, atol=1e-12)
+        assert np.all(s0[2] == 1)
 
 
 def test_single_process_hooks_are_identity():
@@ -123,3 +132,53 @@ def test_single_process_hooks_are_identity():
     lr = L()
     assert lr._last_shard() and lr._n_envs_total() is None
     assert list(lr._sync_perm(np.array([2, 0, 1]))) == [2, 0, 1]
+
+
+class _StubEnv:  # noqa: E302
+    """Just the env attributes DataParallelMixin._setup_data_parallel reads (no GPU needed)."""
+
+    def __init__(self, n_envs, batch_env_base=None):
+        from types import SimpleNamespace
+        self.n_envs = n_envs
+        self.env_base = 0
+        self._batch = None if batch_env_base is None else SimpleNamespace(desc=SimpleNamespace(env_base=batch_env_base))
+
+    def shard(self, rank, world_size):
+        self.env_base = rank * self.n_envs
+        return self
+
+
+def _shard_worker(rank, ws, port, outdir):
+    from algorithms.data_parallel import DataParallelMixin
+
+    class L(DataParallelMixin):
+        pass
+
+    _init(rank, ws, port)
+    try:
+        res = []
+        # (a) env batch not built yet: the learner shards it
+        lr = L()
+        lr.env = _StubEnv(8)
+        lr._setup_data_parallel([torch.zeros(3)])
+        res.append(lr.env.env_base)
+        # (b) env batch built before the learner with the default env_base 0: rank 0 is fine,
+        # every other rank must refuse (identical Philox streams on all ranks otherwise)
+        lr = L()
+        lr.env = _StubEnv(8, batch_env_base=0)
+        try:
+            lr._setup_data_parallel([torch.zeros(3)])
+            res.append("ok")
+        except RuntimeError:
+            res.append("refused")
+        np.save(os.path.join(outdir, f"shard{rank}.npy"), np.array([str(r) for r in res]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_refuses_unsharded_env(tmp_path):
+    port = _free_port()
+    mp.spawn(_shard_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    # rank 1's batch draws rank 0's streams; both ranks refuse (collectively, nobody hangs)
+    assert list(np.load(tmp_path / "shard0.npy")) == ["0", "refused"]
+    assert list(np.load(tmp_path / "shard1.npy")) == ["8", "refused"]

@@ -34,6 +34,17 @@ def names():
     return sorted(os.path.basename(p)[8:-4] for p in glob.glob(os.path.join(GOLDEN, "learner_*.npz")))
 
 
+def cases():
+    """(fixture, n_envs): every trace of W sequential reference episodes is replayed on 1 env (W waves)
+    and on E > 1 envs (reference episode e * waves + w -> env e, wave w: the production multi-env path)."""
+    out = []
+    for n in names():
+        ep = 4 if n.endswith("_ep4") else 2
+        for E in ((1, 2, 4) if ep == 4 else (1, 2)):
+            out.append((n, E))
+    return out
+
+
 def _params(z):
     raw = json.loads(str(z["params_json"]))
     return {k: (np.array(v["__nd__"], dtype=v["dtype"]) if isinstance(v, dict) else v) for k, v in raw.items()}
@@ -47,7 +58,7 @@ def _sd(z, prefix):
     return out
 
 
-def build(z):
+def build(z, n_envs=1):
     from algorithms.d2d_ppo import D2DPPO
     from algorithms.ippo import iPPO
     from envs.channel_selection_env import ChannelSelectionEnv
@@ -56,20 +67,21 @@ def build(z):
     params = _params(z)
     from envs.env import D2DEnv
     cls = {"comb": CombinatorialEnv, "chsel": ChannelSelectionEnv, "single": D2DEnv}[kind]
-    env = cls(**params, n_envs=1, device="cuda", seed=0)
+    env = cls(**params, n_envs=n_envs, device="cuda", seed=0)
     common = dict(hidden_size=int(z["hidden"]), gamma=float(z["gamma"]), policy_lr=3e-3, value_lr=1e-2,
                   device="cuda", useRNN=bool(z["useRNN"]), combinatorial=bool(z["combinatorial"]),
                   history_len=int(z["history_len"]), early_stopping=False)
     return env, kind, common, iPPO, D2DPPO
 
 
-@pytest.mark.parametrize("name", names())
-def test_learner_matches_reference(name):
+@pytest.mark.parametrize("name,E", cases())
+def test_learner_matches_reference(name, E):
     if not torch.cuda.is_available():
         pytest.fail("GPU tests need a ROCm GPU")
     z = np.load(os.path.join(GOLDEN, f"learner_{name}.npz"))
     algo = name.split("_")[0]
-    env, kind, common, iPPO, D2DPPO = build(z)
+    n_ep = int(z["episodes"]) if "episodes" in z.files else 2
+    env, kind, common, iPPO, D2DPPO = build(z, n_envs=E)
     lr = iPPO(env, **common) if algo == "ippo" else D2DPPO(env, beta_entropy=0.02, **common)
     N = env.n_agents
     for i, ag in enumerate(lr.agents):
@@ -80,10 +92,10 @@ def test_learner_matches_reference(name):
         lr.value_network.load_state_dict(_sd(z, "init/critic"))
     teacher = dict(actions=z["ro/actions"], reset_arrivals=z["draws/reset_arrivals"], flips=z["draws/flips"],
                    arrivals=z["draws/arrivals"])
-    ro = lr._rollout(2, teacher=teacher)
+    ro = lr._rollout(n_ep, teacher=teacher)
+    assert ro.E == E and ro.waves * E == n_ep
     s = env.spec
-    T = ro.T
-    obs = ro.obs[:, 0].cpu().numpy()                                            # [T][N][F]
+    obs = ro.obs.permute(1, 0, 2, 3).reshape(E * ro.T, N, -1).cpu().numpy()      # env-major = reference order
     for k in range(N):
         assert np.array_equal(obs[:, k, : s.obs_len[k]], z[f"ro/obs{k}"]), k
     logp = lr._seq(ro.logp).t().cpu().numpy()
@@ -93,9 +105,12 @@ def test_learner_matches_reference(name):
         np.testing.assert_allclose(lr._seq(ro.values).t().cpu().numpy(), z["ro/values"], rtol=0, atol=1e-5)
         np.testing.assert_allclose(ro.adv.t().cpu().numpy(), z["ro/advantages"], rtol=0, atol=1e-5)
         np.testing.assert_allclose(ro.ret.t().cpu().numpy(), z["ro/returns"], rtol=0, atol=1e-5)
+        # the reference-structured view of the same rollout (ippo.py:343)
+        view = lr._reference_view(ro)
+        assert np.array_equal(view[1].reshape(z["ro/actions"].shape), z["ro/actions"])
     else:
         assert np.array_equal(ro.state_seq.cpu().numpy(), z["ro/states"])
-        assert np.array_equal(ro.rewards[:, 0].double().cpu().numpy(), z["ro/rewards_mean"])
+        assert np.array_equal(ro.rewards.t().reshape(-1).double().cpu().numpy(), z["ro/rewards_mean"])
         np.testing.assert_allclose(ro.ret_mean.cpu().numpy(), z["ro/returns"], rtol=0, atol=1e-5)
     if bool(z["useRNN"]):
         win = lr.preprocess_input_for_rnn(torch.from_numpy(z["ro/obs0"]).cuda()).cpu().numpy()
@@ -106,11 +121,11 @@ def test_learner_matches_reference(name):
     lr.test = lambda num_episodes: (0.5, 1.0, 0, 0.0)
     np.random.seed(21)
     if algo == "ippo":
-        res = lr.train(1, n_epoch=2, num_episodes=2, test_freq=10 ** 9)
+        res = lr.train(1, n_epoch=2, num_episodes=n_ep, test_freq=10 ** 9)
         np.testing.assert_allclose(res[2], z["train/policy_loss"], rtol=0, atol=1e-5)
         np.testing.assert_allclose(res[3], z["train/value_loss"], rtol=0, atol=1e-5)
     else:
-        res = lr.train(1, num_episodes=2, n_epoch=2, test_freq=10 ** 9)
+        res = lr.train(1, num_episodes=n_ep, n_epoch=2, test_freq=10 ** 9)
         np.testing.assert_allclose(np.array(res[2]), z["train/policy_loss"], rtol=0, atol=1e-5)
         np.testing.assert_allclose([float(v) for v in res[3]], z["train/value_loss"], rtol=0, atol=1e-5)
     for i, ag in enumerate(lr.agents):
@@ -124,6 +139,39 @@ def test_learner_matches_reference(name):
     if algo == "d2d":
         for k, v in lr.value_network.state_dict().items():
             np.testing.assert_allclose(v.cpu().numpy(), z[f"final/critic/{k}"], rtol=0, atol=1e-4, err_msg=k)
+
+
+def evaltest_names():
+    return sorted(os.path.basename(p)[9:-4] for p in glob.glob(os.path.join(GOLDEN, "evaltest_*.npz")))
+
+
+@pytest.mark.parametrize("name,E", [(n, E) for n in evaltest_names() for E in (1, 2, 4)])
+def test_evaluation_matches_reference(name, E):
+    """test(4) of the reference (ippo.py:345-388, d2d_ppo.py:341-383) replayed with its recorded env draws:
+    the deterministic actions (argmax / p > 0.5) must be the reference's bit for bit, and the returned
+    (URLLC score, Jain's index, channel errors, mean episode reward) equal to 1e-12."""
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm GPU")
+    z = np.load(os.path.join(GOLDEN, f"evaltest_{name}.npz"))
+    algo = name.split("_")[0]
+    n_ep = int(z["episodes"])
+    env, kind, common, iPPO, D2DPPO = build(z, n_envs=E)
+    lr = iPPO(env, **common) if algo == "ippo" else D2DPPO(env, **common)
+    for i, ag in enumerate(lr.agents):
+        ag.policy_network.load_state_dict(_sd(z, f"weights/agent{i}/policy"))
+    teacher = dict(actions=None, reset_arrivals=z["draws/reset_arrivals"], flips=z["draws/flips"],
+                   arrivals=z["draws/arrivals"])
+    res = lr._test(n_ep, teacher=teacher)
+    ro = lr._last_test_rollout
+    # the actions the policy chose, in the reference's (episode-major) order
+    acts = ro.actions.permute(1, 0, 2).reshape(E * ro.T, env.n_agents)
+    if kind == "comb":
+        from algorithms._core import unpack_actions
+        acts = unpack_actions(acts, env.n_channels)
+    ref_acts = z["draws/actions"].reshape(acts.shape)
+    mism = np.argwhere(acts.cpu().numpy() != ref_acts)
+    assert mism.size == 0, f"{len(mism)} action mismatches, first at {mism[:3].tolist()}"
+    np.testing.assert_allclose(np.array(res, dtype=np.float64), z["result"], rtol=0, atol=1e-12)
 
 
 def test_save_load_roundtrip(tmp_path):
@@ -211,15 +259,20 @@ def test_graph_rollout_equals_eager(algo, kind):
     assert not torch.equal(outs[1][1][1], outs[1][2][1])
 
 
-def test_d2d_central_critic_split_gemm_matches_fp32():
+@pytest.mark.parametrize("N", [12, 256])
+def test_d2d_central_critic_split_gemm_matches_fp32(N):
     """The central critic on bf16 split GEMMs (exact bf16 states x three-way split W1; dPre two-way
     split) == torch fp32 autograd of mse(Value(state), returns): values to 1e-5 relative,
-    gradients to 2e-5 of their largest entry."""
+    gradients to 2e-5 of their largest entry.  N = 256: the configs[4] sweep's widest state
+    (S = 15 N + 8 = 3,848 with deadlines 7)."""
     from algorithms.d2d_ppo import D2DPPO
     from envs.combinatorial_env import CombinatorialEnv
-    N, C = 12, 8
-    env = CombinatorialEnv(N, C, np.array([7, 14] * 6), np.full(N, 0.4), episode_length=20,
+    C = 8
+    dl = np.array([7, 14] * (N // 2)) if N == 12 else np.full(N, 7)
+    env = CombinatorialEnv(N, C, dl, np.full(N, 0.4), episode_length=20,
                            channel_switch=np.full((N, C), 0.3), n_envs=64, device="cuda", seed=4)
+    if N == 256:
+        assert env.state_space.shape[0] == 15 * N + 8
     torch.manual_seed(2)
     lr = D2DPPO(env, hidden_size=64, gamma=0.5, device="cuda", combinatorial=True, early_stopping=False)
     lr.CRITIC_SPLIT_MIN_DIM = 0

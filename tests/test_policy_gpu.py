@@ -94,6 +94,29 @@ def test_forced_and_deterministic_match_torch(kind, F, H, A, in_dims, frac):
     assert torch.equal(acts_d, want)
 
 
+@pytest.mark.parametrize("N", [128, 256])
+def test_c5_agent_counts_match_torch(N):
+    """configs[4] shapes (xp_n_agents sweep at 128 / 256 agents, C = 8, D = 7 -> F = 23, H = 64):
+    forced log-probs 1e-5 where well conditioned, deterministic actions exact."""
+    from d2dhip.envbatch import pack_masks_torch
+    from d2dhip.policy import policy_mlp_step
+    from torch.distributions import Bernoulli
+    E, F, H, A = 520, 23, 64, 8
+    actor, _, obs = make("comb", N, E, F, H, A, seed=N, critic=False)
+    probs, _ = torch_ref(actor, None, obs)
+    g = torch.Generator(device="cuda").manual_seed(N)
+    bits = (torch.rand((N, E, A), device="cuda", generator=g) < 0.3).float()
+    forced = pack_masks_torch(bits.transpose(0, 1))
+    ref_lp = Bernoulli(probs=probs, validate_args=False).log_prob(bits).mean(-1)
+    acts, lp, _ = policy_mlp_step(actor, obs, "comb", None, forced=forced)
+    assert torch.equal(acts, forced)
+    well = ((probs > 1e-3) & (probs < 1 - 1e-3)).all(-1)
+    assert well.float().mean() > 0.5
+    torch.testing.assert_close(lp[well], ref_lp[well], rtol=0, atol=1e-5)
+    acts_d, _, _ = policy_mlp_step(actor, obs, "comb", None, deterministic=True)
+    assert torch.equal(acts_d, pack_masks_torch((probs > 0.5).transpose(0, 1)))
+
+
 @pytest.mark.parametrize("kind,F,H,A,in_dims", CASES[:1] + CASES[4:5])
 def test_sampling_uses_philox_stream3(kind, F, H, A, in_dims):
     import sys, os

@@ -121,6 +121,9 @@ CASES = [
     ("chsel", 3, 3, 70, 12, 64, 5, None, True),
     ("chsel", 5, 2, 96, 24, 64, 16, [24, 20, 24, 21, 24], False),
     ("chsel", 2, 1, 17, 40, 48, 9, None, True),
+    # configs[4] (xp_n_agents sweep) shapes bench.py times: 128 / 256 agents, C = 8, D = 7 -> F = 23
+    ("comb", 128, 2, 72, 23, 64, 8, None, False),
+    ("comb", 256, 2, 40, 23, 64, 8, None, False),
 ]
 
 
@@ -237,16 +240,20 @@ def test_update_rejects_bad_shapes():
         actor_grads(net, obs, acts, lo, lo, "comb")
 
 
-def _learner_pair(cls, kind, seed=0, E=96):
-    """Two identical learners (same init, same rollout) on a small batched env."""
+def _learner_pair(cls, kind, seed=0, E=96, N=6):
+    """Two identical learners (same init, same rollout) on a small batched env.  kind "c5": the
+    xp_n_agents sweep env of configs[4] (N agents, 8 channels, deadlines 7, lambda 1/14, switch 0.8)."""
     import copy
     import json
     import os
     from envs.combinatorial_env import CombinatorialEnv
     from envs.channel_selection_env import ChannelSelectionEnv
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    N = 6
-    if kind == "comb":
+    if kind == "c5":
+        params = dict(n_agents=N, n_channels=8, deadlines=np.array([7] * N), lbdas=np.full(N, 1 / 14),
+                      episode_length=20, traffic_model="aperiodic", channel_switch=np.full((N, 8), 0.8))
+        make_env = lambda: CombinatorialEnv(**params, n_envs=E, device="cuda", seed=seed)  # noqa: E731
+    elif kind == "comb":
         cs8 = np.array(json.load(open(os.path.join(root, "d2d-ppo_amd", "combinatorial_load",
                                                    "channel_switch_8.json")))["__nd__"])
         params = dict(n_agents=N, n_channels=8, deadlines=np.array([7, 14] * 3), lbdas=np.full(N, 0.5),
@@ -265,7 +272,7 @@ def _learner_pair(cls, kind, seed=0, E=96):
         torch.manual_seed(seed)
         env = make_env()
         kw = dict(hidden_size=64, gamma=0.6, policy_lr=3e-3, value_lr=1e-3, device="cuda", useRNN=False,
-                  combinatorial=kind == "comb")
+                  combinatorial=kind in ("comb", "c5"))
         lr = cls(env, beta_entropy=0.05, **kw) if cls.__name__ == "D2DPPO" else cls(env, **kw)
         out.append(lr)
     torch.manual_seed(seed + 1)
@@ -273,9 +280,9 @@ def _learner_pair(cls, kind, seed=0, E=96):
     return out, ro, copy
 
 
-@pytest.mark.parametrize("kind", ["comb", "chsel"])
-@pytest.mark.parametrize("algo", ["ippo", "d2d"])
-def test_fused_epoch_matches_torch_epoch(kind, algo):
+@pytest.mark.parametrize("kind,algo,N", [("comb", "ippo", 6), ("chsel", "ippo", 6), ("comb", "d2d", 6),
+                                         ("chsel", "d2d", 6), ("c5", "d2d", 128), ("c5", "d2d", 256)])
+def test_fused_epoch_matches_torch_epoch(kind, algo, N):
     """One learner epoch on the fused kernels == the torch agent-stacked epoch (same rollout, same
     permutation): losses 1e-5; post-Adam weights within 2% of the learning rate.  Adam's first
     steps are lr * g / (|g| + 1e-8): sign-like, so elements whose gradient is ~1e-8 move by a
@@ -283,8 +290,10 @@ def test_fused_epoch_matches_torch_epoch(kind, algo):
     from algorithms.d2d_ppo import D2DPPO
     from algorithms.ippo import iPPO
     cls = iPPO if algo == "ippo" else D2DPPO
-    (fused, ref), ro, _ = _learner_pair(cls, kind)
+    (fused, ref), ro, copy = _learner_pair(cls, kind, E=96 if N <= 64 else 32, N=N)
     assert fused._fused_update_ok()
+    if N > 64:  # the central critic's bf16-split GEMM path (S = 15 N + 8) is the one bench.py times
+        assert ro.state_seq.shape[1] == 15 * N + 8 and fused._critic_split_forward(ro) is not None
     upd = ref._update_inputs(ro)
     for ep in range(2):
         np.random.seed(100 + ep)
@@ -295,15 +304,42 @@ def test_fused_epoch_matches_torch_epoch(kind, algo):
             assert torch.allclose(a[0], b[0], atol=1e-5), (a[0], b[0])
             assert torch.allclose(a[1], b[1], rtol=1e-5, atol=1e-5), (a[1], b[1])
         else:
-            assert np.allclose(a[0], b[0], atol=1e-5), (a[0], b[0])
-            assert abs(float(a[1]) - float(b[1])) < 1e-5
+            # with N > 64 the chain multiplies up to N - 1 ratios, each carrying the fp32 rounding of
+            # two independent log-prob evaluations (exp(d) with |d| ~ 1e-7): the products drift by
+            # ~sqrt(N) * 1e-7 relative per epoch on both paths, so later epochs get 1e-4
+            tol = 1e-5 if (N <= 64 or ep == 0) else 1e-4
+            print(f"  epoch {ep}: max |ploss diff| {np.abs(np.array(a[0]) - np.array(b[0])).max():.2e}  "
+                  f"|vloss diff| {abs(float(a[1]) - float(b[1])):.2e}")
+            assert np.allclose(a[0], b[0], atol=tol), (a[0], b[0])
+            assert abs(float(a[1]) - float(b[1])) < 1e-5 * max(1.0, abs(float(b[1])))
         nets = [(fused.policy.params, ref.policy.params, 3e-3)]
         if algo == "ippo":
             nets.append((fused.value.params, ref.value.params, 1e-3))
         for pf, pr, lr in nets:
             for k in pf:
+                # the (all-reduced, clipped) gradients the optimizer stepped with
+                gscale = pr[k].grad.abs().max().item()
+                gerr = (pf[k].grad - pr[k].grad).abs().max().item()
                 err = (pf[k].data - pr[k].data).abs().max().item()
-                assert err < 0.02 * lr, (ep, k, err)
+                print(f"  epoch {ep} {k}: max |g diff| / max|g| = {gerr / max(gscale, 1e-30):.2e}  "
+                      f"max |w diff| / lr = {err / lr:.2e}")
+                if ep == 0 or N > 64:  # both learners stepped from identical weights
+                    assert gerr <= 2e-5 * gscale + 1e-9, (ep, k, gerr, gscale)
+                if N <= 64:
+                    assert err < 0.02 * lr, (ep, k, err)
+        if N > 64:
+            # c5's sparse inputs (lambda = 1/14: most buffer cells are zero in most samples) leave
+            # many w1 gradients at ~1e-8, where Adam's first steps (lr * g / (|g| + 1e-8)) turn
+            # fp32-level gradient differences into lr-sized weight differences; the gradients are
+            # compared above, and the next epoch starts both learners from the fused one's state
+            with torch.no_grad():
+                for k in fused.policy.params:
+                    ref.policy.params[k].copy_(fused.policy.params[k])
+                for a_, b_ in zip(fused.value_network.parameters(), ref.value_network.parameters()):
+                    b_.copy_(a_)
+            # deep copies: load_state_dict keeps same-device state tensors by reference
+            ref.policy_optimizer.load_state_dict(copy.deepcopy(fused.policy_optimizer.state_dict()))
+            ref.value_optimizer.load_state_dict(copy.deepcopy(fused.value_optimizer.state_dict()))
 
 
 def test_happo_chain_kernel_matches_torch_loop():
@@ -313,7 +349,7 @@ def test_happo_chain_kernel_matches_torch_loop():
     from d2dhip import _lib
     lib = _lib.require_gpu()
     g = torch.Generator(device="cuda").manual_seed(5)
-    for N, T, E in ((1, 3, 5), (7, 20, 33), (64, 50, 128)):
+    for N, T, E in ((1, 3, 5), (7, 20, 33), (64, 50, 128), (128, 20, 64), (256, 20, 40)):
         adv = torch.randn(T * E, device="cuda", generator=g)
         lp_old = -torch.rand((T, N, E), device="cuda", generator=g) * 3
         lp_new = lp_old.permute(1, 0, 2).reshape(N, T * E) + 0.3 * torch.randn((N, T * E), device="cuda", generator=g)

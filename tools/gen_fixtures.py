@@ -512,18 +512,19 @@ def _learner_env(kind, episode_length=20):
     return mod.ChannelSelectionEnv(**p), p
 
 
-def gen_learner():
+def gen_learner(only=None, episodes=2, suffix="", algos=("ippo", "d2d")):
     import torch
     ippo = ref_module("algorithms.ippo")
     d2d = ref_module("algorithms.d2d_ppo")
     import sys as _sys
-    only = [a for a in _sys.argv[2:]]
+    if only is None:
+        only = [a for a in _sys.argv[2:]]
     for vname, (kind, useRNN, comb, hl) in LEARNER_VARIANTS.items():
         if only and vname not in only:
             continue
-        for algo in (("ippo",) if kind == "single" else ("ippo", "d2d")):
+        for algo in (("ippo",) if kind == "single" else algos):
             out = {"kind": kind, "useRNN": useRNN, "combinatorial": comb, "history_len": hl, "hidden": 16,
-                   "gamma": 0.6, "episode_length": 20}
+                   "gamma": 0.6, "episode_length": 20, "episodes": episodes}
             env, params = _learner_env(kind)
             out["params_json"] = json.dumps({k: _jsonable(v) for k, v in params.items()})
             torch.manual_seed(3)
@@ -544,7 +545,7 @@ def gen_learner():
             rec_env = RecordingEnv(env)
             lr.env = rec_env
             torch.manual_seed(11)
-            ro = lr.create_rollouts(2)
+            ro = lr.create_rollouts(episodes)
             lr.env = env
             for k, v in rec_env.rec.items():
                 out[f"draws/{k}"] = np.array(v)
@@ -577,11 +578,11 @@ def gen_learner():
             lr.test = lambda num_episodes: (0.5, 1.0, 0, 0.0)
             np.random.seed(21)  # D2D agent permutation stream (d2d_ppo.py:421-422)
             if algo == "ippo":
-                res = lr.train(1, n_epoch=2, num_episodes=2, test_freq=10 ** 9)
+                res = lr.train(1, n_epoch=2, num_episodes=episodes, test_freq=10 ** 9)
                 out["train/policy_loss"] = np.array(res[2])
                 out["train/value_loss"] = np.array(res[3])
             else:
-                res = lr.train(1, num_episodes=2, n_epoch=2, test_freq=10 ** 9)
+                res = lr.train(1, num_episodes=episodes, n_epoch=2, test_freq=10 ** 9)
                 out["train/policy_loss"] = np.array(res[2])          # [epoch][agent in sigma order]
                 out["train/value_loss"] = np.array([float(v) for v in res[3]])
                 np.random.seed(21)
@@ -599,14 +600,61 @@ def gen_learner():
             # preprocess_input_for_rnn on agent 0's obs (ippo.py:390-403)
             if useRNN:
                 out["rnnwin/agent0"] = lr.preprocess_input_for_rnn(obs_t[0]).numpy()
-            np.savez_compressed(os.path.join(OUT, f"learner_{algo}_{vname}.npz"), **out)
-            print(f"learner_{algo}_{vname}: T={len(dones)} scores={np.round(scores, 3)}")
+            np.savez_compressed(os.path.join(OUT, f"learner_{algo}_{vname}{suffix}.npz"), **out)
+            print(f"learner_{algo}_{vname}{suffix}: T={len(dones)} scores={np.round(scores, 3)}")
+
+
+def gen_learner4():
+    """4-episode traces (run on 2 envs x 2 waves, or 4 envs x 1 wave) for the multi-env sample order."""
+    gen_learner(only=["mlp_comb", "rnn_cat", "mlp_d2denv"], episodes=4, suffix="_ep4")
+
+
+def gen_evaltest():
+    """The reference's deterministic evaluation `test(num_episodes)` (ippo.py:345-388,
+    d2d_ppo.py:341-383) for every learner variant: fixed weights, 4 episodes.  Recorded: the
+    weights, the env draws of every reset / step, the actions test() took (argmax / p > 0.5) and
+    its return tuple (mean URLLC score, mean Jain's index, summed channel errors, mean episode
+    reward).  The MLP actors' last layer is scaled x4 before recording so that the softmax is
+    peaked enough for p > 0.5 / argmax decisions to vary (the weights stored are the scaled ones)."""
+    import torch
+    ippo = ref_module("algorithms.ippo")
+    d2d = ref_module("algorithms.d2d_ppo")
+    n_ep = 4
+    for vname, (kind, useRNN, comb, hl) in LEARNER_VARIANTS.items():
+        for algo in (("ippo",) if kind == "single" else ("ippo", "d2d")):
+            out = {"kind": kind, "useRNN": useRNN, "combinatorial": comb, "history_len": hl, "hidden": 16,
+                   "gamma": 0.6, "episode_length": 20, "episodes": n_ep}
+            env, params = _learner_env(kind)
+            out["params_json"] = json.dumps({k: _jsonable(v) for k, v in params.items()})
+            torch.manual_seed(17)
+            np.random.seed(19)
+            if algo == "ippo":
+                lr = ippo.iPPO(env, hidden_size=16, gamma=0.6, device="cpu", useRNN=useRNN, combinatorial=comb,
+                               history_len=hl, early_stopping=False)
+            else:
+                lr = d2d.D2DPPO(env, hidden_size=16, gamma=0.6, device="cpu", useRNN=useRNN, combinatorial=comb,
+                                history_len=hl, early_stopping=False)
+            for i, ag in enumerate(lr.agents):
+                if not useRNN:
+                    with torch.no_grad():
+                        ag.policy_network.linear2.weight.mul_(4.0)
+                _put(out, f"weights/agent{i}/policy", _sd_np(ag.policy_network))
+            rec_env = RecordingEnv(env)
+            lr.env = rec_env
+            np.random.seed(23)
+            res = lr.test(n_ep)
+            for k, v in rec_env.rec.items():
+                out[f"draws/{k}"] = np.array(v)
+            out["result"] = np.array([float(x) for x in res], dtype=np.float64)
+            np.savez_compressed(os.path.join(OUT, f"evaltest_{algo}_{vname}.npz"), **out)
+            acts = np.array(rec_env.rec["actions"])
+            print(f"evaltest_{algo}_{vname}: result={np.round(out['result'], 5)} mean action={acts.mean():.3f}")
 
 
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     table = {"data": gen_data, "env": gen_env, "d2denv": gen_d2denv, "gae": gen_gae, "learner": gen_learner,
-             "baselines": gen_baselines}
+             "baselines": gen_baselines, "evaltest": gen_evaltest, "learner4": gen_learner4}
     # `learner <variant> ...` regenerates only the named learner variants
     which = sys.argv[1:2] if sys.argv[1:2] == ["learner"] else sys.argv[1:]
     for w in which or list(table):

@@ -51,6 +51,7 @@ if __name__ == "__main__":
         env = dict(os.environ)
         if v:
             env["D2D_LIB_VARIANT"] = v
+            env["D2D_ALLOW_ABLATION"] = "1"
         r = subprocess.run([sys.executable, "-c", CODE.format(root=ROOT)], env=env, capture_output=True, text=True,
                            timeout=300)
         line = [l for l in r.stdout.splitlines() if l.startswith("{")]
