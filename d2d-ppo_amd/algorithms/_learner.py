@@ -228,6 +228,8 @@ class BatchedLearnerBase(DataParallelMixin):
         the env replays the draws, the policy computes probs/log-probs/values of the forced actions
         (or, with actions None, acts itself)."""
         b = self._bind_env()
+        if teacher is None and b.E == 1 and num_episodes > 1:
+            b = self._episode_batch(num_episodes)
         env = self.env
         E, L = b.E, env.episode_length
         waves = max(1, math.ceil(num_episodes / E))
@@ -237,6 +239,29 @@ class BatchedLearnerBase(DataParallelMixin):
         tf = self._teacher_tensors(teacher, b, waves) if teacher is not None else None
         self._waves(bufs, b, waves, train, tf)
         return self._rollout_result(bufs, b, waves, train)
+
+    # ---------------------------------------------- episode-parallel rollouts (n_envs == 1)
+    episode_parallel = os.environ.get("D2D_EPISODE_PARALLEL", "1") != "0"
+
+    def _episode_batch(self, n):
+        """The reference drivers build their envs with the default n_envs = 1 and roll out
+        num_episodes episodes one after another (create_rollouts ippo.py:283, test ippo.py:353).  The
+        episodes are independent, so here they run side by side: a private device batch of n envs with
+        the env's parameters and its own Philox counter range (env indices from 2^40, disjoint from the
+        env's own batch) replaces the n sequential waves.  Single process only (data-parallel ranks
+        shard their envs explicitly); D2D_EPISODE_PARALLEL=0 keeps the sequential waves."""
+        main = self.env.batch()
+        if not self.episode_parallel or getattr(self, "world_size", 1) > 1:
+            return main
+        cache = self.__dict__.setdefault("_episode_batches", {})
+        b = cache.get(n)
+        if b is None:
+            from d2dhip.envbatch import EnvBatch
+            if len(cache) >= 2:  # the training and the test batch sizes of a driver
+                cache.pop(next(iter(cache)))
+            b = EnvBatch(main.spec, n, main.device, seed=main.desc.seed, env_base=(1 << 40) + main.desc.env_base)
+            cache[n] = b
+        return b
 
     # ------------------------------------------------- rollout body (eager or captured)
     def _rollout_buffers(self, b, waves, want_values, want_state):
@@ -259,21 +284,23 @@ class BatchedLearnerBase(DataParallelMixin):
         obs_buf, act_buf, logp_buf, rew_i32 = bufs["obs"], bufs["act"], bufs["logp"], bufs["rew"]
         val_buf, state_buf = bufs["val"], bufs["state"]
         want_state = state_buf is not None
+        s.arrival_kinds()  # the reference's reset-time validation (ValueError / AssertionError)
         with torch.no_grad():
             for w in range(waves):
                 t0 = w * L
-                env.reset_batched(want_obs=True, want_state=want_state, out_obs=obs_buf[t0],
-                                  out_state=state_buf[t0] if want_state else None,
-                                  replay_arrivals=None if tf is None else tf["reset_arrivals"][w])
+                b.reset(want_obs=True, want_state=want_state, out_obs=obs_buf[t0],
+                        out_state=state_buf[t0] if want_state else None,
+                        replay_arrivals=None if tf is None else tf["reset_arrivals"][w])
                 for t in range(L):
                     i = t0 + t
                     act = self._policy_slot(obs_buf, t0, i, train, act_buf[i], logp_buf[i],
                                             val_buf[i] if val_buf is not None else None, tf, b)
                     last = t + 1 == L
-                    env.step_batched(act, want_obs=not last, want_state=want_state and not last,
-                                     out_obs=None if last else obs_buf[i + 1],
-                                     out_state=None if (last or not want_state) else state_buf[i + 1],
-                                     out_reward=rew_i32[i], replay=None if tf is None else tf["replay"][i])
+                    b.step(act, want_obs=not last, want_state=want_state and not last,
+                           out_obs=None if last else obs_buf[i + 1],
+                           out_state=None if (last or not want_state) else state_buf[i + 1],
+                           out_reward=rew_i32[i], replay=None if tf is None else tf["replay"][i])
+                env.timestep = b.timestep
                 bufs["recv"][w].copy_(b.received.sum(1))
                 bufs["disc"][w].copy_(b.discarded.sum(1))
                 bufs["eprew"][w].copy_(rew_i32[t0:t0 + L].sum(0))

@@ -17,14 +17,16 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libd2dhip.so")
 # A/B timing builds only (tools/gpu/ablate_update.py): another in-tree build of the same library.
 # Those builds drop parts of the update on purpose (wrong gradients), so the variable is honoured
 # only together with an explicit D2D_ALLOW_ABLATION=1, loudly, and the learners refuse to train on it.
+# "asan" is the host-sanitizer build (make -C d2d-ppo_amd asan, run only by tests/test_sanitizers_cpu.py
+# on a GPU-less host): correct, but never a product library either.
 VARIANT = os.environ.get("D2D_LIB_VARIANT") or None
 if VARIANT:
-    if os.environ.get("D2D_ALLOW_ABLATION") != "1":
+    if VARIANT != "asan" and os.environ.get("D2D_ALLOW_ABLATION") != "1":
         raise RuntimeError(f"D2D_LIB_VARIANT={VARIANT} selects an ablation build of libd2dhip (wrong results "
                            f"by design); set D2D_ALLOW_ABLATION=1 as well to load it, or unset it")
     LIB_PATH = os.path.join(PKG_DIR, "lib", f"libd2dhip_{VARIANT}.so")
-    print(f"[d2dhip] WARNING: loading ablation build {LIB_PATH} (results are NOT correct)", file=sys.stderr,
-          flush=True)
+    print(f"[d2dhip] WARNING: loading {'sanitizer' if VARIANT == 'asan' else 'ablation'} build {LIB_PATH} "
+          f"(not a product library)", file=sys.stderr, flush=True)
 
 
 def refuse_ablation(what):
