@@ -119,11 +119,25 @@ class BatchedLearnerBase(DataParallelMixin):
                            and os.environ.get("D2D_FUSED_POLICY", "1") != "0")
         return self._fused
 
+    def _gru_ok(self):
+        """The GRU window-policy kernels (csrc/gru_kernels.hip) cover the RNN learners with H <= 64,
+        A <= 16 and F + 1 <= 32 (the update kernel's input tile; the reference's envs have F <= 30)."""
+        if getattr(self, "_gru", None) is None:
+            p = self.policy
+            self._gru = (self.useRNN and p.kind == "rnn" and p.H <= 64 and p.A <= 16 and p.F + 1 <= 32
+                         and (self.kind == "comb") == bool(self.combinatorial)
+                         and os.environ.get("D2D_FUSED_POLICY", "1") != "0")
+        return self._gru
+
+    def _gru_kind(self):
+        return "sigmoid" if self.combinatorial else "softmax"
+
     def _fused_update_ok(self):
-        """The fused HIP update kernels (csrc/update_kernels.hip) cover the MLP actors with
-        F + 1 <= 64 inputs (and the iPPO per-agent MLP critics)."""
+        """The fused HIP update kernels cover the MLP actors with F + 1 <= 64 inputs (and the iPPO
+        per-agent MLP critics; csrc/update_kernels.hip) and the GRU policies / critics
+        (csrc/gru_kernels.hip)."""
         if getattr(self, "_fused_upd", None) is None:
-            self._fused_upd = (self._fused_ok() and self.policy.F + 1 <= 64
+            self._fused_upd = (((self._fused_ok() and self.policy.F + 1 <= 64) or self._gru_ok())
                                and (self.kind == "comb") == bool(self.combinatorial)
                                and os.environ.get("D2D_FUSED_UPDATE", "1") != "0")
         return self._fused_upd
@@ -143,7 +157,13 @@ class BatchedLearnerBase(DataParallelMixin):
 
     def _logp_forced(self, ro):
         """log-probs of the rollout's own actions under the current actor params, for every
-        sample: the policy kernel in forced mode over the T*E slots at once -> [N][T*E] (time-major)."""
+        sample: the policy kernel in forced mode over the T*E slots at once -> [N][T*E] (time-major).
+        GRU policies: the training windows (front-zero-padded, ippo.py:390-403)."""
+        if self.useRNN:
+            from d2dhip import gru
+            _, lp = gru.policy({k: v.data for k, v in self.policy.params.items()}, ro.obs, self._gru_kind(),
+                               self.history_len, ro.L, 0, ro.T, padded=True, forced=ro.actions)
+            return lp
         from d2dhip import _lib
         lib = _lib.require_gpu()
         N, TE = self.policy.N, ro.T * ro.E
@@ -178,6 +198,22 @@ class BatchedLearnerBase(DataParallelMixin):
     def _policy_slot(self, obs_buf, t0, i, train, act_out, logp_out, val_out, tf, b):
         """Actions for slot i of every env (written to act_out [E][N]), log-probs [N][E], values [N][E]."""
         forced = None if (tf is None or tf["actions"] is None) else tf["actions"][i]
+        if self._gru_ok():
+            # GRU window policy (+ the iPPO GRU critic): the window of slot i is rebuilt in-kernel from
+            # the rollout buffer (unpadded, the last <= history_len obs of the episode, ippo.py:302-304)
+            from d2dhip import gru
+            E, N = b.E, self.policy.N
+            fz = None if forced is None else self._env_actions(forced).contiguous().view(1, E, N)
+            gru.policy({k: v.data for k, v in self.policy.params.items()}, obs_buf, self._gru_kind(),
+                       self.history_len, self.env.episode_length, i, 1, padded=False, forced=fz,
+                       rng_step=b.rng_step, deterministic=not train, seed=self._policy_seed(),
+                       env_base=b.desc.env_base, rng_offset=b.rng_off.data_ptr(), actions_out=act_out.view(1, E, N),
+                       out=logp_out)
+            if val_out is not None:
+                crit = self.value
+                gru.policy({k: v.data for k, v in crit.params.items()}, obs_buf, None, self.history_len,
+                           self.env.episode_length, i, 1, padded=False, out=val_out)
+            return act_out
         if self._fused_ok() and (self.kind == "comb") == bool(self.combinatorial):
             from d2dhip import _lib
             lib = _lib.require_gpu()
@@ -335,7 +371,7 @@ class BatchedLearnerBase(DataParallelMixin):
         (policy kernel, env kernel) per wave + the statistics): at small batches the slot loop is
         bound by per-launch host work, not the GPU.  Large rollouts (obs buffer > 4 GiB, where the
         kernels dominate) stay eager rather than pinning a second copy of the buffers."""
-        if not (self.graph_rollout and train and not self.useRNN and self._fused_ok()
+        if not (self.graph_rollout and train and (self._gru_ok() or (not self.useRNN and self._fused_ok()))
                 and (self.kind == "comb") == bool(self.combinatorial)):
             return False
         s = b.spec

@@ -227,10 +227,11 @@ class D2DPPO(BatchedLearnerBase):
         T, E, N = ro.T, ro.E, self.n_agents
         A = adv[:, :, 0].reshape(-1)                                                   # [T*E]
         with torch.no_grad():
-            if self._actors_unchanged_since(ro):
+            if not self.useRNN and self._actors_unchanged_since(ro):
                 # first epoch on this rollout: the epoch-start actors ARE the rollout's, and the
                 # policy kernel's forced log-probs equal the sampled ones bit for bit, so every
-                # ratio is exactly 1 and the chain is A for every agent (no forced pass needed)
+                # ratio is exactly 1 and the chain is A for every agent (no forced pass needed).
+                # Not for GRU policies: their training windows are padded, the rollout's were not (Q5)
                 M = A.expand(N, T * E)
             else:
                 M = self._chain_dev(A, self._logp_forced(ro), ro.logp, cycle, T, E)     # [N][T*E]
@@ -238,9 +239,16 @@ class D2DPPO(BatchedLearnerBase):
         pp = self.policy.params
         kind = "comb" if self.combinatorial else "chsel"
         beta = float(self.beta_entropy)
-        _, sa = actor_grads({k: v.data for k, v in pp.items()}, ro.obs, ro.actions, ro.logp.permute(0, 2, 1),
-                            M.view(N, T, E).permute(1, 2, 0), kind, clip=cliprange, beta=beta,
-                            grads=self._grad_buffers(pp))
+        if self.useRNN:  # GRU policies: BPTT over the padded training windows (gru_kernels.hip)
+            from d2dhip import gru
+            _, sa = gru.grads({k: v.data for k, v in pp.items()}, ro.obs, self._gru_kind(), self.history_len, ro.L,
+                              M.view(N, T, E).permute(1, 2, 0), actions=ro.actions,
+                              logp_old=ro.logp.permute(0, 2, 1), clip=cliprange, beta=beta,
+                              grads=self._grad_buffers(pp))
+        else:
+            _, sa = actor_grads({k: v.data for k, v in pp.items()}, ro.obs, ro.actions, ro.logp.permute(0, 2, 1),
+                                M.view(N, T, E).permute(1, 2, 0), kind, clip=cliprange, beta=beta,
+                                grads=self._grad_buffers(pp))
         self._phase("actor_grad")
         self._reduce_grads(self.policy.parameters())
         self._phase("allreduce")

@@ -221,16 +221,27 @@ class iPPO(BatchedLearnerBase):
         pp, vp = self.policy.params, self.value.params
         kind = "comb" if self.combinatorial else "chsel"
         B = ro.T * ro.E
-        _, sa = actor_grads({k: v.data for k, v in pp.items()}, ro.obs, ro.actions, ro.logp.permute(0, 2, 1),
-                            ro.adv_tne.permute(0, 2, 1), kind, clip=cliprange, beta=beta,
-                            grads=self._grad_buffers(pp))
+        if self.useRNN:  # GRU policies / critics: BPTT over the padded training windows (gru_kernels.hip)
+            from d2dhip import gru
+            _, sa = gru.grads({k: v.data for k, v in pp.items()}, ro.obs, self._gru_kind(), self.history_len, ro.L,
+                              ro.adv_tne.permute(0, 2, 1), actions=ro.actions, logp_old=ro.logp.permute(0, 2, 1),
+                              clip=cliprange, beta=beta, grads=self._grad_buffers(pp))
+        else:
+            _, sa = actor_grads({k: v.data for k, v in pp.items()}, ro.obs, ro.actions, ro.logp.permute(0, 2, 1),
+                                ro.adv_tne.permute(0, 2, 1), kind, clip=cliprange, beta=beta,
+                                grads=self._grad_buffers(pp))
         self._phase("actor_grad")
         self._reduce_grads(self.policy.parameters())
         self._phase("allreduce")
         self.policy_optimizer.step()
         self._phase("adam")
-        _, sv = critic_grads({k: v.data for k, v in vp.items()}, ro.obs, ro.ret_tne.permute(0, 2, 1),
-                             grads=self._grad_buffers(vp))
+        if self.useRNN:
+            from d2dhip import gru
+            _, sv = gru.grads({k: v.data for k, v in vp.items()}, ro.obs, None, self.history_len, ro.L,
+                              ro.ret_tne.permute(0, 2, 1), grads=self._grad_buffers(vp))
+        else:
+            _, sv = critic_grads({k: v.data for k, v in vp.items()}, ro.obs, ro.ret_tne.permute(0, 2, 1),
+                                 grads=self._grad_buffers(vp))
         self._phase("critic_grad")
         self._reduce_grads(self.value.parameters())
         self._phase("allreduce")

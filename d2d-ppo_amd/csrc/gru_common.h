@@ -1,0 +1,222 @@
+// GRU window policies (the reference's RNN module, /root/reference/algorithms/ippo.py:14-51 ==
+// d2d_ppo.py:24-59) on gfx950: shared pieces of the behaviour-policy kernel and the BPTT update
+// kernel (gru_kernels.hip).
+//
+//   r = sigmoid(W_ir x + b_ir + W_hr h + b_hr)          torch.nn.GRU, gate order (r, z, n)
+//   z = sigmoid(W_iz x + b_iz + W_hz h + b_hz)
+//   n = tanh   (W_in x + b_in + r * (W_hn h + b_hn))
+//   h' = (1 - z) * n + z * h                             h0 = 0 for every window
+//   head: relu(W1 h_L + b1) -> W2 . + b2 -> sigmoid (combinatorial) / softmax / none (value)
+//
+// Layout (v_mfma_f32_16x16x4_f32, lane = (g, i), g = lane >> 4, i = lane & 15): one 16-sample
+// tile per wave, the sample (env) on i.  Gate pre-activations are computed transposed,
+// G^T[gate row][sample] = W . [x | h]^T, so an accumulator tile holds gate rows 16T + 4g + r of
+// sample i -- and the r, z and n rows of hidden unit u = 16t + 4g + r sit in the SAME lane and
+// register (tiles t, HT + t, 2HT + t): the gate math is lane-local, and the new h lands exactly
+// where the next step's MFMA wants its B operand with the k order permuted to
+// kidx(s, g) = 16 (s >> 2) + 4 g + (s & 3) (k-step s, lane group g).  No data movement
+// between steps.  fp32 MFMA: every product exact, fp32 accumulation -- the torch fp32 numerics to
+// ~1e-7 relative per step.
+//
+// Gate-row index R in [0, 3 HW), HW = 16 HT: gate G = R / HW, unit u = R % HW (rows with u >= H are
+// zero and keep their h at 0).  Input column F of the input image carries the biases (x_F = 1):
+// b_ir + b_hr, b_iz + b_hz, b_in; b_hn is added to the recurrent n part separately.
+#pragma once
+#include "mlp_common.h"
+
+namespace d2d {
+
+struct GruW {  // agent-stacked torch tensors (StackedNets kind "rnn")
+  const float *w_ih, *w_hh, *b_ih, *b_hh;  // [N][3H][F], [N][3H][H], [N][3H], [N][3H]
+  const float *w1, *b1, *w2, *b2;          // layers.0 [N][H][H], [N][H]; layers.2 [N][A][H], [N][A]
+};
+
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// LDS weight images, fp32, row-major with an XOR swizzle of the 4-float groups (row-dependent)
+// so that the 16 rows of a ds_read_b128 A fragment hit distinct banks.  W = 16, 32 or 64.
+template <int W>
+__device__ __forceinline__ int swz(int row, int col) {
+  return row * W + (col ^ ((row & (W / 4 - 1)) << 2));
+}
+template <int W>
+__device__ __forceinline__ f32x4 lds4(const float* img, int row, int col4) {
+  return *reinterpret_cast<const f32x4*>(img + swz<W>(row, col4));
+}
+
+// e^v to ~1 ulp on the hardware exp2: v * log2(e) is carried as th + tl (FMA residual plus the
+// low part of log2 e), 2^tl ~ 1 + tl ln 2.  (__expf rounds v * log2 e first: ~|v| ulp of error,
+// which the recurrence accumulates over the window.)
+__device__ __forceinline__ float exp_acc(float v) {
+  const float kL = 1.44269502162933349609375f, kLlo = 1.925963033500e-08f;
+  const float th = v * kL;
+  const float tl = fmaf(v, kL, -th) + v * kLlo;
+  return __builtin_amdgcn_exp2f(th) * fmaf(tl, 0.693147180559945f, 1.f);
+}
+__device__ __forceinline__ float sigmoidf_(float v) { return __builtin_amdgcn_rcpf(1.f + exp_acc(-v)); }
+// tanh(v) = 1 - 2 / (e^{2v} + 1): absolute error ~1e-7, saturates cleanly at +-1
+__device__ __forceinline__ float tanhf_(float v) { return 1.f - 2.f * __builtin_amdgcn_rcpf(exp_acc(2.f * v) + 1.f); }
+
+// Fill the input / recurrent images of agent k (all threads of the workgroup).
+template <int HT, int IT>
+__device__ void load_gru_images(float* wih_s, float* whh_s, const GruW& w, int k, int H, int F, int tid, int nthr) {
+  constexpr int HW = 16 * HT, IW = 16 * IT, R3 = 3 * HW;
+  const float* Wih = w.w_ih + (size_t)k * 3 * H * F;
+  const float* Whh = w.w_hh + (size_t)k * 3 * H * H;
+  const float* bih = w.b_ih + (size_t)k * 3 * H;
+  const float* bhh = w.b_hh + (size_t)k * 3 * H;
+  for (int idx = tid; idx < R3 * IW; idx += nthr) {
+    const int R = idx / IW, c = idx - R * IW, G = R / HW, u = R - G * HW;
+    float v = 0.f;
+    if (u < H) {
+      const int src = G * H + u;
+      if (c < F) v = Wih[(size_t)src * F + c];
+      else if (c == F) v = G < 2 ? bih[src] + bhh[src] : bih[src];
+    }
+    wih_s[swz<IW>(R, c)] = v;
+  }
+  for (int idx = tid; idx < R3 * HW; idx += nthr) {
+    const int R = idx / HW, c = idx - R * HW, G = R / HW, u = R - G * HW;
+    whh_s[swz<HW>(R, c)] = (u < H && c < H) ? Whh[(size_t)(G * H + u) * H + c] : 0.f;
+  }
+}
+
+// x tile of one window step: lane (g, i) <- x[env i][16q + 4g + r] (q < IT, r < 4), the bias
+// column F = 1, columns past F = 0.  `off0` = float offset of the obs row (slot, e0, agent k),
+// `row_stride` = floats between consecutive envs (N * F); rows of envs >= E read 0 through the
+// range-checked buffer descriptor (zero: the x of a front-padding step, bias column only).
+template <int IT>
+__device__ __forceinline__ void load_x(float (&x)[IT][4], const float* obs, size_t off0, int64_t total_floats,
+                                       int row_stride, int F, int g, int i, bool env_ok, bool zero) {
+  const size_t row0 = off0;
+  const int64_t rest = (total_floats - (int64_t)row0) * 4;
+  const uint32_t nbytes = zero || rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(obs + row0), 0, nbytes, 0x00020000);
+  const uint32_t vbase = env_ok ? (uint32_t)(i * row_stride) * 4u : 0x80000000u;
+#pragma unroll
+  for (int q = 0; q < IT; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int col = 16 * q + 4 * g + r;
+      const float v = uf(__builtin_amdgcn_raw_buffer_load_b32(rsrc, vbase + 4u * (uint32_t)col, 0, 0));
+      x[q][r] = col < F ? v : col == F ? 1.f : 0.f;
+    }
+}
+
+// Pre-activations of one step: rz[T] (T < 2 HT: input + recurrent + both biases of r / z rows),
+// ni[t] (input part of n incl. b_in), nh[t] (recurrent part of n incl. b_hn).  h_zero: h = 0 (the
+// recurrent products vanish).  W_ih from the swizzled LDS image (WIH_LDS) or from the same image
+// unswizzled in global memory (L2-resident; the update kernel).
+template <int HT, int IT, bool WIH_LDS>
+__device__ __forceinline__ void gru_preact(const float* wih, const float* whh_s,
+                                           const float (&x)[IT][4], const float (&h)[HT][4], const f32x4 (&bhn)[HT],
+                                           f32x4 (&rz)[2 * HT], f32x4 (&ni)[HT], f32x4 (&nh)[HT], int g, int i,
+                                           bool h_zero) {
+  constexpr int HW = 16 * HT, IW = 16 * IT;
+#pragma unroll
+  for (int T = 0; T < 3 * HT; ++T) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+      f32x4 wv;
+      if constexpr (WIH_LDS) wv = lds4<IW>(wih, 16 * T + i, 16 * q + 4 * g);
+      else wv = *reinterpret_cast<const f32x4*>(wih + (size_t)(16 * T + i) * IW + 16 * q + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = mfma4(wv[r], x[q][r], acc);
+    }
+    if (T < 2 * HT) rz[T] = acc;
+    else ni[T - 2 * HT] = acc;
+  }
+#pragma unroll
+  for (int t = 0; t < HT; ++t) nh[t] = bhn[t];
+  if (h_zero) return;
+#pragma unroll
+  for (int T = 0; T < 3 * HT; ++T) {
+    f32x4 acc = T < 2 * HT ? rz[T] : nh[T - 2 * HT];
+#pragma unroll
+    for (int q = 0; q < HT; ++q) {
+      const f32x4 wv = lds4<HW>(whh_s, 16 * T + i, 16 * q + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = mfma4(wv[r], h[q][r], acc);
+    }
+    if (T < 2 * HT) rz[T] = acc;
+    else nh[T - 2 * HT] = acc;
+  }
+}
+
+// Gate math in place: h <- (1 - z) n + z h.  Optionally returns r, z, n (the backward recomputes).
+template <int HT>
+__device__ __forceinline__ void gru_gates(const f32x4 (&rz)[2 * HT], const f32x4 (&ni)[HT], const f32x4 (&nh)[HT],
+                                          float (&h)[HT][4]) {
+#pragma unroll
+  for (int t = 0; t < HT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float rr = sigmoidf_(rz[t][r]), zz = sigmoidf_(rz[HT + t][r]);
+      const float nn = tanhf_(ni[t][r] + rr * nh[t][r]);
+      h[t][r] = (1.f - zz) * nn + zz * h[t][r];
+    }
+}
+
+// b_hn of agent k in accumulator layout (unit 16t + 4g + r)
+template <int HT>
+__device__ __forceinline__ void load_bhn(f32x4 (&bhn)[HT], const GruW& w, int k, int H, int g) {
+#pragma unroll
+  for (int t = 0; t < HT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int u = 16 * t + 4 * g + r;
+      bhn[t][r] = u < H ? w.b_hh[(size_t)k * 3 * H + 2 * H + u] : 0.f;
+    }
+}
+
+// Head forward: pre1 = W1 h + b1 (accumulator layout, unit 16t + 4g + r), y = relu(pre1),
+// lg = W2 y + b2 (rows = output 4g + r, sample i).  W1 / W2 fragments straight from global (L2):
+// once per window.
+template <int HT>
+__device__ __forceinline__ void gru_head(const GruW& w, int k, int H, int A, const float (&h)[HT][4],
+                                         f32x4 (&pre1)[HT], float (&y)[HT][4], f32x4& lg, int g, int i) {
+  const float* W1 = w.w1 + (size_t)k * H * H;
+  const float* W2 = w.w2 + (size_t)k * A * H;
+#pragma unroll
+  for (int t = 0; t < HT; ++t) {
+    f32x4 acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int u = 16 * t + 4 * g + r;
+      acc[r] = u < H ? w.b1[(size_t)k * H + u] : 0.f;
+    }
+    const int row = 16 * t + i;
+#pragma unroll
+    for (int q = 0; q < HT; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = 16 * q + 4 * g + r;
+        const float wv = (row < H && col < H) ? W1[(size_t)row * H + col] : 0.f;
+        acc = mfma4(wv, h[q][r], acc);
+      }
+    pre1[t] = acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[t][r] = relu(acc[r]);
+  }
+  f32x4 acc;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int o = 4 * g + r;
+    acc[r] = o < A ? w.b2[(size_t)k * A + o] : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < HT; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int col = 16 * q + 4 * g + r;
+      const float wv = (i < A && col < H) ? W2[(size_t)i * H + col] : 0.f;
+      acc = mfma4(wv, y[q][r], acc);
+    }
+  lg = acc;
+}
+
+}  // namespace d2d

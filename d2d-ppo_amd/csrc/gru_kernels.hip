@@ -1,0 +1,756 @@
+// GRU window policies on gfx950 (gru_common.h has the cell and the layout).
+//
+// 1. gru_policy_kernel -- the behaviour policy / value of the RNN learners, replacing per agent and
+//    per step the reference's batch-1 calls
+//      RNN.forward over the history window          /root/reference/algorithms/ippo.py:14-51
+//      PPO.select_action / evaluate                 ippo.py:154-191 (d2d_ppo.py:159-196)
+//    for every (slot, env, agent) tile of a launch.  Windows are rebuilt in-kernel from the rollout
+//    buffer obs[T][E][N][F]: for slot s with episode position p = s % ep_len the window is the last
+//    S = min(p + 1, L) obs of the episode, either unpadded (rollout / test: create_rollouts
+//    ippo.py:302-304, test ippo.py:362-364) or front-zero-padded to L steps (training:
+//    preprocess_input_for_rnn ippo.py:390-403; quirk Q5).  h0 = 0 for every window.
+// 2. gru_grad_kernel -- evaluate + clipped-surrogate / MSE loss + backward of PPO.train_step
+//    (ippo.py:194-217, d2d_ppo.py:198-216) for GRU policies and the iPPO GRU critic: per 16-sample
+//    tile the padded window's forward (hidden states kept in a per-wave global scratch), the head
+//    and the loss gradient, then backpropagation through time over the window.  Weight gradients:
+//    W_hh in LDS (accumulated by the four waves with ds_add_f32), W_ih / head / biases in
+//    registers; one partial per (workgroup, agent), summed in fixed order by gru_reduce_kernel.
+#include <algorithm>
+#include <cmath>
+
+#include "gru_common.h"
+#include "policy_epilogue.h"
+#include "ppo_epilogue.h"
+
+namespace d2d {
+
+struct GruArgs {
+  int T, E, N, F, H, A, L, ep_len, kind;
+  int slot0, n_slots, padded, env_tiles;  // tiles: slots [slot0, slot0 + n_slots) x ceil(E / 16)
+  GruW w;
+  const float* obs;                       // [T][E][N][F]
+  int64_t obs_floats;                     // T * E * N * F
+  // ---- policy kernel
+  MlpArgs ep;                             // epilogue view: ep.E = n_slots * E (slot-major samples)
+  float* value_out;                       // kind 2: [N][n_slots * E]
+  // ---- grad kernel
+  float clip_lo, clip_hi, beta, scale, inv_A;
+  int mask_bytes;
+  const void* actions;                    // [T][E][N] masks / ids
+  const float* logp_old;                  // element (t, e, k) at t*st[0] + e*st[1] + k*st[2]
+  const float* weight;                    // advantage / M (actor) or return target (critic)
+  int64_t lo_st[3], w_st[3];
+  float* partial;                         // [G][N][P]
+  float* hist;                            // [G * N * 4 waves][L][64 lanes][4 HT] per-wave hidden-state scratch
+  float* wimg;                            // [N][3 * 16 HT][16 IT] input images (gru_wih_image_kernel)
+  int G, P;
+};
+
+enum { kGruBernoulli = 0, kGruCategorical = 1, kGruValue = 2 };
+
+// ------------------------------------------------------------------------------ policy kernel
+// Workgroup = agent k x a strided set of tiles; 8 waves (2 per SIMD), one 16-env tile per wave at a
+// time.  LDS: the agent's input and recurrent images (fp32, swizzled; 72 KB at H = 64, F < 32).
+template <int HT, int IT, int KIND, int MODE>
+__global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
+  constexpr int HW = 16 * HT, IW = 16 * IT, R3 = 3 * HW;
+  __shared__ float wih_s[R3 * IW];
+  __shared__ float whh_s[R3 * HW];
+  const int k = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, F = a.F, N = a.N, E = a.E;
+  load_gru_images<HT, IT>(wih_s, whh_s, a.w, k, H, F, tid, blockDim.x);
+  f32x4 bhn[HT];
+  load_bhn<HT>(bhn, a.w, k, H, g);
+  const uint32_t rng = (MODE == kModeSample && a.ep.rng_off) ? a.ep.rng_step + *a.ep.rng_off : a.ep.rng_step;
+  __syncthreads();
+
+  const int n_tiles = a.n_slots * a.env_tiles;
+  const int nw = gridDim.y * (blockDim.x >> 6);
+  for (int tile = blockIdx.y * (blockDim.x >> 6) + wave; tile < n_tiles; tile += nw) {  // wave-uniform
+    const int sl = tile / a.env_tiles;
+    const int slot = a.slot0 + sl;
+    const int e0 = (tile - sl * a.env_tiles) * 16;
+    const int env = e0 + i;
+    const bool ok = env < E;
+    const int pos = slot % a.ep_len;
+    const int S = min(pos + 1, a.L);
+    const int lo = slot - S + 1;
+    const int pad = a.padded ? a.L - S : 0;
+    float h[HT][4];
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[t][r] = 0.f;
+    float x[IT][4];
+    for (int j = 0; j < pad + S; ++j) {
+      const bool zero = j < pad;
+      const int row_slot = zero ? lo : lo + (j - pad);
+      load_x<IT>(x, a.obs, (((size_t)row_slot * E + e0) * N + k) * F, a.obs_floats, N * F, F, g, i, ok, zero);
+      f32x4 rz[2 * HT], ni[HT], nh[HT];
+      gru_preact<HT, IT, true>(wih_s, whh_s, x, h, bhn, rz, ni, nh, g, i, j == 0);
+      gru_gates<HT>(rz, ni, nh, h);
+    }
+    f32x4 pre1[HT], lg;
+    float y[HT][4];
+    gru_head<HT>(a.w, k, H, KIND == kGruValue ? 1 : a.A, h, pre1, y, lg, g, i);
+    const int samp = sl * E + env;  // slot-major sample index of the launch
+    if constexpr (KIND == kGruValue) {
+      if (ok && g == 0) a.value_out[(size_t)k * a.ep.E + samp] = lg[0];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lg[r] *= kLog2e;
+      // HALF = false: every lane group holds 4 outputs of the same sample
+      policy_epilogue<KIND == kGruBernoulli ? 0 : 1, false, false, MODE, false, KIND == kGruBernoulli>(
+          a.ep, lg, 0.f, samp, ok, k, g, rng);
+    }
+  }
+}
+
+
+// -------------------------------------------------------------------------------- grad kernel
+// Per-wave LDS scratch: accumulator-layout columns (one sample per lane i) written so that the MFMA
+// k axis runs over samples: row-major [rows][16], sample e at column pcol(e) = 4 (e & 3) + (e >> 2),
+// so the ds_read_b128 of lane (g, i) at columns [4g, 4g + 4) yields samples 4s + g for k-steps
+// s = 0..3 (the A fragment of row `row`, or the B fragment of column `row`).
+__device__ __forceinline__ int pcol(int e) { return ((e & 3) << 2) | (e >> 2); }
+__device__ __forceinline__ f32x4 sc_frag(const float* sc, int row, int g) {
+  return *reinterpret_cast<const f32x4*>(sc + row * 16 + 4 * g);
+}
+
+// Per-sample epilogue inputs of a tile (every lane group holds its sample's values).
+struct GruIn {
+  uint32_t act;
+  float lo, w;
+};
+
+template <int KIND>
+__device__ __forceinline__ GruIn load_gru_in(const GruArgs& a, int t, int env, int k, bool ok) {
+  GruIn in{0u, 0.f, 0.f};
+  const int e = ok ? env : 0;
+  in.w = a.weight[(int64_t)t * a.w_st[0] + (int64_t)e * a.w_st[1] + (int64_t)k * a.w_st[2]];
+  if constexpr (KIND != kGruValue) {
+    const size_t cell = ((size_t)t * a.E + e) * a.N + k;
+    in.act = KIND == kGruCategorical ? reinterpret_cast<const unsigned char*>(a.actions)[cell]
+                                     : load_mask(a.actions, cell, a.mask_bytes);
+    in.lo = a.logp_old[(int64_t)t * a.lo_st[0] + (int64_t)e * a.lo_st[1] + (int64_t)k * a.lo_st[2]];
+  }
+  return in;
+}
+
+// Register partial sums of one wave, flattened for the cross-wave reduction.
+template <int HT, int IT>
+struct GruAcc {
+  f32x4 wih[3 * HT][IT];   // dW_ih (+ bias column F): D[gate row 16T + 4g + r][input 16U + i]
+  f32x4 w1[HT][HT];        // dW1: D[unit 16t + 4g + r][unit 16U + i]
+  f32x4 w2[HT];            // dW2: D[output 4g + r][unit 16U + i]
+  float b1[HT][4], b2[4], bhn[HT][4];  // per-sample-lane partial sums (rows 16t + 4g + r / 4g + r)
+  float st[2];             // loss sums
+  static constexpr int NV = 3 * HT * IT * 4 + HT * HT * 4 + HT * 4 + HT * 4 + 4 + HT * 4 + 2;
+  // fn(v, x) on every accumulator in a fixed order (x a local copy, written back)
+  template <class Fn>
+  __device__ __forceinline__ void each(Fn fn) {
+    int v = 0;
+#pragma unroll
+    for (int T = 0; T < 3 * HT; ++T)
+#pragma unroll
+      for (int U = 0; U < IT; ++U)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { float x = wih[T][U][r]; fn(v++, x); wih[T][U][r] = x; }
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int U = 0; U < HT; ++U)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { float x = w1[t][U][r]; fn(v++, x); w1[t][U][r] = x; }
+#pragma unroll
+    for (int U = 0; U < HT; ++U)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { float x = w2[U][r]; fn(v++, x); w2[U][r] = x; }
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { fn(v++, b1[t][r]); fn(v++, bhn[t][r]); }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) fn(v++, b2[r]);
+    fn(v++, st[0]);
+    fn(v++, st[1]);
+  }
+};
+
+// Partial layout per (workgroup, agent): the gradient of every torch tensor of the RNN module
+// (StackedNets "rnn": w_ih, w_hh, b_ih, b_hh, layers.0 w/b, layers.2 w/b), then the 2 loss sums.
+struct GruOff {
+  int wih, whh, bih, bhh, w1, b1, w2, b2, st, P;
+  __device__ __host__ GruOff(int H, int F, int A) {
+    wih = 0; whh = 3 * H * F; bih = whh + 3 * H * H; bhh = bih + 3 * H; w1 = bhh + 3 * H; b1 = w1 + H * H;
+    w2 = b1 + H; b2 = w2 + A * H; st = b2 + A; P = st + 2;
+  }
+};
+
+// Workgroup = agent k x a strided set of 16-sample tiles; 4 waves (one per SIMD: ~400 VGPRs).
+// LDS (H = 64): W_hh image 48 KB + dW_hh accumulator 48 KB + 4 x 16 KB wave scratch = 160 KB.
+template <int HT, int IT, int KIND>
+__global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
+  constexpr int HW = 16 * HT, R3 = 3 * HW, SROWS = R3 + HW;
+  __shared__ float whh_s[R3 * HW];
+  __shared__ float dwhh_s[R3 * HW];
+  __shared__ float scr[4][SROWS * 16];
+  const int k = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H, F = a.F, N = a.N, E = a.E, A = KIND == kGruValue ? 1 : a.A, L = a.L;
+  float* sc = scr[wave];
+  {
+    const float* Whh = a.w.w_hh + (size_t)k * 3 * H * H;
+    for (int idx = tid; idx < R3 * HW; idx += blockDim.x) {
+      const int R = idx / HW, c = idx - R * HW, G = R / HW, u = R - G * HW;
+      whh_s[swz<HW>(R, c)] = (u < H && c < H) ? Whh[(size_t)(G * H + u) * H + c] : 0.f;
+      dwhh_s[idx] = 0.f;
+    }
+  }
+  f32x4 bhn[HT];
+  load_bhn<HT>(bhn, a.w, k, H, g);
+  GruAcc<HT, IT> acc;
+  acc.each([](int, float& x) { x = 0.f; });
+  const float* W1 = a.w.w1 + (size_t)k * H * H;
+  const float* W2 = a.w.w2 + (size_t)k * A * H;
+  // the input image of gru_common.h (bias column F) written by gru_wih_image_kernel: A fragments
+  // straight from L2 every step (registers are the update kernel's scarce resource)
+  const float* wimg = a.wimg + (size_t)k * 3 * HW * (16 * IT);
+  float* hist = a.hist + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave) * (size_t)L * 64 * 4 * HT;
+  __syncthreads();
+
+  const int n_tiles = a.T * a.env_tiles;
+  for (int tile = blockIdx.y * 4 + wave; tile < n_tiles; tile += gridDim.y * 4) {  // wave-uniform
+    const int slot = tile / a.env_tiles;
+    const int e0 = (tile - slot * a.env_tiles) * 16;
+    const int env = e0 + i;
+    const bool ok = env < E;
+    const int pos = slot % a.ep_len;
+    const int S = min(pos + 1, L);
+    const int lo = slot - S + 1;
+    const int pad = L - S;  // training windows: front-zero-padded to L (preprocess_input_for_rnn)
+    const GruIn in = load_gru_in<KIND>(a, slot, env, k, ok);
+    auto row_of = [&](int j) { return (((size_t)(j < pad ? lo : lo + j - pad) * E + e0) * N + k) * F; };
+
+    // ---- forward over the window; h_j (j < L - 1) to the wave's scratch
+    float h[HT][4];
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[t][r] = 0.f;
+    for (int j = 0; j < L; ++j) {
+      float x[IT][4];
+      load_x<IT>(x, a.obs, row_of(j), a.obs_floats, N * F, F, g, i, ok, j < pad);
+      f32x4 rz[2 * HT], ni[HT], nh[HT];
+      gru_preact<HT, IT, false>(wimg, whh_s, x, h, bhn, rz, ni, nh, g, i, j == 0);
+      gru_gates<HT>(rz, ni, nh, h);
+      if (j + 1 < L) {
+        f32x4* dst = reinterpret_cast<f32x4*>(hist + ((size_t)j * 64 + lane) * 4 * HT);
+#pragma unroll
+        for (int t = 0; t < HT; ++t) dst[t] = f32x4{h[t][0], h[t][1], h[t][2], h[t][3]};
+      }
+    }
+
+    // ---- head forward + loss gradient w.r.t. the head outputs
+    f32x4 pre1[HT], lg;
+    float y[HT][4];
+    gru_head<HT>(a.w, k, H, A, h, pre1, y, lg, g, i);
+    f32x4 dlg;
+    if constexpr (KIND == kGruValue) {
+      const float d = lg[0] - in.w;  // V - R
+      acc.st[0] += (ok && g == 0) ? d * d : 0.f;
+      dlg = f32x4{(ok && g == 0) ? 2.f * a.scale * d : 0.f, 0.f, 0.f, 0.f};
+    } else {
+      dlg = ppo_dz<KIND == kGruBernoulli ? 0 : 1, false, KIND == kGruBernoulli>(a, lg, in.act, in.lo, in.w, ok, g,
+                                                                                  acc.st[0], acc.st[1]);
+    }
+
+    // ---- head backward.  dW2 += dlg y^T, db2, dy = W2^T dlg, dpre1 = dy [pre1 > 0]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      sc[(4 * g + r) * 16 + pcol(i)] = dlg[r];
+      acc.b2[r] += dlg[r];
+#pragma unroll
+      for (int t = 0; t < HT; ++t) sc[(16 + 16 * t + 4 * g + r) * 16 + pcol(i)] = y[t][r];
+    }
+    lds_order();
+    {
+      const f32x4 af = sc_frag(sc, i, g);
+#pragma unroll
+      for (int U = 0; U < HT; ++U) {
+        const f32x4 bf = sc_frag(sc, 16 + 16 * U + i, g);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) acc.w2[U] = mfma4(af[s4], bf[s4], acc.w2[U]);
+      }
+    }
+    float dpre1[HT][4];
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      f32x4 dy = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int o = 4 * g + s4, col = 16 * t + i;
+        const float wv = (o < A && col < H) ? W2[(size_t)o * H + col] : 0.f;
+        dy = mfma4(wv, dlg[s4], dy);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dpre1[t][r] = pre1[t][r] > 0.f ? dy[r] : 0.f;
+        acc.b1[t][r] += dpre1[t][r];
+      }
+    }
+    lds_order();
+    // dW1 += dpre1 h_L^T, dh_L = W1^T dpre1
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        sc[(16 * t + 4 * g + r) * 16 + pcol(i)] = dpre1[t][r];
+        sc[(HW + 16 * t + 4 * g + r) * 16 + pcol(i)] = h[t][r];
+      }
+    lds_order();
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      const f32x4 af = sc_frag(sc, 16 * t + i, g);
+#pragma unroll
+      for (int U = 0; U < HT; ++U) {
+        const f32x4 bf = sc_frag(sc, HW + 16 * U + i, g);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) acc.w1[t][U] = mfma4(af[s4], bf[s4], acc.w1[t][U]);
+      }
+    }
+    float gcur[HT][4];
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      f32x4 dh = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < HT; ++q)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int rowk = 16 * q + 4 * g + s4, col = 16 * t + i;
+          const float wv = (rowk < H && col < H) ? W1[(size_t)rowk * H + col] : 0.f;
+          dh = mfma4(wv, dpre1[q][s4], dh);
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gcur[t][r] = dh[r];
+    }
+    lds_order();
+
+    // ---- backpropagation through time, j = L-1 .. 0 (gates recomputed from h_{j-1})
+    for (int j = L - 1; j >= 0; --j) {
+      float hp[HT][4];
+      if (j == 0) {
+#pragma unroll
+        for (int t = 0; t < HT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hp[t][r] = 0.f;
+      } else {
+        const f32x4* src = reinterpret_cast<const f32x4*>(hist + ((size_t)(j - 1) * 64 + lane) * 4 * HT);
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+          const f32x4 v = src[t];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hp[t][r] = v[r];
+        }
+      }
+      const bool zero = j < pad;
+      const size_t xoff = row_of(j);
+      float x[IT][4];
+      load_x<IT>(x, a.obs, xoff, a.obs_floats, N * F, F, g, i, ok, zero);
+      f32x4 rz[2 * HT], ni[HT], nh[HT];
+      gru_preact<HT, IT, false>(wimg, whh_s, x, hp, bhn, rz, ni, nh, g, i, j == 0);
+      float drp[HT][4], dzp[HT][4], dnp[HT][4], dghn[HT][4], gz[HT][4];
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float rr = sigmoidf_(rz[t][r]), zz = sigmoidf_(rz[HT + t][r]);
+          const float nn = tanhf_(ni[t][r] + rr * nh[t][r]);
+          const float gv = gcur[t][r];
+          const float dn = gv * (1.f - zz), dz = gv * (hp[t][r] - nn);
+          dnp[t][r] = dn * (1.f - nn * nn);
+          dghn[t][r] = dnp[t][r] * rr;
+          drp[t][r] = dnp[t][r] * nh[t][r] * rr * (1.f - rr);
+          dzp[t][r] = dz * zz * (1.f - zz);
+          gz[t][r] = gv * zz;
+          acc.bhn[t][r] += dghn[t][r];
+        }
+      // dgi (r, z, n_in rows) and h_{j-1} to the scratch
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int u = 16 * t + 4 * g + r, c = pcol(i);
+          sc[u * 16 + c] = drp[t][r];
+          sc[(HW + u) * 16 + c] = dzp[t][r];
+          sc[(2 * HW + u) * 16 + c] = dnp[t][r];
+          sc[(R3 + u) * 16 + c] = hp[t][r];
+        }
+      lds_order();
+      // dW_ih += dgi x^T: x^T operand sample-on-k from global (sample 4 s4 + g, input 16U + i)
+      {
+        float xt[IT][4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const int ee = 4 * s4 + g;
+          const bool eok = e0 + ee < E;
+          const int64_t rest = (a.obs_floats - (int64_t)xoff) * 4;
+          const uint32_t nbytes = zero || rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
+          const __amdgpu_buffer_rsrc_t rsrc =
+              __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.obs + xoff), 0, nbytes, 0x00020000);
+          const uint32_t vb = eok ? (uint32_t)(ee * N * F) * 4u : 0x80000000u;
+#pragma unroll
+          for (int U = 0; U < IT; ++U) {
+            const int col = 16 * U + i;
+            const float v = uf(__builtin_amdgcn_raw_buffer_load_b32(rsrc, vb + 4u * (uint32_t)col, 0, 0));
+            xt[U][s4] = col < F ? v : col == F ? 1.f : 0.f;
+          }
+        }
+#pragma unroll
+        for (int T = 0; T < 3 * HT; ++T) {
+          const f32x4 af = sc_frag(sc, 16 * T + i, g);
+#pragma unroll
+          for (int U = 0; U < IT; ++U)
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) acc.wih[T][U] = mfma4(af[s4], xt[U][s4], acc.wih[T][U]);
+        }
+      }
+      lds_order();
+      // n rows of dgh = dn_pre * r
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sc[(2 * HW + 16 * t + 4 * g + r) * 16 + pcol(i)] = dghn[t][r];
+      lds_order();
+      // dW_hh += dgh h_{j-1}^T, accumulated in LDS by the four waves
+#pragma unroll
+      for (int T = 0; T < 3 * HT; ++T) {
+        const f32x4 af = sc_frag(sc, 16 * T + i, g);
+#pragma unroll
+        for (int U = 0; U < HT; ++U) {
+          const f32x4 bf = sc_frag(sc, R3 + 16 * U + i, g);
+          f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) d = mfma4(af[s4], bf[s4], d);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) atomicAdd(&dwhh_s[(16 * T + 4 * g + r) * HW + 16 * U + i], d[r]);
+        }
+      }
+      // dh_{j-1} = g z + W_hh^T dgh
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        f32x4 dh = {gz[t][0], gz[t][1], gz[t][2], gz[t][3]};
+#pragma unroll
+        for (int T = 0; T < 3 * HT; ++T)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const float wv = whh_s[swz<HW>(16 * T + 4 * g + s4, 16 * t + i)];
+            const float bv = T < HT ? drp[T][s4] : T < 2 * HT ? dzp[T - HT][s4] : dghn[T - 2 * HT][s4];
+            dh = mfma4(wv, bv, dh);
+          }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gcur[t][r] = dh[r];
+      }
+      lds_order();
+    }
+  }
+
+  // ---- cross-wave sum of the register partials (fixed order, through the scratch), then the
+  // workgroup's partial: registers of wave 0 + the LDS dW_hh
+  constexpr int NV = GruAcc<HT, IT>::NV;
+  float* red = &scr[0][0];
+  static_assert(NV * 64 <= 4 * SROWS * 16, "reduction buffer");
+#pragma unroll 1
+  for (int w = 1; w < 4; ++w) {
+    __syncthreads();
+    if (wave == w) acc.each([&](int v, float& x) { red[v * 64 + lane] = x; });
+    __syncthreads();
+    if (wave == 0) acc.each([&](int v, float& x) { x += red[v * 64 + lane]; });
+  }
+  __syncthreads();
+  const GruOff o(H, F, A);
+  float* part = a.partial + ((size_t)blockIdx.y * N + k) * a.P;
+  for (int idx = tid; idx < R3 * HW; idx += blockDim.x) {
+    const int R = idx / HW, c = idx - R * HW, G = R / HW, u = R - G * HW;
+    if (u < H && c < H) part[o.whh + (G * H + u) * H + c] = dwhh_s[idx];
+  }
+  if (wave == 0) {
+#pragma unroll
+    for (int T = 0; T < 3 * HT; ++T)
+#pragma unroll
+      for (int U = 0; U < IT; ++U)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int R = 16 * T + 4 * g + r, G = R / HW, u = R - G * HW, c = 16 * U + i;
+          if (u >= H) continue;
+          const float v = acc.wih[T][U][r];
+          if (c < F) part[o.wih + (G * H + u) * F + c] = v;
+          else if (c == F) {
+            part[o.bih + G * H + u] = v;
+            if (G < 2) part[o.bhh + G * H + u] = v;  // b_hr / b_hz enter exactly like b_ir / b_iz
+          }
+        }
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int U = 0; U < HT; ++U)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 16 * t + 4 * g + r, col = 16 * U + i;
+          if (row < H && col < H) part[o.w1 + row * H + col] = acc.w1[t][U][r];
+        }
+#pragma unroll
+    for (int U = 0; U < HT; ++U)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = 4 * g + r, col = 16 * U + i;
+        if (row < A && col < H) part[o.w2 + row * H + col] = acc.w2[U][r];
+      }
+    // bias sums: the 16 sample lanes of each row group
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int u = 16 * t + 4 * g + r;
+        const float sb1 = row_sum16(acc.b1[t][r]), sbn = row_sum16(acc.bhn[t][r]);
+        if (i == 0 && u < H) {
+          part[o.b1 + u] = sb1;
+          part[o.bhh + 2 * H + u] = sbn;
+        }
+      }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float sb2 = row_sum16(acc.b2[r]);
+      if (i == 0 && 4 * g + r < A) part[o.b2 + 4 * g + r] = sb2;
+    }
+    float s0 = acc.st[0], s1 = acc.st[1];
+    s0 = group_sum(row_sum16(s0));
+    s1 = group_sum(row_sum16(s1));
+    if (lane == 0) {
+      part[o.st] = s0;
+      part[o.st + 1] = s1;
+    }
+  }
+}
+
+// The input images of all agents, unswizzled: img[k][R][c] (gate row R of the padded layout, input
+// column c; column F = the biases of gru_common.h), zero outside the real rows / columns.
+__global__ void gru_wih_image_kernel(GruW w, int N, int H, int F, int HW, int IW, float* img) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)N * 3 * HW * IW) return;
+  const int k = (int)(idx / (3 * HW * IW)), rem = (int)(idx - (int64_t)k * 3 * HW * IW);
+  const int R = rem / IW, c = rem - R * IW, G = R / HW, u = R - G * HW, src = G * H + u;
+  float v = 0.f;
+  if (u < H) {
+    if (c < F) v = w.w_ih[((size_t)k * 3 * H + src) * F + c];
+    else if (c == F) v = G < 2 ? w.b_ih[(size_t)k * 3 * H + src] + w.b_hh[(size_t)k * 3 * H + src]
+                               : w.b_ih[(size_t)k * 3 * H + src];
+  }
+  img[idx] = v;
+}
+
+// Fixed-order sum of the G workgroup partials -> the gradient tensors (+ loss sums).
+__global__ void gru_reduce_kernel(const float* __restrict__ partial, int G, int N, int P, int H, int F, int A,
+                                  float* gwih, float* gwhh, float* gbih, float* gbhh, float* gw1, float* gb1,
+                                  float* gw2, float* gb2, float* stats) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)N * P) return;
+  const int k = (int)(idx / P), p = (int)(idx - (int64_t)k * P);
+  float s = 0.f;
+  for (int b = 0; b < G; ++b) s += partial[((size_t)b * N + k) * P + p];
+  const GruOff o(H, F, A);
+  if (p < o.whh) gwih[(size_t)k * 3 * H * F + p] = s;
+  else if (p < o.bih) gwhh[(size_t)k * 3 * H * H + (p - o.whh)] = s;
+  else if (p < o.bhh) gbih[(size_t)k * 3 * H + (p - o.bih)] = s;
+  else if (p < o.w1) gbhh[(size_t)k * 3 * H + (p - o.bhh)] = s;
+  else if (p < o.b1) gw1[(size_t)k * H * H + (p - o.w1)] = s;
+  else if (p < o.w2) gb1[(size_t)k * H + (p - o.b1)] = s;
+  else if (p < o.b2) gw2[(size_t)k * A * H + (p - o.w2)] = s;
+  else if (p < o.st) gb2[(size_t)k * A + (p - o.b2)] = s;
+  else if (stats) stats[(size_t)k * 2 + (p - o.st)] = s;
+}
+
+}  // namespace d2d
+
+using namespace d2d;
+
+template <int HT, int IT, int KIND>
+static void launch_policy_mode(const GruArgs& a, dim3 grid, hipStream_t s) {
+  if (KIND == kGruValue || a.ep.forced == nullptr) {
+    if (KIND != kGruValue && a.ep.deterministic)
+      hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeDeterministic>), grid, dim3(512), 0, s, a);
+    else
+      hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeSample>), grid, dim3(512), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeForced>), grid, dim3(512), 0, s, a);
+  }
+}
+
+template <int HT, int IT>
+static void launch_policy_kind(const GruArgs& a, dim3 grid, hipStream_t s) {
+  if (a.kind == kGruBernoulli) launch_policy_mode<HT, IT, kGruBernoulli>(a, grid, s);
+  else if (a.kind == kGruCategorical) launch_policy_mode<HT, IT, kGruCategorical>(a, grid, s);
+  else launch_policy_mode<HT, IT, kGruValue>(a, grid, s);
+}
+
+template <int HT>
+static void launch_policy_it(const GruArgs& a, dim3 grid, hipStream_t s) {
+  if (a.F + 1 <= 16) launch_policy_kind<HT, 1>(a, grid, s);
+  else if (a.F + 1 <= 32) launch_policy_kind<HT, 2>(a, grid, s);
+  else launch_policy_kind<HT, 4>(a, grid, s);
+}
+
+static int check_gru_desc(const d2d_gru_desc* d) {
+  if (!d || !d->w_ih || !d->w_hh || !d->b_ih || !d->b_hh || !d->w1 || !d->b1 || !d->w2 || !d->b2) {
+    d2d_set_error("d2d_gru: NULL weight");
+    return D2D_EINVAL;
+  }
+  if (d->n_agents < 0 || d->n_envs < 0) { d2d_set_error("negative size"); return D2D_EINVAL; }
+  if (d->hidden < 1 || d->hidden > 64) { d2d_set_error("hidden=%d outside [1,64]", d->hidden); return D2D_EUNSUPPORTED; }
+  if (d->obs_dim < 1 || d->obs_dim + 1 > 64) { d2d_set_error("obs_dim=%d outside [1,63]", d->obs_dim); return D2D_EUNSUPPORTED; }
+  if (d->kind < 0 || d->kind > 2) { d2d_set_error("kind=%d outside [0,2]", d->kind); return D2D_EINVAL; }
+  if (d->kind != 2 && (d->n_out < 1 || d->n_out > 16)) { d2d_set_error("n_out=%d outside [1,16]", d->n_out); return D2D_EUNSUPPORTED; }
+  if (d->history_len < 1 || d->episode_length < 1) { d2d_set_error("history_len / episode_length < 1"); return D2D_EINVAL; }
+  return D2D_OK;
+}
+
+static GruArgs make_gru_args(const d2d_gru_desc* d, int T, const float* obs) {
+  GruArgs a{};
+  a.T = T; a.E = d->n_envs; a.N = d->n_agents; a.F = d->obs_dim; a.H = d->hidden;
+  a.A = d->kind == 2 ? 1 : d->n_out; a.kind = d->kind;
+  a.L = d->history_len; a.ep_len = d->episode_length;
+  a.env_tiles = (a.E + 15) / 16;
+  a.w = {d->w_ih, d->w_hh, d->b_ih, d->b_hh, d->w1, d->b1, d->w2, d->b2};
+  a.obs = obs;
+  a.obs_floats = (int64_t)T * a.E * a.N * a.F;
+  a.inv_A = 1.f / (float)a.A;
+  a.mask_bytes = a.A <= 8 ? 1 : a.A <= 16 ? 2 : 4;
+  return a;
+}
+
+extern "C" int d2d_policy_gru(const d2d_gru_desc* d, int32_t T, const float* obs, int32_t slot0, int32_t n_slots,
+                              int32_t padded, const void* forced, uint32_t rng_step, int32_t deterministic,
+                              void* actions, float* out, void* stream) {
+  int rc = check_gru_desc(d);
+  if (rc) return rc;
+  if (!obs || !out || (d->kind != 2 && !actions)) { d2d_set_error("d2d_policy_gru: NULL buffer"); return D2D_EINVAL; }
+  if (T < 1 || slot0 < 0 || n_slots < 0 || slot0 + n_slots > T) {
+    d2d_set_error("d2d_policy_gru: slots [%d, %d) outside the %d-slot buffer", slot0, slot0 + n_slots, T);
+    return D2D_EINVAL;
+  }
+  if (T % d->episode_length != 0 && slot0 + n_slots > T - T % d->episode_length + d->episode_length) {
+    d2d_set_error("d2d_policy_gru: buffer is not whole episodes");
+    return D2D_EINVAL;
+  }
+  GruArgs a = make_gru_args(d, T, obs);
+  a.slot0 = slot0; a.n_slots = n_slots; a.padded = padded ? 1 : 0;
+  MlpArgs& ep = a.ep;
+  ep.E = n_slots * a.E; ep.N = a.N; ep.F = a.F; ep.H = a.H; ep.A = a.A; ep.kind = d->kind == 0 ? 0 : 1;
+  ep.deterministic = deterministic ? 1 : 0; ep.inv_A = a.inv_A; ep.rng_step = rng_step; ep.rng_off = d->rng_offset;
+  ep.seed = d->seed; ep.env_base = d->env_base; ep.forced = forced; ep.act_out = actions; ep.logp_out = out;
+  ep.value_out = nullptr; ep.mask_bytes = a.mask_bytes;
+  a.value_out = out;
+  if (a.N == 0 || a.E == 0 || n_slots == 0) return D2D_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int64_t tiles = (int64_t)n_slots * a.env_tiles;
+  // about 2 workgroups of 8 waves per CU over the whole grid, at least one tile per wave
+  const int gy = (int)std::max<int64_t>(1, std::min<int64_t>((512 + a.N - 1) / a.N, (tiles + 7) / 8));
+  dim3 grid(a.N, gy);
+  const int ht = (a.H + 15) / 16;
+  if (ht <= 1) launch_policy_it<1>(a, grid, s);
+  else if (ht <= 2) launch_policy_it<2>(a, grid, s);
+  else launch_policy_it<4>(a, grid, s);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
+// ------------------------------------------------------------------------------------ grad ABI
+static int gru_grad_blocks(int N, int64_t n_tiles) {
+  // about one workgroup (4 waves, 160 KB LDS) per CU over the grid, at least one tile per wave
+  return (int)std::max<int64_t>(1, std::min<int64_t>((256 + N - 1) / N, (n_tiles + 3) / 4));
+}
+
+extern "C" int64_t d2d_gru_grad_workspace(const d2d_gru_desc* d, int32_t T) {
+  if (!d || d->n_agents <= 0 || T <= 0 || d->n_envs <= 0 || d->hidden < 1 || d->history_len < 1) return 0;
+  const int A = d->kind == 2 ? 1 : d->n_out, H = d->hidden, ht = H <= 16 ? 1 : H <= 32 ? 2 : 4;
+  const int64_t tiles = (int64_t)T * ((d->n_envs + 15) / 16);
+  const int G = gru_grad_blocks(d->n_agents, tiles);
+  const GruOff o(H, d->obs_dim, A);
+  const int64_t partial = (int64_t)G * d->n_agents * o.P;
+  const int64_t hist = (int64_t)G * d->n_agents * 4 * d->history_len * 64 * 4 * ht;
+  const int64_t img = (int64_t)d->n_agents * 3 * 16 * ht * 32;
+  return partial + hist + img;
+}
+
+template <int HT, int IT>
+static void launch_grad_kind(const GruArgs& a, dim3 grid, hipStream_t s) {
+  if (a.kind == kGruBernoulli) hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruBernoulli>), grid, dim3(256), 0, s, a);
+  else if (a.kind == kGruCategorical)
+    hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruCategorical>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruValue>), grid, dim3(256), 0, s, a);
+}
+
+extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const float* obs, const void* actions,
+                            const float* logp_old, const int64_t* logp_strides, const float* weight,
+                            const int64_t* weight_strides, float clip, float beta, float scale, float* g_w_ih,
+                            float* g_w_hh, float* g_b_ih, float* g_b_hh, float* g_w1, float* g_b1, float* g_w2,
+                            float* g_b2, float* stats, float* workspace, int64_t workspace_floats, void* stream) {
+  int rc = check_gru_desc(d);
+  if (rc) return rc;
+  if (d->obs_dim + 1 > 32) { d2d_set_error("d2d_gru_grad: obs_dim=%d > 31", d->obs_dim); return D2D_EUNSUPPORTED; }
+  if (!obs || !weight || !weight_strides || !g_w_ih || !g_w_hh || !g_b_ih || !g_b_hh || !g_w1 || !g_b1 || !g_w2 ||
+      !g_b2 || !workspace || (d->kind != 2 && (!actions || !logp_old || !logp_strides))) {
+    d2d_set_error("d2d_gru_grad: NULL argument");
+    return D2D_EINVAL;
+  }
+  if (T < 0 || (T > 0 && T % d->episode_length != 0)) {
+    d2d_set_error("d2d_gru_grad: T=%d is not a whole number of %d-slot episodes", T, d->episode_length);
+    return D2D_EINVAL;
+  }
+  const int64_t need = d2d_gru_grad_workspace(d, T);
+  if (workspace_floats < need) {
+    d2d_set_error("workspace %lld < %lld floats", (long long)workspace_floats, (long long)need);
+    return D2D_EINVAL;
+  }
+  GruArgs a = make_gru_args(d, T, obs);
+  a.actions = actions; a.logp_old = logp_old; a.weight = weight;
+  for (int q = 0; q < 3; ++q) {
+    a.lo_st[q] = logp_strides ? logp_strides[q] : 0;
+    a.w_st[q] = weight_strides[q];
+  }
+  a.clip_lo = 1.f - clip; a.clip_hi = 1.f + clip; a.beta = beta; a.scale = scale;
+  const int64_t tiles = (int64_t)T * a.env_tiles;
+  a.G = gru_grad_blocks(a.N, tiles);
+  const GruOff o(a.H, a.F, a.A);
+  a.P = o.P;
+  a.partial = workspace;
+  a.hist = workspace + (int64_t)a.G * a.N * a.P;
+  const int ht = (a.H + 15) / 16, htp = ht <= 1 ? 1 : ht <= 2 ? 2 : 4, itp = a.F + 1 <= 16 ? 1 : 2;
+  a.wimg = a.hist + (int64_t)a.G * a.N * 4 * a.L * 64 * 4 * htp;
+  if (a.N == 0) return D2D_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  {
+    const int64_t n = (int64_t)a.N * 3 * 16 * htp * 16 * itp;
+    hipLaunchKernelGGL(gru_wih_image_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.w, a.N, a.H, a.F,
+                       16 * htp, 16 * itp, a.wimg);
+  }
+  if (tiles == 0) {
+    D2D_CHECK_HIP(hipMemsetAsync(workspace, 0, sizeof(float) * (size_t)a.N * a.P, s));
+    a.G = 1;
+  } else {
+    dim3 grid(a.N, a.G);
+    const bool it1 = itp == 1;
+    if (ht <= 1) { if (it1) launch_grad_kind<1, 1>(a, grid, s); else launch_grad_kind<1, 2>(a, grid, s); }
+    else if (ht <= 2) { if (it1) launch_grad_kind<2, 1>(a, grid, s); else launch_grad_kind<2, 2>(a, grid, s); }
+    else { if (it1) launch_grad_kind<4, 1>(a, grid, s); else launch_grad_kind<4, 2>(a, grid, s); }
+    D2D_CHECK_HIP(hipGetLastError());
+  }
+  const int64_t n = (int64_t)a.N * a.P;
+  hipLaunchKernelGGL(gru_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.partial, a.G, a.N, a.P,
+                     a.H, a.F, a.A, g_w_ih, g_w_hh, g_b_ih, g_b_hh, g_w1, g_b1, g_w2, g_b2, stats);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}

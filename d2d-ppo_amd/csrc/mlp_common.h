@@ -139,6 +139,21 @@ __device__ __forceinline__ f32x4 mfma_split(const Parts& w, const Parts& x, bool
   return acc;
 }
 
+// Sum over the 16 lanes of a row (lanes with equal g), result in every lane of the row.
+__device__ __forceinline__ float row_sum16(float v) {
+  v += uf((uint32_t)__builtin_amdgcn_update_dpp(0, (int)fu(v), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
+  v += uf((uint32_t)__builtin_amdgcn_update_dpp(0, (int)fu(v), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
+  v += uf((uint32_t)__builtin_amdgcn_update_dpp(0, (int)fu(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v += uf((uint32_t)__builtin_amdgcn_update_dpp(0, (int)fu(v), 0x140, 0xF, 0xF, false));  // row_mirror
+  return v;
+}
+
+// order a wave's LDS writes before its following LDS reads of other lanes' data
+__device__ __forceinline__ void lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int N_OUTSTANDING>
 __device__ __forceinline__ void wait_vmem() {
   static_assert(N_OUTSTANDING < 64, "vmcnt field is 6 bits");

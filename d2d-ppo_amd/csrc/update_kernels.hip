@@ -38,7 +38,7 @@
 #include <cmath>
 #include <type_traits>
 
-#include "mlp_common.h"
+#include "ppo_epilogue.h"
 
 #ifndef D2D_UPD_ABLATE
 #define D2D_UPD_ABLATE 0  // != 0 only in tools/gpu/ablate_update.py's timing builds
@@ -65,7 +65,6 @@ struct UpdArgs {
   float* partial;                   // [G][N][P]
 };
 
-constexpr float kEps = 1.1920928955078125e-07f;  // torch.finfo(float32).eps (probs_to_logits clamp)
 
 // three bf16 parts of 4 floats as 2 + 2 + 2 dwords
 struct Parts4 {
@@ -117,15 +116,6 @@ __device__ __forceinline__ bf16x8 hi_frag(const float (&v)[8]) {
 #pragma unroll
   for (int q = 0; q < 4; ++q) u[q] = pack_hi(v[2 * q], v[2 * q + 1]);
   return as_frag(u);
-}
-
-// Sum over the 16 lanes of a row (lanes with equal g), result in every lane of the row.
-__device__ __forceinline__ float row_sum16(float v) {
-  v += uf((uint32_t)__builtin_amdgcn_update_dpp(0, (int)fu(v), 0xB1, 0xF, 0xF, false));   // quad_perm 1,0,3,2
-  v += uf((uint32_t)__builtin_amdgcn_update_dpp(0, (int)fu(v), 0x4E, 0xF, 0xF, false));   // quad_perm 2,3,0,1
-  v += uf((uint32_t)__builtin_amdgcn_update_dpp(0, (int)fu(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
-  v += uf((uint32_t)__builtin_amdgcn_update_dpp(0, (int)fu(v), 0x140, 0xF, 0xF, false));  // row_mirror
-  return v;
 }
 
 __device__ __forceinline__ float ld_st(const float* base, const int64_t (&st)[3], int t, int e, int k) {
@@ -185,129 +175,6 @@ __device__ __forceinline__ void load_actor_in(ActorIn<KC, PAIR>& in, const UpdAr
   }
 }
 
-// dL/dz for one epilogue pass.  Lane (g, i): sample i of its half, actions 4 ga + r (HALF: the
-// two 32-lane halves are independent tiles, ga = g & 1; else ga = g).
-// Bernoulli (KIND 0, ippo.py:157-160 + 185-189, quirk Q6: softmax probs as Bernoulli probs):
-//   logp = mean_c log_prob(a_c) with torch's clamp(p, eps, 1-eps); entropy = mean_c
-//   BCEWithLogits(logit(pc), p) = -p log pc - (1-p) log(1-pc).
-// Categorical (KIND 1): Categorical(probs) renormalises q = p / sum p; logp = log clamp(q_a);
-//   entropy = -sum q log clamp(q).
-// Surrogate -min(r W, clamp(r) W) with torch.min's tie rule (each side gets half the gradient,
-// so inside [1-eps, 1+eps] the slope is r W) and clamp passing the gradient inclusively.
-template <int KIND, bool HALF>
-__device__ __forceinline__ f32x4 ppo_dz(const UpdArgs& a, f32x4 z, uint32_t act, float lo, float W, bool ok, int ga,
-                                        float& surr_acc, float& ent_acc) {
-  const int A = a.A;
-  bool valid[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) valid[r] = 4 * ga + r < A;
-  float mx = -INFINITY;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-    if (valid[r]) mx = fmaxf(mx, z[r]);
-  mx = group_max<HALF>(mx);
-  float ex[4], sum = 0.f;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    ex[r] = valid[r] ? __expf(z[r] - mx) : 0.f;
-    sum += ex[r];
-  }
-  sum = group_sum<HALF>(sum);
-  const float inv = __builtin_amdgcn_rcpf(sum);  // v_rcp_f32, 1 ulp (IEEE division: ~10 VALU + branches)
-  float p[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) p[r] = ex[r] * inv;
-  float gr[4], dsur[4];
-  float logp, ent;
-  if constexpr (KIND == 0) {
-    const uint32_t bits = act >> (4 * ga);
-    float lsum = 0.f, esum = 0.f, logit[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float pc = fminf(fmaxf(p[r], kEps), 1.f - kEps);
-      const bool inside = p[r] >= kEps && p[r] <= 1.f - kEps;
-      const float l1 = __logf(pc), l0 = __logf(1.f - pc);
-      const bool bit = (bits >> r) & 1u;
-      lsum += valid[r] ? (bit ? l1 : l0) : 0.f;
-      esum += valid[r] ? -(p[r] * l1 + (1.f - p[r]) * l0) : 0.f;
-      logit[r] = l1 - l0;
-      // d log_prob / dp: 1/pc or -1/(1-pc) -- one reciprocal of the selected denominator
-      const float rden = __builtin_amdgcn_rcpf(bit ? pc : 1.f - pc);
-      dsur[r] = (valid[r] && inside) ? (bit ? rden : -rden) : 0.f;
-    }
-    logp = group_sum<HALF>(lsum) * a.inv_A;
-    ent = group_sum<HALF>(esum) * a.inv_A;
-    const float ratio = __expf(logp - lo);
-    const float cr = fminf(fmaxf(ratio, a.clip_lo), a.clip_hi);
-    const float s1 = ratio * W, s2 = cr * W;
-    const bool gate = (ratio >= a.clip_lo && ratio <= a.clip_hi) || s1 < s2;
-    const float coef = gate ? -a.scale * ratio * W * a.inv_A : 0.f;
-    const float eb = a.beta * a.scale * a.inv_A;  // d(-beta*mean ent)/dp_c = +beta * logit_c / A / B
-#pragma unroll
-    for (int r = 0; r < 4; ++r) gr[r] = valid[r] ? coef * dsur[r] + eb * logit[r] : 0.f;
-    surr_acc += (ok && ga == 0) ? fminf(s1, s2) : 0.f;
-    ent_acc += (ok && ga == 0) ? ent : 0.f;
-    float dot = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dot += p[r] * gr[r];
-    dot = group_sum<HALF>(dot);
-    f32x4 dz;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dz[r] = (ok && valid[r]) ? p[r] * (gr[r] - dot) : 0.f;
-    return dz;
-  } else {
-    const int aid = (int)act;
-    float psum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) psum += p[r];
-    psum = group_sum<HALF>(psum);
-    const float ipsum = __builtin_amdgcn_rcpf(psum);
-    float q[4], lsel = 0.f, esum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      q[r] = p[r] * ipsum;
-      const float qc = fminf(fmaxf(q[r], kEps), 1.f - kEps);
-      const bool inside = q[r] >= kEps && q[r] <= 1.f - kEps;
-      const float lq = __logf(qc);
-      const bool chosen = valid[r] && 4 * ga + r == aid;
-      lsel += chosen ? lq : 0.f;
-      esum += valid[r] ? q[r] * lq : 0.f;
-      const float iqc = __builtin_amdgcn_rcpf(qc);
-      dsur[r] = (chosen && inside) ? iqc : 0.f;
-      // d(-beta * ent)/dq = beta * (log qc + q * [inside] / qc)
-      gr[r] = valid[r] ? (lq + (inside ? q[r] * iqc : 0.f)) : 0.f;
-    }
-    logp = group_sum<HALF>(lsel);
-    ent = -group_sum<HALF>(esum);
-    const float ratio = __expf(logp - lo);
-    const float cr = fminf(fmaxf(ratio, a.clip_lo), a.clip_hi);
-    const float s1 = ratio * W, s2 = cr * W;
-    const bool gate = (ratio >= a.clip_lo && ratio <= a.clip_hi) || s1 < s2;
-    const float coef = gate ? -a.scale * ratio * W : 0.f;
-    const float eb = a.beta * a.scale;
-    float gq = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      gr[r] = coef * dsur[r] + eb * gr[r];  // dL/dq
-      gq += gr[r] * q[r];
-    }
-    gq = group_sum<HALF>(gq);
-    float dp[4], dot = 0.f;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      dp[r] = valid[r] ? (gr[r] - gq) * ipsum : 0.f;  // through q = p / sum p
-      dot += p[r] * dp[r];
-    }
-    dot = group_sum<HALF>(dot);
-    surr_acc += (ok && ga == 0) ? fminf(s1, s2) : 0.f;
-    ent_acc += (ok && ga == 0) ? ent : 0.f;
-    f32x4 dz;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) dz[r] = (ok && valid[r]) ? p[r] * (dp[r] - dot) : 0.f;
-    return dz;
-  }
-}
-
 // Deterministic cross-wave sum of NV per-lane accumulators into wave 0's registers.
 template <int NV>
 __device__ __forceinline__ void reduce_waves(float (&acc)[NV], float* red, int wave, int lane) {
@@ -336,10 +203,6 @@ __device__ __forceinline__ void lds_row(float (&v)[8], const float (*xw)[XS], in
   }
 }
 
-__device__ __forceinline__ void lds_order() {
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
 
 // ------------------------------------------------------------------------- actor gradients
 // KC = input chunks of 32 (F + 1 <= 32 KC), HT = hidden tiles of 16 (H <= 16 HT), A <= 16;

@@ -36,7 +36,7 @@ def refuse_ablation(what):
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 3
+ABI_VERSION = 4
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
 
@@ -71,6 +71,14 @@ class MlpDesc(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("env_base", ctypes.c_uint64), ("rng_offset", _p)]
 
 
+class GruDesc(ctypes.Structure):
+    _fields_ = [("n_agents", ctypes.c_int32), ("n_envs", ctypes.c_int32), ("obs_dim", ctypes.c_int32),
+                ("hidden", ctypes.c_int32), ("n_out", ctypes.c_int32), ("kind", ctypes.c_int32),
+                ("history_len", ctypes.c_int32), ("episode_length", ctypes.c_int32),
+                ("w_ih", _p), ("w_hh", _p), ("b_ih", _p), ("b_hh", _p), ("w1", _p), ("b1", _p), ("w2", _p), ("b2", _p),
+                ("seed", ctypes.c_uint64), ("env_base", ctypes.c_uint64), ("rng_offset", _p)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "d2d_env_reset": (ctypes.c_int, [ctypes.POINTER(EnvDesc), ctypes.POINTER(EnvState), ctypes.POINTER(EnvReplay),
@@ -102,6 +110,12 @@ _SIGS = {
                                            ctypes.c_int64, _p]),
     "d2d_ppo_critic_grad": (ctypes.c_int, [ctypes.POINTER(MlpDesc), ctypes.c_int32, _p, _p, _p, ctypes.c_float,
                                             _p, _p, _p, _p, _p, _p, ctypes.c_int64, _p]),
+    "d2d_policy_gru": (ctypes.c_int, [ctypes.POINTER(GruDesc), ctypes.c_int32, _p, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_int32, _p, ctypes.c_uint32, ctypes.c_int32, _p, _p, _p]),
+    "d2d_gru_grad_workspace": (ctypes.c_int64, [ctypes.POINTER(GruDesc), ctypes.c_int32]),
+    "d2d_gru_grad": (ctypes.c_int, [ctypes.POINTER(GruDesc), ctypes.c_int32, _p, _p, _p, _p, _p, _p, ctypes.c_float,
+                                     ctypes.c_float, ctypes.c_float, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,
+                                     ctypes.c_int64, _p]),
     "d2d_last_error": (ctypes.c_char_p, []),
     "d2d_abi_version": (ctypes.c_int, []),
 }

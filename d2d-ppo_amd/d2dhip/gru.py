@@ -1,0 +1,103 @@
+"""Python entry to the GRU window-policy kernels (C ABI d2d_policy_gru / d2d_gru_grad,
+csrc/gru_kernels.hip): the reference's RNN module (algorithms/ippo.py:14-51 == d2d_ppo.py:24-59)
+for every agent at once, windows rebuilt in-kernel from the rollout buffer."""
+import ctypes
+
+import torch
+
+from . import _lib
+
+KIND = {"sigmoid": 0, "softmax": 1, None: 2}
+
+
+def desc(params, n_envs, kind, history_len, episode_length, seed=0, env_base=0, rng_offset=None):
+    """d2d_gru_desc of agent-stacked RNN params (StackedNets kind 'rnn': w_ih, w_hh, b_ih, b_hh, w1, b1, w2, b2)."""
+    p = params
+    N, threeH, F = p["w_ih"].shape
+    H = threeH // 3
+    A = p["w2"].shape[1]
+    for t in p.values():
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("GRU params must be contiguous float32")
+    d = _lib.GruDesc(N, int(n_envs), F, H, A, int(kind), int(history_len), int(episode_length),
+                     *(p[n].data_ptr() for n in ("w_ih", "w_hh", "b_ih", "b_hh", "w1", "b1", "w2", "b2")),
+                     int(seed) & 0xFFFFFFFFFFFFFFFF, int(env_base), None if rng_offset is None else rng_offset)
+    return d
+
+
+def policy(params, obs, kind, history_len, episode_length, slot0, n_slots, padded=False, forced=None, rng_step=0,
+           deterministic=False, seed=0, env_base=0, rng_offset=None, actions_out=None, out=None):
+    """obs [T][E][N][F] (the rollout buffer).  kind 'sigmoid' / 'softmax' (actors): returns
+    (actions [n_slots][E][N], logp [N][n_slots * E]); kind None (value): returns values [N][n_slots * E]."""
+    lib = _lib.require_gpu()
+    T, E, N, F = obs.shape
+    if obs.dtype != torch.float32 or not obs.is_contiguous():
+        raise ValueError("obs must be a contiguous float32 [T][E][N][F] tensor")
+    k = KIND[kind]
+    d = desc(params, E, k, history_len, episode_length, seed, env_base, rng_offset)
+    dev = obs.device
+    if out is None:
+        out = torch.empty((N, n_slots * E), dtype=torch.float32, device=dev)
+    act = None
+    if k != 2:
+        A = params["w2"].shape[1]
+        mb = 1 if (k == 1 or A <= 8) else 2 if A <= 16 else 4
+        dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[mb]
+        act = actions_out if actions_out is not None else torch.empty((n_slots, E, N), dtype=dt, device=dev)
+    rc = lib.d2d_policy_gru(ctypes.byref(d), T, obs.data_ptr(), int(slot0), int(n_slots), 1 if padded else 0,
+                            None if forced is None else forced.data_ptr(), int(rng_step) & 0xFFFFFFFF,
+                            1 if deterministic else 0, None if act is None else act.data_ptr(), out.data_ptr(),
+                            _lib.stream_ptr())
+    _lib.check(rc, "d2d_policy_gru")
+    return (act, out) if k != 2 else out
+
+
+def _strides3(t, T, E, N):
+    if t.dim() == 3:
+        assert tuple(t.shape) == (T, E, N)
+        return t.stride(0), t.stride(1), t.stride(2)
+    assert t.dim() == 2 and tuple(t.shape) == (N, E * T), tuple(t.shape)
+    return t.stride(1), T * t.stride(1), t.stride(0)
+
+
+def _arr(st):
+    return (ctypes.c_int64 * 3)(*[int(v) for v in st])
+
+
+class _Workspace:
+    def __init__(self):
+        self.buf = None
+
+    def get(self, floats, device):
+        if self.buf is None or self.buf.numel() < floats or self.buf.device != device:
+            self.buf = torch.empty((max(int(floats), 1),), dtype=torch.float32, device=device)
+        return self.buf
+
+
+_ws = _Workspace()
+
+
+def grads(params, obs, kind, history_len, episode_length, weight, actions=None, logp_old=None, clip=0.1, beta=0.01,
+          scale=None, grads=None, stats=None):
+    """Gradients of every agent's loss w.r.t. its RNN params (what autograd leaves in .grad):
+    actors (kind 'sigmoid' / 'softmax'): -mean min(r W, clip(r) W) - beta mean entropy over the padded
+    training windows of every sample; value (kind None): mean (V - R)^2, weight = R.
+    weight / logp_old: [T][E][N] or [N][E*T] (env-major), any strides.  Returns (grads, stats [N][2])."""
+    lib = _lib.require_gpu()
+    T, E, N, F = obs.shape
+    k = KIND[kind]
+    d = desc(params, E, k, history_len, episode_length)
+    dev = obs.device
+    grads = grads if grads is not None else {n: torch.empty_like(v) for n, v in params.items()}
+    if stats is None:
+        stats = torch.empty((N, 2), dtype=torch.float32, device=dev)
+    scale = 1.0 / (T * E) if scale is None else scale
+    ws = _ws.get(lib.d2d_gru_grad_workspace(ctypes.byref(d), T), dev)
+    lo_st = _arr(_strides3(logp_old, T, E, N)) if logp_old is not None else None
+    rc = lib.d2d_gru_grad(ctypes.byref(d), T, obs.data_ptr(), None if actions is None else actions.data_ptr(),
+                          None if logp_old is None else logp_old.data_ptr(), lo_st, weight.data_ptr(),
+                          _arr(_strides3(weight, T, E, N)), float(clip), float(beta), float(scale),
+                          *(grads[n].data_ptr() for n in ("w_ih", "w_hh", "b_ih", "b_hh", "w1", "b1", "w2", "b2")),
+                          stats.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_ptr())
+    _lib.check(rc, "d2d_gru_grad")
+    return grads, stats

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 3
+#define D2D_ABI_VERSION 4  /* 4: GRU entry points (d2d_policy_gru, d2d_gru_grad) */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -249,6 +249,45 @@ int d2d_ppo_actor_grad(const d2d_mlp_desc* desc, int32_t T, const float* obs, co
 int d2d_ppo_critic_grad(const d2d_mlp_desc* desc, int32_t T, const float* obs, const float* returns,
                         const int64_t* return_strides, float scale, float* gw1, float* gb1, float* gw2, float* gb2,
                         float* stats, float* workspace, int64_t workspace_floats, void* stream);
+
+/* ---- GRU window policies (the reference's RNN module, algorithms/ippo.py:14-51 == d2d_ppo.py:24-59) ----
+ * Per agent: torch.nn.GRU(F, H) weights w_ih [N][3H][F], w_hh [N][3H][H], b_ih, b_hh [N][3H] (gate order
+ * r, z, n) and the head layers.0 w1 [N][H][H], b1 [N][H], layers.2 w2 [N][n_out][H], b2 [N][n_out]
+ * (agent-stacked).  kind 0: sigmoid head -> Bernoulli per channel (combinatorial actor), 1: softmax ->
+ * Categorical (channel-selection / D2DEnv actor), 2: no activation, n_out 1 (iPPO value critic).
+ * Windows are rebuilt in-kernel from the rollout buffer obs [T][n_envs][N][F] (T a multiple of
+ * episode_length): for slot s at episode position p = s % episode_length the window is the last
+ * S = min(p + 1, history_len) obs of the episode, unpadded (rollout / test, ippo.py:302-304, 362-364)
+ * or front-zero-padded to history_len steps (training, preprocess_input_for_rnn ippo.py:390-403);
+ * h0 = 0 for every window.  Sampling as d2d_policy_mlp_step (Philox stream 3, sample index
+ * (s - slot0) * n_envs + e, i.e. the env index for one-slot launches). */
+typedef struct d2d_gru_desc {
+    int32_t n_agents, n_envs, obs_dim, hidden, n_out, kind;
+    int32_t history_len, episode_length;
+    const float *w_ih, *w_hh, *b_ih, *b_hh, *w1, *b1, *w2, *b2;
+    uint64_t seed, env_base;
+    const uint32_t* rng_offset;  /* optional device uint32 added to rng_step (graph replays) */
+} d2d_gru_desc;
+
+/* Behaviour policy / value over slots [slot0, slot0 + n_slots) of the buffer (ippo.py:154-191 per agent,
+ * batch 1, replaced for all agents and envs): kinds 0/1 write actions [n_slots][n_envs][N] (masks / ids;
+ * forced != NULL: evaluate these instead of sampling; deterministic: p > 0.5 / argmax) and log-probs
+ * out [N][n_slots * n_envs]; kind 2 writes the values to out [N][n_slots * n_envs]. */
+int d2d_policy_gru(const d2d_gru_desc* desc, int32_t T, const float* obs, int32_t slot0, int32_t n_slots,
+                   int32_t padded, const void* forced, uint32_t rng_step, int32_t deterministic, void* actions,
+                   float* out, void* stream);
+
+/* PPO.train_step's evaluate + loss + backward for GRU policies (ippo.py:178-217, d2d_ppo.py:183-216) and
+ * the iPPO GRU critic's MSE (ippo.py:210-216) over every sample of the buffer (training windows, padded):
+ * the gradients of all tensors above (overwritten) and stats [N][2] = (sum min-surrogate, sum entropy)
+ * or (sum (V - R)^2, 0).  actions / logp_old / weight strides as d2d_ppo_actor_grad; weight = advantage
+ * or M (kinds 0, 1), return target (kind 2).  obs_dim <= 31.  workspace: d2d_gru_grad_workspace floats. */
+int64_t d2d_gru_grad_workspace(const d2d_gru_desc* desc, int32_t T);
+int d2d_gru_grad(const d2d_gru_desc* desc, int32_t T, const float* obs, const void* actions, const float* logp_old,
+                 const int64_t* logp_strides, const float* weight, const int64_t* weight_strides, float clip,
+                 float beta, float scale, float* g_w_ih, float* g_w_hh, float* g_b_ih, float* g_b_hh, float* g_w1,
+                 float* g_b1, float* g_w2, float* g_b2, float* stats, float* workspace, int64_t workspace_floats,
+                 void* stream);
 
 /* Process-wide tuning options (not part of the reference interface).
  * D2D_OPT_NT_STORES: 1 = write obs/state with non-temporal (streaming) stores.

@@ -1,0 +1,255 @@
+"""GPU parity of the GRU window-policy kernels (csrc/gru_kernels.hip) against plain torch of the same
+ops: the reference's RNN module (GRU over the window from h0 = 0 -> Linear -> ReLU -> Linear ->
+sigmoid / softmax / none, algorithms/ippo.py:14-51), its rollout windows (last <= L obs of the
+episode, unpadded, ippo.py:302-304) and training windows (front-zero-padded to L,
+preprocess_input_for_rnn ippo.py:390-403), the Bernoulli / Categorical log-probs of
+PPO.select_action / evaluate (ippo.py:154-191), and the gradients of PPO.train_step's losses
+(ippo.py:194-217, d2d_ppo.py:198-216) through the window (BPTT).
+
+Tolerances: values 1e-5 absolute; log-probs 1e-5 absolute (or twice torch fp32's own distance to
+float64, where a long window's fp32 rounding exceeds that) wherever every probability is in
+[1e-3, 1 - 1e-3], as the MLP kernel tests; deterministic actions exact away from ties; gradients within
+2e-5 * max|g| of float64 autograd where torch fp32 itself lands in that band, else within 4x torch
+fp32's distance (saturated gates / probabilities)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def make_net(N, F, H, A, seed, in_dims=None):
+    from algorithms._core import RNN, StackedNets
+    torch.manual_seed(seed)
+    dims = in_dims or [F] * N
+    st = StackedNets([RNN(d, A, H) for d in dims], dims, "rnn", "cpu")
+    p = {k: v.detach().clone() for k, v in st.params.items()}
+    # the reference's GRU keeps torch's default init (uniform +-1/sqrt(H)); spread it so the gates
+    # leave their linear regime
+    p["w_ih"] *= 2.0
+    p["w_hh"] *= 2.0
+    return p, dims
+
+
+def make_obs(T, E, N, F, dims, seed, frac=False):
+    g = torch.Generator().manual_seed(seed)
+    obs = torch.zeros(T, E, N, F)
+    D = max(1, F // 3)
+    obs[..., :D] = torch.randint(0, 4, (T, E, N, D), generator=g).float()
+    obs[..., D:] = torch.randint(-1, 2, (T, E, N, F - D), generator=g).float()
+    if frac:
+        obs += torch.rand(obs.shape, generator=g) * 0.3
+    for k, d in enumerate(dims):
+        obs[:, :, k, d:] = 0
+    return obs
+
+
+def gru_ref(p, obs, ep_len, L, padded, kind, dtype=torch.float64):
+    """torch reference: outputs [N][T][E][A] (probs, or values [N][T][E]) of every slot's window."""
+    from algorithms._core import gru_window
+    T, E, N, F = obs.shape
+    q = {k: v.to(dtype) for k, v in p.items()}
+    outs = []
+    for t in range(T):
+        S = min(t % ep_len + 1, L)
+        win = obs[t - S + 1: t + 1].to(dtype).permute(2, 1, 0, 3)                # [N][E][S][F]
+        if padded and S < L:
+            win = torch.cat([torch.zeros(N, E, L - S, F, dtype=dtype), win], 2)
+        h = gru_window(win, q["w_ih"], q["w_hh"], q["b_ih"], q["b_hh"])          # [N][E][H]
+        y = torch.relu(torch.baddbmm(q["b1"].unsqueeze(1), h, q["w1"].transpose(1, 2)))
+        z = torch.baddbmm(q["b2"].unsqueeze(1), y, q["w2"].transpose(1, 2))        # [N][E][A]
+        outs.append(torch.sigmoid(z) if kind == "sigmoid" else torch.softmax(z, -1) if kind == "softmax" else z[..., 0])
+    return torch.stack(outs, 1)
+
+
+CASES = [
+    # kind, N, F, H, A, L, ep_len, T, E
+    ("sigmoid", 3, 30, 64, 8, 6, 10, 20, 37),
+    ("sigmoid", 2, 23, 16, 8, 12, 10, 20, 20),      # L > episode: every window starts at the episode start
+    ("softmax", 3, 12, 32, 5, 4, 8, 16, 40),
+    ("softmax", 2, 25, 64, 2, 3, 6, 12, 17),
+    (None, 3, 30, 64, 1, 6, 10, 20, 37),
+    (None, 2, 15, 16, 1, 5, 7, 14, 19),              # F + 1 = 16: one input tile
+]
+
+
+@pytest.mark.parametrize("padded", [False, True])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: f"{c[0]}-N{c[1]}-F{c[2]}-H{c[3]}-A{c[4]}-L{c[5]}-ep{c[6]}")
+def test_gru_policy_matches_torch(case, padded):
+    from d2dhip import gru
+    from d2dhip.envbatch import pack_masks_torch
+    from torch.distributions import Bernoulli, Categorical
+    kind, N, F, H, A, L, ep, T, E = case
+    p, dims = make_net(N, F, H, A, seed=H + A)
+    obs = make_obs(T, E, N, F, dims, seed=7, frac=kind == "softmax")
+    ref = gru_ref(p, obs, ep, L, padded, kind)                                   # float64
+    dev = "cuda"
+    pd = {k: v.to(dev).contiguous() for k, v in p.items()}
+    od = obs.to(dev).contiguous()
+    if kind is None:
+        vals = gru.policy(pd, od, None, L, ep, 0, T, padded=padded)
+        got = vals.view(N, T, E).cpu().double()
+        torch.testing.assert_close(got, ref, rtol=0, atol=1e-5)
+        return
+    g = torch.Generator().manual_seed(3)
+    probs = ref                                                                  # [N][T][E][A]
+    if kind == "sigmoid":
+        bits = (torch.rand(N, T, E, A, generator=g) < 0.4).double()
+        ref_lp = Bernoulli(probs=probs, validate_args=False).log_prob(bits).mean(-1)
+        forced = pack_masks_torch(bits.permute(1, 2, 0, 3)).to(dev)              # [T][E][N]
+    else:
+        ids = torch.randint(0, A, (N, T, E), generator=g)
+        ref_lp = Categorical(probs=probs, validate_args=False).log_prob(ids)
+        forced = ids.permute(1, 2, 0).to(torch.uint8).contiguous().to(dev)
+    acts, lp = gru.policy(pd, od, kind, L, ep, 0, T, padded=padded, forced=forced)
+    assert torch.equal(acts, forced)
+    lp = lp.view(N, T, E).cpu().double()
+    well = ((probs > 1e-3) & (probs < 1 - 1e-3)).all(-1)
+    assert well.float().mean() > 0.5
+    # 1e-5, or twice torch fp32's own distance to float64 where a long window's fp32 rounding is larger
+    with torch.no_grad():
+        p32 = gru_ref(p, obs, ep, L, padded, kind, torch.float32).double()
+    if kind == "sigmoid":
+        lp32 = Bernoulli(probs=p32, validate_args=False).log_prob(bits).mean(-1)
+    else:
+        lp32 = Categorical(probs=p32, validate_args=False).log_prob(ids)
+    tol = torch.clamp(2 * (lp32 - ref_lp).abs(), min=1e-5)
+    err = (lp - ref_lp).abs()
+    assert bool((err[well] <= tol[well]).all()), (err[well].max().item(), (err / tol)[well].max().item())
+    # deterministic evaluation (ippo.py:166 / 171); one slot at a time like the rollout
+    margin = (probs - 0.5).abs().min(-1).values if kind == "sigmoid" else \
+        (probs.topk(2, -1).values[..., 0] - probs.topk(2, -1).values[..., 1])
+    for t in (0, T // 2 + 1, T - 1):
+        a_t, _ = gru.policy(pd, od, kind, L, ep, t, 1, padded=padded, deterministic=True)
+        if kind == "sigmoid":
+            want = pack_masks_torch((probs[:, t] > 0.5).permute(1, 0, 2))
+        else:
+            want = probs[:, t].argmax(-1).t().to(torch.uint8)
+        clear = (margin[:, t] > 1e-5).t()                                        # [E][N]
+        assert torch.equal(a_t[0].cpu()[clear], want[clear])
+    # sampling: the forced evaluation of sampled actions reproduces their log-probs bit for bit
+    a_s, lp_s = gru.policy(pd, od, kind, L, ep, 0, T, padded=padded, rng_step=5, seed=11)
+    _, lp_f = gru.policy(pd, od, kind, L, ep, 0, T, padded=padded, forced=a_s)
+    torch.testing.assert_close(lp_f, lp_s, rtol=0, atol=0)
+
+
+def ref_loss_grads(p, obs, ep, L, kind, acts, logp_old, W, clip, beta, dtype):
+    """autograd of the per-agent losses summed over agents (each agent's gradient is its own)."""
+    from torch.distributions import Bernoulli, Categorical
+    q = {k: v.to(dtype).clone().requires_grad_() for k, v in p.items()}
+    out = gru_ref(q, obs, ep, L, True, kind, dtype)                            # [N][T][E](A)
+    N = out.shape[0]
+    if kind is None:
+        loss = ((out - W.to(dtype)) ** 2).reshape(N, -1).mean(1)
+        sq = ((out - W.to(dtype)) ** 2).reshape(N, -1).sum(1)
+        stats = torch.stack([sq, torch.zeros_like(sq)], 1)
+    else:
+        if kind == "sigmoid":
+            d = Bernoulli(probs=out, validate_args=False)
+            logp = d.log_prob(acts.to(dtype)).mean(-1)
+            ent = d.entropy().mean(-1)
+        else:
+            d = Categorical(probs=out, validate_args=False)
+            logp = d.log_prob(acts)
+            ent = d.entropy()
+        ratio = torch.exp(logp - logp_old.to(dtype))
+        Wd = W.to(dtype)
+        s = torch.min(ratio * Wd, torch.clamp(ratio, 1 - clip, 1 + clip) * Wd)
+        loss = -s.reshape(N, -1).mean(1) - beta * ent.reshape(N, -1).mean(1)
+        stats = torch.stack([s.reshape(N, -1).sum(1), ent.reshape(N, -1).sum(1)], 1)
+    loss.sum().backward()
+    return {k: v.grad for k, v in q.items()}, stats.detach(), out.detach()
+
+
+GRAD_CASES = [
+    ("sigmoid", 3, 23, 16, 8, 4, 10, 20, 20),
+    ("sigmoid", 2, 30, 64, 8, 6, 8, 16, 18),
+    ("softmax", 3, 12, 32, 5, 3, 6, 12, 23),
+    ("softmax", 2, 15, 16, 4, 8, 6, 12, 16),         # L > episode
+    (None, 3, 30, 64, 1, 5, 8, 16, 18),
+    (None, 2, 12, 32, 1, 3, 6, 12, 21),
+]
+
+
+@pytest.mark.parametrize("case", GRAD_CASES, ids=lambda c: f"{c[0]}-N{c[1]}-F{c[2]}-H{c[3]}-A{c[4]}-L{c[5]}-ep{c[6]}")
+def test_gru_grads_match_autograd(case):
+    from d2dhip import gru
+    from d2dhip.envbatch import pack_masks_torch
+    kind, N, F, H, A, L, ep, T, E = case
+    p, dims = make_net(N, F, H, A, seed=5 + H)
+    obs = make_obs(T, E, N, F, dims, seed=9)
+    g = torch.Generator().manual_seed(4)
+    clip, beta = 0.1, 0.05
+    with torch.no_grad():
+        out64 = gru_ref(p, obs, ep, L, True, kind)
+    acts = acts_dev = logp_old = None
+    if kind is None:
+        W = torch.randn(N, T, E, generator=g)
+    else:
+        if kind == "sigmoid":
+            acts = (torch.rand(N, T, E, A, generator=g) < 0.4).float()
+            acts_dev = pack_masks_torch(acts.permute(1, 2, 0, 3))
+            lp = torch.distributions.Bernoulli(probs=out64).log_prob(acts.double()).mean(-1)
+        else:
+            acts = torch.randint(0, A, (N, T, E), generator=g)
+            acts_dev = acts.permute(1, 2, 0).to(torch.uint8).contiguous()
+            lp = torch.distributions.Categorical(probs=out64).log_prob(acts)
+        logp_old = (lp + (torch.rand(N, T, E, generator=g) * 0.6 - 0.3)).float()
+        W = torch.randn(N, T, E, generator=g)
+    r64, s64, _ = ref_loss_grads(p, obs, ep, L, kind, acts, logp_old, W, clip, beta, torch.float64)
+    r32, s32, _ = ref_loss_grads(p, obs, ep, L, kind, acts, logp_old, W, clip, beta, torch.float32)
+    well = True
+    dev = "cuda"
+    pd = {k: v.to(dev).contiguous() for k, v in p.items()}
+    # per-sample inputs in the rollout layout [T][E][N]
+    W_te = W.permute(1, 2, 0).contiguous().to(dev)
+    lo_te = None if logp_old is None else logp_old.permute(1, 2, 0).contiguous().to(dev)
+    got, stats = gru.grads(pd, obs.to(dev).contiguous(), kind, L, ep, W_te,
+                           actions=None if acts_dev is None else acts_dev.to(dev), logp_old=lo_te, clip=clip, beta=beta)
+    torch.cuda.synchronize()
+    for name in r64:
+        gk = got[name].cpu().double()
+        scale = r64[name].abs().max().item()
+        err64 = (gk - r64[name]).abs().max().item()
+        band = (r32[name].double() - r64[name]).abs().max().item()
+        print(f"  {name}: max|g| {scale:.3e}  |kernel-f64| {err64:.2e}  |torchf32-f64| {band:.2e}")
+        tol = 2e-5 * scale + 1e-7
+        if band <= tol:
+            assert err64 <= tol, (name, err64, tol)
+        else:
+            well = False
+            # ill-conditioned samples (saturated gates / probabilities, where fp32 rounding of 1 - p
+            # decides): within a few times torch fp32's own distance to float64
+            assert err64 <= 4 * band, (name, err64, band)
+    for k, d in enumerate(dims):  # padded input columns get exactly zero gradient
+        assert torch.all(got["w_ih"][k, :, d:] == 0)
+    # loss sums: vs float64 when well conditioned, else vs torch fp32 (log(1 - p) for p -> 1)
+    st = stats.cpu().double()
+    s_ref = s64 if well else s32.double()
+    torch.testing.assert_close(st[:, 0], s_ref[:, 0], rtol=1e-5, atol=1e-4)
+    if kind is not None:
+        torch.testing.assert_close(st[:, 1], s_ref[:, 1], rtol=1e-5, atol=1e-4)
+
+
+def test_gru_grads_deterministic_enough_and_large():
+    """64 agents x 64-step windows (xp_load.py's history_len = n_agents) on a 4-env x 2-episode batch:
+    two launches agree to fp32 rounding (dW_hh is summed with LDS atomics), finite everywhere."""
+    from d2dhip import gru
+    from d2dhip.envbatch import pack_masks_torch
+    N, F, H, A, L, ep, T, E = 64, 30, 64, 8, 64, 100, 200, 4
+    p, dims = make_net(N, F, H, A, seed=1)
+    obs = make_obs(T, E, N, F, dims, seed=2)
+    g = torch.Generator().manual_seed(3)
+    acts = pack_masks_torch((torch.rand(T, E, N, A, generator=g) < 0.3).float())
+    dev = "cuda"
+    pd = {k: v.to(dev).contiguous() for k, v in p.items()}
+    lo = (-torch.rand(T, E, N, generator=g) * 3).to(dev)
+    W = torch.randn(T, E, N, generator=g).to(dev)
+    od = obs.to(dev).contiguous()
+    g1, s1 = gru.grads(pd, od, "sigmoid", L, ep, W, actions=acts.to(dev), logp_old=lo)
+    g1 = {k: v.clone() for k, v in g1.items()}
+    g2, s2 = gru.grads(pd, od, "sigmoid", L, ep, W, actions=acts.to(dev), logp_old=lo)
+    for k in g1:
+        assert torch.isfinite(g1[k]).all()
+        scale = g1[k].abs().max().item()
+        assert (g1[k] - g2[k]).abs().max().item() <= 1e-6 * scale + 1e-9, k

@@ -23,9 +23,9 @@ ENV_BASE = {"ASAN_OPTIONS": "detect_leaks=0:alloc_dealloc_mismatch=0:abort_on_er
 
 
 def _build(target_dir, lib):
-    if not os.path.exists(lib):
-        subprocess.run(["make", "-s", "-j", str(min(8, os.cpu_count() or 2)), "-C", target_dir, "asan"], check=True,
-                       timeout=900)
+    # incremental (a no-op when the sanitizer build is current; build() makes it up front)
+    subprocess.run(["make", "-s", "-j", str(min(8, os.cpu_count() or 2)), "-C", target_dir, "asan"], check=True,
+                   timeout=900)
     assert os.path.exists(lib)
 
 
