@@ -552,6 +552,111 @@ def d2denv_leg(args, rank, world, local):
     return out
 
 
+def gru_leg(args, rank, world, local):
+    """xp_load.py's learner (D2D-PPO with GRU policies, hidden 64, history_len = n_agents = 64,
+    xp_load.py:78-89) on the configs[2] env (64 agents x 8 channels):
+      (1) one behaviour-policy slot at the full --envs batch: the GRU window kernel over a full 64-step
+          window (slot 63 of the episode) for every agent of every env, sampling + log-probs;
+      (2) the BPTT update kernel (PPO.train_step's evaluate + loss + backward through the padded
+          training windows) over a 200-slot rollout of --gru-envs envs;
+      (3) one whole D2D-PPO iteration (rollout + 5 epochs) at --gru-envs envs.
+    Roofline: fp32 MFMA (the kernels compute in v_mfma_f32_16x16x4_f32).  Algorithmic FLOP per
+    agent-sample and window step: GRU cell 2*3H*(F+1) + 2*3H*H (input + recurrent products); the
+    update counts the forward and the two backward products (dW, dh) of every step: 3x that."""
+    from algorithms.d2d_ppo import D2DPPO
+    from d2dhip import gru
+    from envs.combinatorial_env import CombinatorialEnv
+    params = config3_params(args.episode_length)
+    N, H, L = params["n_agents"], 64, params["n_agents"]
+    dev = f"cuda:{local}"
+    E = args.envs
+    env = CombinatorialEnv(**params, n_envs=E, device=dev, seed=51)
+    env.shard(rank, world)
+    b = env.batch()
+    torch.manual_seed(5)
+    lr = D2DPPO(env, hidden_size=H, gamma=0.6, policy_lr=3e-4, value_lr=1e-3, device=dev, useRNN=True,
+                combinatorial=True, history_len=L, early_stopping=False)
+    assert lr._gru_ok()
+    F = b.spec.F
+    # 64 real env slots of obs (random attempts) = the window of slot 63
+    buf = torch.empty((L, E, N, F), dtype=torch.float32, device=dev)
+    act = b.action_buffer()
+    b.reset(want_obs=True, out_obs=buf[0])
+    for i in range(1, L):
+        b.sample_actions(0.1, out=act)
+        b.step(act, want_obs=True, out_obs=buf[i])
+    pp = {k: v.data for k, v in lr.policy.params.items()}
+    logp = torch.empty((N, E), dtype=torch.float32, device=dev)
+    acts = torch.empty((1, E, N), dtype=act.dtype, device=dev)
+
+    def slot():
+        gru.policy(pp, buf, "sigmoid", L, args.episode_length, L - 1, 1, rng_step=7, seed=3, actions_out=acts,
+                   out=logp)
+
+    slot()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record()
+    for _ in range(3):
+        slot()
+    ev[1].record()
+    torch.cuda.synchronize()
+    pol_ms = max_over_ranks(ev[0].elapsed_time(ev[1]) / 3, world)
+    cell = 2 * 3 * H * (F + 1) + 2 * 3 * H * H
+    head = 2 * (H * H + H * 8)
+    pol_flop = (L * cell + head) * E * N
+    del buf, lr, env, b
+    torch.cuda.empty_cache()
+    # (2) + (3) at --gru-envs envs
+    E2 = args.gru_envs
+    env = CombinatorialEnv(**params, n_envs=E2, device=dev, seed=52)
+    env.shard(rank, world)
+    torch.manual_seed(6)
+    np.random.seed(6)
+    lr = D2DPPO(env, hidden_size=H, gamma=0.6, policy_lr=3e-4, value_lr=1e-3, device=dev, useRNN=True,
+                combinatorial=True, history_len=L, early_stopping=False)
+    ro = lr._rollout(E2)
+    pp = {k: v.data for k, v in lr.policy.params.items()}
+    W = torch.randn((ro.T, E2, N), device=dev)
+    gbuf = {k: torch.empty_like(v) for k, v in pp.items()}
+    args_g = (pp, ro.obs, "sigmoid", L, ro.L, W)
+    gru.grads(*args_g, actions=ro.actions, logp_old=ro.logp.permute(0, 2, 1), grads=gbuf)
+    torch.cuda.synchronize()
+    ev[2].record()
+    gru.grads(*args_g, actions=ro.actions, logp_old=ro.logp.permute(0, 2, 1), grads=gbuf)
+    ev[3].record()
+    torch.cuda.synchronize()
+    grad_ms = max_over_ranks(ev[2].elapsed_time(ev[3]), world)
+    samples = ro.T * E2 * N
+    grad_flop = 3 * L * cell * samples + 3 * head * samples
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    ro = lr._rollout(E2)
+    for _ in range(5):
+        lr._update_epoch(ro, lr._update_state(ro))
+    torch.cuda.synchronize()
+    it_s = max_over_ranks(time.perf_counter() - t0, world)
+    peak = 157.3
+    out = {"config": f"xp_load.py learner: D2D-PPO, GRU H={H}, history_len={L}, {N} agents x 8 channels",
+           "policy_slot": {"envs_per_gpu": E, "window": L, "kernel": "d2d::gru_policy_kernel<4, 2, 0, sample>",
+                           "ms": pol_ms, "agent_steps_per_s": E * world * N / (pol_ms / 1e3),
+                           "env_steps_per_s": E * world / (pol_ms / 1e3),
+                           "flop": pol_flop, "achieved_tflops": pol_flop / (pol_ms / 1e3) / 1e12,
+                           "peak_tflops_fp32_mfma": peak, "frac": pol_flop / (pol_ms / 1e3) / 1e12 / peak},
+           "update": {"envs_per_gpu": E2, "slots": ro.T, "agent_samples": samples,
+                      "kernel": "d2d::gru_grad_kernel<4, 2, 0>", "ms": grad_ms,
+                      "agent_samples_per_s": samples * world / (grad_ms / 1e3), "flop": grad_flop,
+                      "achieved_tflops": grad_flop / (grad_ms / 1e3) / 1e12, "peak_tflops_fp32_mfma": peak,
+                      "frac": grad_flop / (grad_ms / 1e3) / 1e12 / peak},
+           "d2d_iteration_s": it_s, "d2d_iteration_envs_per_gpu": E2, "n_epoch": 5,
+           "d2d_env_steps_per_s_end_to_end": E2 * world * ro.T / it_s,
+           "flop_per_agent_step_cell": cell}
+    del lr, env, ro
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -561,7 +666,8 @@ def main():
     ap.add_argument("--episode-length", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
-    ap.add_argument("--legs", default="env,rollout,ppo,train,configs,d2denv")
+    ap.add_argument("--legs", default="env,rollout,ppo,train,configs,d2denv,gru")
+    ap.add_argument("--gru-envs", type=int, default=256, help="envs per GPU in the GRU update / iteration")
     ap.add_argument("--rollout-steps", type=int, default=60)
     ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
     ap.add_argument("--ppo-epochs", type=int, default=6)
@@ -636,6 +742,7 @@ def main():
     train = train_leg(env, args, rank, world, local) if "train" in legs else None
     configs = configs_leg(args, rank, world, local) if "configs" in legs else None
     d2denv = d2denv_leg(args, rank, world, local) if "d2denv" in legs else None
+    gru_res = gru_leg(args, rank, world, local) if "gru" in legs else None
 
     if rank == 0:
         res = {
@@ -673,6 +780,8 @@ def main():
             res["configs"] = configs
         if d2denv is not None:
             res["d2denv"] = d2denv
+        if gru_res is not None:
+            res["gru"] = gru_res
         if cpu is not None:
             res["cpu_baseline"] = cpu
         print(json.dumps(res))

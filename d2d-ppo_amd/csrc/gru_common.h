@@ -31,6 +31,16 @@ struct GruW {  // agent-stacked torch tensors (StackedNets kind "rnn")
   const float *w1, *b1, *w2, *b2;          // layers.0 [N][H][H], [N][H]; layers.2 [N][A][H], [N][A]
 };
 
+// A zero the compiler cannot see through (an SGPR through an empty volatile asm).  Weight-image
+// addresses offset by it inside a loop are loop-variant, so the fragment loads of every window step /
+// tile are not hoisted out of the loop into hundreds of registers (LDS and the images are never
+// written inside those loops, which would otherwise make the loads invariant).
+__device__ __forceinline__ int opaque_zero() {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return z;
+}
+
 __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -45,6 +55,23 @@ template <int W>
 __device__ __forceinline__ f32x4 lds4(const float* img, int row, int col4) {
   return *reinterpret_cast<const f32x4*>(img + swz<W>(row, col4));
 }
+// Per-lane offsets of the A-fragment reads of a W-wide image: row 16T + i, columns [16q + 4g, +4)
+// (forward), and row 16T + 4g + s, column 16t + i (transposed), both = 16 T W + a per-lane offset
+// independent of T (the swizzle only reads row bits below 4), so every tile T is an immediate
+// offset from a handful of registers instead of one computed address per (T, q) / (T, s, t).
+template <int W>
+struct SwzOff {
+  int fwd[W / 16];
+  int tr[W / 16][4];
+  __device__ __forceinline__ SwzOff(int g, int i) {
+#pragma unroll
+    for (int q = 0; q < W / 16; ++q) {
+      fwd[q] = swz<W>(i, 16 * q + 4 * g);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) tr[q][s] = swz<W>(4 * g + s, 16 * q + i);
+    }
+  }
+};
 
 // e^v to ~1 ulp on the hardware exp2: v * log2(e) is carried as th + tl (FMA residual plus the
 // low part of log2 e), 2^tl ~ 1 + tl ln 2.  (__expf rounds v * log2 e first: ~|v| ulp of error,
@@ -111,10 +138,10 @@ __device__ __forceinline__ void load_x(float (&x)[IT][4], const float* obs, size
 // recurrent products vanish).  W_ih from the swizzled LDS image (WIH_LDS) or from the same image
 // unswizzled in global memory (L2-resident; the update kernel).
 template <int HT, int IT, bool WIH_LDS>
-__device__ __forceinline__ void gru_preact(const float* wih, const float* whh_s,
-                                           const float (&x)[IT][4], const float (&h)[HT][4], const f32x4 (&bhn)[HT],
-                                           f32x4 (&rz)[2 * HT], f32x4 (&ni)[HT], f32x4 (&nh)[HT], int g, int i,
-                                           bool h_zero) {
+__device__ __forceinline__ void gru_preact(const float* wih, const float* whh_s, const SwzOff<16 * IT>& oi,
+                                           const SwzOff<16 * HT>& oh, const float (&x)[IT][4],
+                                           const float (&h)[HT][4], const f32x4 (&bhn)[HT], f32x4 (&rz)[2 * HT],
+                                           f32x4 (&ni)[HT], f32x4 (&nh)[HT], int g, int i, bool h_zero) {
   constexpr int HW = 16 * HT, IW = 16 * IT;
 #pragma unroll
   for (int T = 0; T < 3 * HT; ++T) {
@@ -122,7 +149,7 @@ __device__ __forceinline__ void gru_preact(const float* wih, const float* whh_s,
 #pragma unroll
     for (int q = 0; q < IT; ++q) {
       f32x4 wv;
-      if constexpr (WIH_LDS) wv = lds4<IW>(wih, 16 * T + i, 16 * q + 4 * g);
+      if constexpr (WIH_LDS) wv = *reinterpret_cast<const f32x4*>(wih + 16 * T * IW + oi.fwd[q]);
       else wv = *reinterpret_cast<const f32x4*>(wih + (size_t)(16 * T + i) * IW + 16 * q + 4 * g);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc = mfma4(wv[r], x[q][r], acc);
@@ -138,7 +165,7 @@ __device__ __forceinline__ void gru_preact(const float* wih, const float* whh_s,
     f32x4 acc = T < 2 * HT ? rz[T] : nh[T - 2 * HT];
 #pragma unroll
     for (int q = 0; q < HT; ++q) {
-      const f32x4 wv = lds4<HW>(whh_s, 16 * T + i, 16 * q + 4 * g);
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(whh_s + 16 * T * HW + oh.fwd[q]);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc = mfma4(wv[r], h[q][r], acc);
     }
@@ -173,49 +200,65 @@ __device__ __forceinline__ void load_bhn(f32x4 (&bhn)[HT], const GruW& w, int k,
     }
 }
 
-// Head forward: pre1 = W1 h + b1 (accumulator layout, unit 16t + 4g + r), y = relu(pre1),
-// lg = W2 y + b2 (rows = output 4g + r, sample i).  W1 / W2 fragments straight from global (L2):
-// once per window.
+// Zero-padded head image of one agent: W1p [HW][HW], W2p [16][HW], b1p [HW], b2p [16] (HW = 16 HT):
+// no masks in the fragment loads, every address an immediate offset from a per-lane base.
 template <int HT>
-__device__ __forceinline__ void gru_head(const GruW& w, int k, int H, int A, const float (&h)[HT][4],
-                                         f32x4 (&pre1)[HT], float (&y)[HT][4], f32x4& lg, int g, int i) {
-  const float* W1 = w.w1 + (size_t)k * H * H;
-  const float* W2 = w.w2 + (size_t)k * A * H;
+struct HeadImg {
+  static constexpr int HW = 16 * HT, W1 = 0, W2 = HW * HW, B1 = W2 + 16 * HW, B2 = B1 + HW, SIZE = B2 + 16;
+};
+
+// idx-th element of agent k's head image (threads of a workgroup or a grid fill it cooperatively)
+template <int HT>
+__device__ __forceinline__ float head_img_elem(const GruW& w, int k, int H, int A, int idx) {
+  using HI = HeadImg<HT>;
+  constexpr int HW = HI::HW;
+  if (idx < HI::W2) {
+    const int r = idx / HW, c = idx - r * HW;
+    return (r < H && c < H) ? w.w1[((size_t)k * H + r) * H + c] : 0.f;
+  }
+  if (idx < HI::B1) {
+    const int r = (idx - HI::W2) / HW, c = (idx - HI::W2) - r * HW;
+    return (r < A && c < H) ? w.w2[((size_t)k * A + r) * H + c] : 0.f;
+  }
+  if (idx < HI::B2) {
+    const int u = idx - HI::B1;
+    return u < H ? w.b1[(size_t)k * H + u] : 0.f;
+  }
+  const int o = idx - HI::B2;
+  return o < A ? w.b2[(size_t)k * A + o] : 0.f;
+}
+
+// Head forward: pre1 = W1 h + b1 (accumulator layout, unit 16t + 4g + r), y = relu(pre1),
+// lg = W2 y + b2 (rows = output 4g + r, sample i), from the padded head image.
+template <int HT>
+__device__ __forceinline__ void gru_head(const float* img, const float (&h)[HT][4], f32x4 (&pre1)[HT],
+                                         float (&y)[HT][4], f32x4& lg, int g, int i) {
+  using HI = HeadImg<HT>;
+  constexpr int HW = HI::HW;
 #pragma unroll
   for (int t = 0; t < HT; ++t) {
     f32x4 acc;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int u = 16 * t + 4 * g + r;
-      acc[r] = u < H ? w.b1[(size_t)k * H + u] : 0.f;
+    for (int r = 0; r < 4; ++r) acc[r] = img[HI::B1 + 16 * t + 4 * g + r];
+#pragma unroll
+    for (int q = 0; q < HT; ++q) {
+      const f32x4 wv = *reinterpret_cast<const f32x4*>(img + HI::W1 + (16 * t + i) * HW + 16 * q + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc = mfma4(wv[r], h[q][r], acc);
     }
-    const int row = 16 * t + i;
-#pragma unroll
-    for (int q = 0; q < HT; ++q)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = 16 * q + 4 * g + r;
-        const float wv = (row < H && col < H) ? W1[(size_t)row * H + col] : 0.f;
-        acc = mfma4(wv, h[q][r], acc);
-      }
     pre1[t] = acc;
 #pragma unroll
     for (int r = 0; r < 4; ++r) y[t][r] = relu(acc[r]);
   }
   f32x4 acc;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int o = 4 * g + r;
-    acc[r] = o < A ? w.b2[(size_t)k * A + o] : 0.f;
+  for (int r = 0; r < 4; ++r) acc[r] = img[HI::B2 + 4 * g + r];
+#pragma unroll
+  for (int q = 0; q < HT; ++q) {
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(img + HI::W2 + i * HW + 16 * q + 4 * g);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc = mfma4(wv[r], y[q][r], acc);
   }
-#pragma unroll
-  for (int q = 0; q < HT; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int col = 16 * q + 4 * g + r;
-      const float wv = (i < A && col < H) ? W2[(size_t)i * H + col] : 0.f;
-      acc = mfma4(wv, y[q][r], acc);
-    }
   lg = acc;
 }
 

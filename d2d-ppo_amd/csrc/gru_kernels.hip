@@ -43,6 +43,8 @@ struct GruArgs {
   float* partial;                         // [G][N][P]
   float* hist;                            // [G * N * 4 waves][L][64 lanes][4 HT] per-wave hidden-state scratch
   float* wimg;                            // [N][3 * 16 HT][16 IT] input images (gru_wih_image_kernel)
+  float* hacc;                            // [G * N * 4 waves][GruHeadAcc::NV][64] head-gradient sums
+  float* himg;                            // [N][HeadImg::SIZE] padded head images (gru_images_kernel)
   int G, P;
 };
 
@@ -56,14 +58,19 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
   constexpr int HW = 16 * HT, IW = 16 * IT, R3 = 3 * HW;
   __shared__ float wih_s[R3 * IW];
   __shared__ float whh_s[R3 * HW];
+  __shared__ float head_s[HeadImg<HT>::SIZE];
   const int k = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H, F = a.F, N = a.N, E = a.E;
   load_gru_images<HT, IT>(wih_s, whh_s, a.w, k, H, F, tid, blockDim.x);
+  for (int idx = tid; idx < HeadImg<HT>::SIZE; idx += blockDim.x)
+    head_s[idx] = head_img_elem<HT>(a.w, k, H, KIND == kGruValue ? 1 : a.A, idx);
   f32x4 bhn[HT];
   load_bhn<HT>(bhn, a.w, k, H, g);
   const uint32_t rng = (MODE == kModeSample && a.ep.rng_off) ? a.ep.rng_step + *a.ep.rng_off : a.ep.rng_step;
+  const SwzOff<IW> oi(g, i);
+  const SwzOff<HW> oh(g, i);
   __syncthreads();
 
   const int n_tiles = a.n_slots * a.env_tiles;
@@ -89,12 +96,13 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
       const int row_slot = zero ? lo : lo + (j - pad);
       load_x<IT>(x, a.obs, (((size_t)row_slot * E + e0) * N + k) * F, a.obs_floats, N * F, F, g, i, ok, zero);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
-      gru_preact<HT, IT, true>(wih_s, whh_s, x, h, bhn, rz, ni, nh, g, i, j == 0);
+      const int z = opaque_zero();
+      gru_preact<HT, IT, true>(wih_s + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
       gru_gates<HT>(rz, ni, nh, h);
     }
     f32x4 pre1[HT], lg;
     float y[HT][4];
-    gru_head<HT>(a.w, k, H, KIND == kGruValue ? 1 : a.A, h, pre1, y, lg, g, i);
+    gru_head<HT>(head_s + opaque_zero(), h, pre1, y, lg, g, i);
     const int samp = sl * E + env;  // slot-major sample index of the launch
     if constexpr (KIND == kGruValue) {
       if (ok && g == 0) a.value_out[(size_t)k * a.ep.E + samp] = lg[0];
@@ -139,16 +147,15 @@ __device__ __forceinline__ GruIn load_gru_in(const GruArgs& a, int t, int env, i
   return in;
 }
 
-// Register partial sums of one wave, flattened for the cross-wave reduction.
+// Register partial sums of one wave, flattened for the cross-wave reduction.  The head's gradients
+// (layers.0 / layers.2, once per window) are accumulated in a per-wave global block instead
+// (GruHeadAcc, read-modify-write per tile), which keeps the BPTT loop within the register file.
 template <int HT, int IT>
 struct GruAcc {
   f32x4 wih[3 * HT][IT];   // dW_ih (+ bias column F): D[gate row 16T + 4g + r][input 16U + i]
-  f32x4 w1[HT][HT];        // dW1: D[unit 16t + 4g + r][unit 16U + i]
-  f32x4 w2[HT];            // dW2: D[output 4g + r][unit 16U + i]
-  float b1[HT][4], b2[4], bhn[HT][4];  // per-sample-lane partial sums (rows 16t + 4g + r / 4g + r)
+  float bhn[HT][4];        // per-sample-lane partial sums of dL/db_hn (unit 16t + 4g + r)
   float st[2];             // loss sums
-  static constexpr int NV = 3 * HT * IT * 4 + HT * HT * 4 + HT * 4 + HT * 4 + 4 + HT * 4 + 2;
-  // fn(v, x) on every accumulator in a fixed order (x a local copy, written back)
+  static constexpr int NV = 3 * HT * IT * 4 + HT * 4 + 2;
   template <class Fn>
   __device__ __forceinline__ void each(Fn fn) {
     int v = 0;
@@ -161,22 +168,18 @@ struct GruAcc {
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
-      for (int U = 0; U < HT; ++U)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) { float x = w1[t][U][r]; fn(v++, x); w1[t][U][r] = x; }
-#pragma unroll
-    for (int U = 0; U < HT; ++U)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { float x = w2[U][r]; fn(v++, x); w2[U][r] = x; }
-#pragma unroll
-    for (int t = 0; t < HT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { fn(v++, b1[t][r]); fn(v++, bhn[t][r]); }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) fn(v++, b2[r]);
+      for (int r = 0; r < 4; ++r) fn(v++, bhn[t][r]);
     fn(v++, st[0]);
     fn(v++, st[1]);
   }
+};
+
+// Head gradients of one wave in global memory, [v][64 lanes] (coalesced): dW1 tiles
+// D[unit 16t + 4g + r][unit 16U + i], dW2 tiles D[output 4g + r][unit 16U + i], and per-sample-lane
+// partial sums of db1 (unit 16t + 4g + r) and db2 (output 4g + r).
+template <int HT>
+struct GruHeadAcc {
+  static constexpr int W1 = 0, W2 = HT * HT * 4, B1 = W2 + HT * 4, B2 = B1 + HT * 4, NV = B2 + 4;
 };
 
 // Partial layout per (workgroup, agent): the gradient of every torch tensor of the RNN module
@@ -214,12 +217,17 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   load_bhn<HT>(bhn, a.w, k, H, g);
   GruAcc<HT, IT> acc;
   acc.each([](int, float& x) { x = 0.f; });
-  const float* W1 = a.w.w1 + (size_t)k * H * H;
-  const float* W2 = a.w.w2 + (size_t)k * A * H;
+  using HI = HeadImg<HT>;
+  const float* himg = a.himg + (size_t)k * HI::SIZE;  // padded head image (gru_images_kernel)
   // the input image of gru_common.h (bias column F) written by gru_wih_image_kernel: A fragments
   // straight from L2 every step (registers are the update kernel's scarce resource)
   const float* wimg = a.wimg + (size_t)k * 3 * HW * (16 * IT);
-  float* hist = a.hist + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave) * (size_t)L * 64 * 4 * HT;
+  const SwzOff<16 * IT> oi(g, i);  // (unused: W_ih comes from the global image)
+  const SwzOff<HW> oh(g, i);
+  const size_t wave_id = (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave;
+  float* hist = a.hist + wave_id * (size_t)L * 64 * 4 * HT;
+  float* hacc = a.hacc + wave_id * (size_t)GruHeadAcc<HT>::NV * 64;
+  for (int v = 0; v < GruHeadAcc<HT>::NV; ++v) hacc[v * 64 + lane] = 0.f;
   __syncthreads();
 
   const int n_tiles = a.T * a.env_tiles;
@@ -245,7 +253,8 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       float x[IT][4];
       load_x<IT>(x, a.obs, row_of(j), a.obs_floats, N * F, F, g, i, ok, j < pad);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
-      gru_preact<HT, IT, false>(wimg, whh_s, x, h, bhn, rz, ni, nh, g, i, j == 0);
+      const int z = opaque_zero();
+      gru_preact<HT, IT, false>(wimg + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
       gru_gates<HT>(rz, ni, nh, h);
       if (j + 1 < L) {
         f32x4* dst = reinterpret_cast<f32x4*>(hist + ((size_t)j * 64 + lane) * 4 * HT);
@@ -257,7 +266,8 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     // ---- head forward + loss gradient w.r.t. the head outputs
     f32x4 pre1[HT], lg;
     float y[HT][4];
-    gru_head<HT>(a.w, k, H, A, h, pre1, y, lg, g, i);
+    const float* hi_ = himg + opaque_zero();
+    gru_head<HT>(hi_, h, pre1, y, lg, g, i);
     f32x4 dlg;
     if constexpr (KIND == kGruValue) {
       const float d = lg[0] - in.w;  // V - R
@@ -268,11 +278,13 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
                                                                                   acc.st[0], acc.st[1]);
     }
 
-    // ---- head backward.  dW2 += dlg y^T, db2, dy = W2^T dlg, dpre1 = dy [pre1 > 0]
+    // ---- head backward.  dW2 += dlg y^T, db2, dy = W2^T dlg, dpre1 = dy [pre1 > 0]; dW1 += dpre1 h_L^T,
+    // db1; dh_L = W1^T dpre1.  The head's gradient sums are read-modified-written in the wave's global block.
+    using HA = GruHeadAcc<HT>;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       sc[(4 * g + r) * 16 + pcol(i)] = dlg[r];
-      acc.b2[r] += dlg[r];
+      hacc[(HA::B2 + r) * 64 + lane] += dlg[r];
 #pragma unroll
       for (int t = 0; t < HT; ++t) sc[(16 + 16 * t + 4 * g + r) * 16 + pcol(i)] = y[t][r];
     }
@@ -282,8 +294,11 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
       for (int U = 0; U < HT; ++U) {
         const f32x4 bf = sc_frag(sc, 16 + 16 * U + i, g);
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) acc.w2[U] = mfma4(af[s4], bf[s4], acc.w2[U]);
+        for (int s4 = 0; s4 < 4; ++s4) d = mfma4(af[s4], bf[s4], d);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hacc[(HA::W2 + 4 * U + r) * 64 + lane] += d[r];
       }
     }
     float dpre1[HT][4];
@@ -291,19 +306,14 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     for (int t = 0; t < HT; ++t) {
       f32x4 dy = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        const int o = 4 * g + s4, col = 16 * t + i;
-        const float wv = (o < A && col < H) ? W2[(size_t)o * H + col] : 0.f;
-        dy = mfma4(wv, dlg[s4], dy);
-      }
+      for (int s4 = 0; s4 < 4; ++s4) dy = mfma4(hi_[HI::W2 + (4 * g + s4) * HW + 16 * t + i], dlg[s4], dy);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         dpre1[t][r] = pre1[t][r] > 0.f ? dy[r] : 0.f;
-        acc.b1[t][r] += dpre1[t][r];
+        hacc[(HA::B1 + 4 * t + r) * 64 + lane] += dpre1[t][r];
       }
     }
     lds_order();
-    // dW1 += dpre1 h_L^T, dh_L = W1^T dpre1
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
@@ -318,8 +328,11 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
       for (int U = 0; U < HT; ++U) {
         const f32x4 bf = sc_frag(sc, HW + 16 * U + i, g);
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) acc.w1[t][U] = mfma4(af[s4], bf[s4], acc.w1[t][U]);
+        for (int s4 = 0; s4 < 4; ++s4) d = mfma4(af[s4], bf[s4], d);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hacc[(HA::W1 + (t * HT + U) * 4 + r) * 64 + lane] += d[r];
       }
     }
     float gcur[HT][4];
@@ -329,11 +342,8 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
       for (int q = 0; q < HT; ++q)
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const int rowk = 16 * q + 4 * g + s4, col = 16 * t + i;
-          const float wv = (rowk < H && col < H) ? W1[(size_t)rowk * H + col] : 0.f;
-          dh = mfma4(wv, dpre1[q][s4], dh);
-        }
+        for (int s4 = 0; s4 < 4; ++s4)
+          dh = mfma4(hi_[HI::W1 + (16 * q + 4 * g + s4) * HW + 16 * t + i], dpre1[q][s4], dh);
 #pragma unroll
       for (int r = 0; r < 4; ++r) gcur[t][r] = dh[r];
     }
@@ -361,7 +371,10 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       float x[IT][4];
       load_x<IT>(x, a.obs, xoff, a.obs_floats, N * F, F, g, i, ok, zero);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
-      gru_preact<HT, IT, false>(wimg, whh_s, x, hp, bhn, rz, ni, nh, g, i, j == 0);
+      const int z = opaque_zero();
+      const float* wh = whh_s + z;
+      gru_preact<HT, IT, false>(wimg + z, wh, oi, oh, x, hp, bhn, rz, ni, nh, g, i, j == 0);
+      __builtin_amdgcn_sched_barrier(0);
       float drp[HT][4], dzp[HT][4], dnp[HT][4], dghn[HT][4], gz[HT][4];
 #pragma unroll
       for (int t = 0; t < HT; ++t)
@@ -390,6 +403,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
           sc[(R3 + u) * 16 + c] = hp[t][r];
         }
       lds_order();
+      __builtin_amdgcn_sched_barrier(0);
       // dW_ih += dgi x^T: x^T operand sample-on-k from global (sample 4 s4 + g, input 16U + i)
       {
         float xt[IT][4];
@@ -425,6 +439,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) sc[(2 * HW + 16 * t + 4 * g + r) * 16 + pcol(i)] = dghn[t][r];
       lds_order();
+      __builtin_amdgcn_sched_barrier(0);
       // dW_hh += dgh h_{j-1}^T, accumulated in LDS by the four waves
 #pragma unroll
       for (int T = 0; T < 3 * HT; ++T) {
@@ -439,6 +454,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
           for (int r = 0; r < 4; ++r) atomicAdd(&dwhh_s[(16 * T + 4 * g + r) * HW + 16 * U + i], d[r]);
         }
       }
+      __builtin_amdgcn_sched_barrier(0);
       // dh_{j-1} = g z + W_hh^T dgh
 #pragma unroll
       for (int t = 0; t < HT; ++t) {
@@ -447,7 +463,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
         for (int T = 0; T < 3 * HT; ++T)
 #pragma unroll
           for (int s4 = 0; s4 < 4; ++s4) {
-            const float wv = whh_s[swz<HW>(16 * T + 4 * g + s4, 16 * t + i)];
+            const float wv = wh[16 * T * HW + oh.tr[t][s4]];
             const float bv = T < HT ? drp[T][s4] : T < 2 * HT ? dzp[T - HT][s4] : dghn[T - 2 * HT][s4];
             dh = mfma4(wv, bv, dh);
           }
@@ -493,6 +509,13 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
             if (G < 2) part[o.bhh + G * H + u] = v;  // b_hr / b_hz enter exactly like b_ir / b_iz
           }
         }
+    // the head's sums: the workgroup's four wave blocks in fixed order
+    using HA = GruHeadAcc<HT>;
+    const float* hb = a.hacc + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 * HA::NV * 64;
+    auto hsum = [&](int v) {
+      return ((hb[v * 64 + lane] + hb[(HA::NV + v) * 64 + lane]) + hb[(2 * HA::NV + v) * 64 + lane]) +
+             hb[(3 * HA::NV + v) * 64 + lane];
+    };
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
@@ -500,14 +523,16 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = 16 * t + 4 * g + r, col = 16 * U + i;
-          if (row < H && col < H) part[o.w1 + row * H + col] = acc.w1[t][U][r];
+          const float v = hsum(HA::W1 + (t * HT + U) * 4 + r);
+          if (row < H && col < H) part[o.w1 + row * H + col] = v;
         }
 #pragma unroll
     for (int U = 0; U < HT; ++U)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = 4 * g + r, col = 16 * U + i;
-        if (row < A && col < H) part[o.w2 + row * H + col] = acc.w2[U][r];
+        const float v = hsum(HA::W2 + 4 * U + r);
+        if (row < A && col < H) part[o.w2 + row * H + col] = v;
       }
     // bias sums: the 16 sample lanes of each row group
 #pragma unroll
@@ -515,7 +540,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int u = 16 * t + 4 * g + r;
-        const float sb1 = row_sum16(acc.b1[t][r]), sbn = row_sum16(acc.bhn[t][r]);
+        const float sb1 = row_sum16(hsum(HA::B1 + 4 * t + r)), sbn = row_sum16(acc.bhn[t][r]);
         if (i == 0 && u < H) {
           part[o.b1 + u] = sb1;
           part[o.bhh + 2 * H + u] = sbn;
@@ -523,7 +548,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float sb2 = row_sum16(acc.b2[r]);
+      const float sb2 = row_sum16(hsum(HA::B2 + r));
       if (i == 0 && 4 * g + r < A) part[o.b2 + 4 * g + r] = sb2;
     }
     float s0 = acc.st[0], s1 = acc.st[1];
@@ -538,6 +563,15 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 
 // The input images of all agents, unswizzled: img[k][R][c] (gate row R of the padded layout, input
 // column c; column F = the biases of gru_common.h), zero outside the real rows / columns.
+template <int HT>
+__global__ void gru_head_image_kernel(GruW w, int N, int H, int A, float* img) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int SZ = HeadImg<HT>::SIZE;
+  if (idx >= (int64_t)N * SZ) return;
+  const int k = (int)(idx / SZ);
+  img[idx] = head_img_elem<HT>(w, k, H, A, (int)(idx - (int64_t)k * SZ));
+}
+
 __global__ void gru_wih_image_kernel(GruW w, int N, int H, int F, int HW, int IW, float* img) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)N * 3 * HW * IW) return;
@@ -682,7 +716,9 @@ extern "C" int64_t d2d_gru_grad_workspace(const d2d_gru_desc* d, int32_t T) {
   const int64_t partial = (int64_t)G * d->n_agents * o.P;
   const int64_t hist = (int64_t)G * d->n_agents * 4 * d->history_len * 64 * 4 * ht;
   const int64_t img = (int64_t)d->n_agents * 3 * 16 * ht * 32;
-  return partial + hist + img;
+  const int64_t hacc = (int64_t)G * d->n_agents * 4 * 64 * (ht * ht * 4 + ht * 8 + 4);
+  const int64_t himg = (int64_t)d->n_agents * (16 * ht * 16 * ht + 16 * 16 * ht + 16 * ht + 16);
+  return partial + hist + img + hacc + himg;
 }
 
 template <int HT, int IT>
@@ -730,12 +766,19 @@ extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const float* obs, 
   a.hist = workspace + (int64_t)a.G * a.N * a.P;
   const int ht = (a.H + 15) / 16, htp = ht <= 1 ? 1 : ht <= 2 ? 2 : 4, itp = a.F + 1 <= 16 ? 1 : 2;
   a.wimg = a.hist + (int64_t)a.G * a.N * 4 * a.L * 64 * 4 * htp;
+  a.hacc = a.wimg + (int64_t)a.N * 3 * 16 * htp * 32;
+  a.himg = a.hacc + (int64_t)a.G * a.N * 4 * 64 * (htp * htp * 4 + htp * 8 + 4);
   if (a.N == 0) return D2D_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   {
     const int64_t n = (int64_t)a.N * 3 * 16 * htp * 16 * itp;
     hipLaunchKernelGGL(gru_wih_image_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.w, a.N, a.H, a.F,
                        16 * htp, 16 * itp, a.wimg);
+    const int64_t nh = (int64_t)a.N * (16 * htp * 16 * htp + 16 * 16 * htp + 16 * htp + 16);
+    const dim3 gh((unsigned)((nh + 255) / 256));
+    if (htp == 1) hipLaunchKernelGGL(gru_head_image_kernel<1>, gh, dim3(256), 0, s, a.w, a.N, a.H, a.A, a.himg);
+    else if (htp == 2) hipLaunchKernelGGL(gru_head_image_kernel<2>, gh, dim3(256), 0, s, a.w, a.N, a.H, a.A, a.himg);
+    else hipLaunchKernelGGL(gru_head_image_kernel<4>, gh, dim3(256), 0, s, a.w, a.N, a.H, a.A, a.himg);
   }
   if (tiles == 0) {
     D2D_CHECK_HIP(hipMemsetAsync(workspace, 0, sizeof(float) * (size_t)a.N * a.P, s));
