@@ -25,6 +25,8 @@ import torch
 
 from d2dhip.envbatch import pack_masks_torch
 from d2dhip.gae import gae_returns
+from d2dhip._lib import record_bytes as _lib_record_bytes
+from d2dhip.record import ObsRecord, set_format
 
 from ._core import make_dist, rnn_windows, unpack_actions
 from .data_parallel import DataParallelMixin, allreduce_mean_scalar
@@ -34,12 +36,18 @@ class Rollout:
     """Device tensors of one rollout ([T][E]... time-major as produced).  `adv` / `ret` (agent-
     major [N][E*T], env-major sample order) are materialised from `adv_tne` / `ret_tne`
     ([T][N][E], the GAE output) only when a consumer asks for them; the fused update kernels
-    read the [T][N][E] tensors in place."""
+    read the [T][N][E] tensors in place.  `obs` is the env kernel's compact record (ObsRecord,
+    d2dhip/record.py) when the learner runs on it; `obs_f32` is the fp32 [T][E][N][F] view either way."""
 
     def __init__(self, **kw):
         self.__dict__.update(kw)
 
     def __getattr__(self, name):
+        if name == "obs_f32":
+            o = self.__dict__["obs"]
+            v = o.decode() if isinstance(o, ObsRecord) else o
+            self.__dict__[name] = v
+            return v
         src = self.__dict__.get(name + "_tne") if name in ("adv", "ret") else None
         if src is None:
             raise AttributeError(name)
@@ -132,6 +140,14 @@ class BatchedLearnerBase(DataParallelMixin):
     def _gru_kind(self):
         return "sigmoid" if self.combinatorial else "softmax"
 
+    # compact obs record (d2dhip/record.py): on by default where every consumer of the rollout's obs
+    # is a HIP kernel that reads it; D2D_OBS_RECORD=0 keeps the fp32 obs buffer (A/B timing, tests)
+    obs_record = os.environ.get("D2D_OBS_RECORD", "1") != "0"
+
+    def _record_ok(self):
+        return (self.obs_record and self.kind == "comb" and bool(self.combinatorial)
+                and (self._gru_ok() or (not self.useRNN and self._fused_ok())) and self._fused_update_ok())
+
     def _fused_update_ok(self):
         """The fused HIP update kernels cover the MLP actors with F + 1 <= 64 inputs (and the iPPO
         per-agent MLP critics; csrc/update_kernels.hip) and the GRU policies / critics
@@ -171,7 +187,8 @@ class BatchedLearnerBase(DataParallelMixin):
         desc.v1 = desc.c1 = desc.v2 = desc.c2 = None
         logp = torch.empty((N, TE), dtype=torch.float32, device=self.device)
         scratch = torch.empty_like(ro.actions)
-        rc = lib.d2d_policy_mlp_step(desc, ro.obs.data_ptr(), ro.actions.data_ptr(), 0, 0, scratch.data_ptr(),
+        optr = set_format(desc, ro.obs)
+        rc = lib.d2d_policy_mlp_step(desc, optr, ro.actions.data_ptr(), 0, 0, scratch.data_ptr(),
                                      logp.data_ptr(), None, _lib.stream_ptr())
         _lib.check(rc, "d2d_policy_mlp_step (forced)")
         return logp
@@ -222,7 +239,8 @@ class BatchedLearnerBase(DataParallelMixin):
             fz = None
             if forced is not None:
                 fz = self._env_actions(forced).contiguous()
-            rc = lib.d2d_policy_mlp_step(desc, obs_buf[i].data_ptr(), None if fz is None else fz.data_ptr(),
+            optr = set_format(desc, obs_buf[i])
+            rc = lib.d2d_policy_mlp_step(desc, optr, None if fz is None else fz.data_ptr(),
                                          b.rng_step, 0 if train else 1, act_out.data_ptr(), logp_out.data_ptr(),
                                          None if val_out is None else val_out.data_ptr(), _lib.stream_ptr())
             _lib.check(rc, "d2d_policy_mlp_step")
@@ -304,7 +322,9 @@ class BatchedLearnerBase(DataParallelMixin):
         s, E, L, dev = b.spec, b.E, self.env.episode_length, self.device
         T = waves * L
         f64 = lambda: torch.zeros((waves, E), dtype=torch.float64, device=dev)  # noqa: E731
-        return dict(obs=torch.empty((T, E, s.N, s.F), dtype=torch.float32, device=dev),
+        obs = b.record_buffer((T,)) if self._record_ok() else torch.empty((T, E, s.N, s.F), dtype=torch.float32,
+                                                                         device=dev)
+        return dict(obs=obs,
                     act=torch.empty((T, E, s.N), dtype=b.action_buffer().dtype, device=dev),
                     logp=torch.empty((T, s.N, E), dtype=torch.float32, device=dev),
                     rew=torch.empty((T, E), dtype=torch.int32, device=dev),
@@ -375,7 +395,8 @@ class BatchedLearnerBase(DataParallelMixin):
                 and (self.kind == "comb") == bool(self.combinatorial)):
             return False
         s = b.spec
-        return T * b.E * s.N * s.F * 4 <= self.GRAPH_ROLLOUT_MAX_BYTES
+        row = _lib_record_bytes(s.F) if self._record_ok() else 4 * s.F
+        return T * b.E * s.N * row <= self.GRAPH_ROLLOUT_MAX_BYTES
 
     def _collect_graph(self, b, waves, want_values, want_state):
         """Capture once per rollout shape, replay afterwards.  The kernels add the device word
@@ -479,12 +500,12 @@ class BatchedLearnerBase(DataParallelMixin):
         s = self.env.batch().spec
         N = s.N
         if self.useRNN:
-            seq = ro.obs.permute(1, 2, 0, 3).reshape(ro.E * N, ro.T, -1)          # [E*N][T][F]
+            seq = ro.obs_f32.permute(1, 2, 0, 3).reshape(ro.E * N, ro.T, -1)      # [E*N][T][F]
             win = rnn_windows(seq, self.history_len, ro.L)                        # [E*N][T][L][F]
             x = win.view(ro.E, N, ro.T, self.history_len, -1).transpose(0, 1).reshape(N, ro.E * ro.T,
                                                                                        self.history_len, -1)
         else:
-            x = ro.obs.permute(2, 1, 0, 3).reshape(N, ro.E * ro.T, -1)
+            x = ro.obs_f32.permute(2, 1, 0, 3).reshape(N, ro.E * ro.T, -1)
         acts = ro.actions.permute(2, 1, 0).reshape(N, -1)                        # [N][E*T]
         if self.kind == "comb":
             acts = unpack_actions(acts, s.C)                                      # [N][B][C]

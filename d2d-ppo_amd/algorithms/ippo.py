@@ -182,7 +182,7 @@ class iPPO(BatchedLearnerBase):
     def _reference_view(self, ro):
         s = self.env.batch().spec
         N = s.N
-        obs = ro.obs.permute(2, 1, 0, 3).reshape(N, ro.E * ro.T, -1)
+        obs = ro.obs_f32.permute(2, 1, 0, 3).reshape(N, ro.E * ro.T, -1)
         obs_list = [obs[k, :, : s.obs_len[k]] for k in range(N)]
         acts = ro.actions.permute(1, 0, 2).reshape(ro.E * ro.T, N)
         if self.kind == "comb":

@@ -69,3 +69,17 @@ void d2d_set_error(const char* fmt, ...);
       return D2D_EHIP;                                                         \
     }                                                                          \
   } while (0)
+
+// obs_format of a d2d_mlp_desc / d2d_gru_desc: the obs argument as fp32 rows (f32) or as the
+// env kernel's compact record (rec, with the int8-column masks sgn); exactly one is set
+inline int obs_format_args(int32_t format, const uint32_t* sgn_in, int32_t obs_dim, const void* obs, const float*& f32,
+                           const uint8_t*& rec, const uint32_t*& sgn) {
+  f32 = nullptr; rec = nullptr; sgn = nullptr;
+  if (format == D2D_OBS_F32) { f32 = static_cast<const float*>(obs); return D2D_OK; }
+  if (format != D2D_OBS_U8) { d2d_set_error("unknown obs_format %d", format); return D2D_EINVAL; }
+  if (!sgn_in) { d2d_set_error("obs_format D2D_OBS_U8 needs obs_signed"); return D2D_EINVAL; }
+  if (reinterpret_cast<uintptr_t>(obs) & 15) { d2d_set_error("the obs record must be 16-byte aligned"); return D2D_EINVAL; }
+  (void)obs_dim;
+  rec = static_cast<const uint8_t*>(obs); sgn = sgn_in;
+  return D2D_OK;
+}

@@ -45,6 +45,8 @@ struct EnvArgs {
   const void* flips;
   const uint8_t* arrivals;
   float* obs;
+  uint8_t* rec;   // comb: compact obs record [E][N][rec_bytes] (D2D_RECORD_BYTES(F))
+  int rec_bytes;
   float* state;
   int32_t* reward;
   void* ack;
@@ -459,6 +461,48 @@ __global__ __launch_bounds__(kMaxAgents) void comb_kernel(EnvArgs a) {
       if (nrows > 0) wave_flush(a.obs + ((size_t)blockIdx.x * N + k0) * F, lds_obs, nrows * F, a.flags & 1u);
     } else if (wave_nenv > 0) {
       wave_flush(a.obs + (size_t)wave_env0 * N * F, lds_obs, wave_nenv * N * F, a.flags & 1u);
+    }
+  }
+  // ---- the same row as the compact record: one byte per obs column (packet counts and channel
+  // bits unsigned, acks int8), zero-padded to rec_bytes.  Built in registers (the column of a byte
+  // is fixed by the unrolled position; w_k, C are wave-uniform) and stored by each lane as whole
+  // 16-byte words: the rows of a wave's agents are contiguous, so the stores coalesce fully.
+  if (a.rec && L.active) {
+    const int w = ag.obs_width;
+    const uint32_t ack_neg = ~(ack_one | ack_zero) & cmask;
+    // byte value of obs column p >= w (channel bits, acks, padding)
+    auto tail_byte = [&](int p) -> uint32_t {
+      const int m = p - w;
+      if (m < C) return (h_pre >> m) & 1u;
+      const int c = m - C;
+      if (c < C) return ((ack_one >> c) & 1u) | (((ack_neg >> c) & 1u) * 0xFFu);
+      return 0u;
+    };
+    uint4* dst = reinterpret_cast<uint4*>(a.rec + row * (size_t)a.rec_bytes);
+    uint32_t v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      uint32_t word = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = 4 * q + j;
+        const uint32_t bb = p < 4 * DW ? (b.w[(p < 4 * DW ? p : 0) >> 2] >> (8 * (p & 3))) & 0xFFu : 0u;
+        word |= (p < w ? bb : tail_byte(p)) << (8 * j);
+      }
+      v[q] = word;
+    }
+    dst[0] = make_uint4(v[0], v[1], v[2], v[3]);
+    dst[1] = make_uint4(v[4], v[5], v[6], v[7]);
+    for (int q32 = 1; q32 < a.rec_bytes / 32; ++q32) {  // columns >= 32: channel bits and acks only
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) word |= tail_byte(32 * q32 + 4 * q + j) << (8 * j);
+        v[q] = word;
+      }
+      dst[2 * q32] = make_uint4(v[0], v[1], v[2], v[3]);
+      dst[2 * q32 + 1] = make_uint4(v[4], v[5], v[6], v[7]);
     }
   }
   // state = [concat_k B'[k,:d_k], channel_state (post-evolve).flatten(), acknack] (207-209)
@@ -1002,7 +1046,13 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
   if (rp) { a.flips = rp->flips; a.arrivals = rp->arrivals; }
   a.gather = d->gather;
   a.rng_off = d->rng_offset;
-  if (out) { a.obs = out->obs; a.state = out->state; a.reward = out->reward; a.ack = out->ack; a.success = out->success; }
+  if (out) {
+    a.obs = out->obs; a.state = out->state; a.reward = out->reward; a.ack = out->ack; a.success = out->success;
+    a.rec = out->obs_record;
+  }
+  a.rec_bytes = D2D_RECORD_BYTES(a.F);
+  if (a.rec && !comb) { d2d_set_error("obs_record is implemented for the combinatorial env only"); return D2D_EUNSUPPORTED; }
+  if (a.rec && (reinterpret_cast<uintptr_t>(a.rec) & 15)) { d2d_set_error("obs_record must be 16-byte aligned"); return D2D_EINVAL; }
   draw_mask(d, reset ? 0 : t, a.draw);
   a.flags = store_flags();
   const bool large = a.N > kWave;

@@ -110,19 +110,53 @@ __device__ void load_gru_images(float* wih_s, float* whh_s, const GruW& w, int k
   }
 }
 
-// x tile of one window step: lane (g, i) <- x[env i][16q + 4g + r] (q < IT, r < 4), the bias
-// column F = 1, columns past F = 0.  `off0` = float offset of the obs row (slot, e0, agent k),
-// `row_stride` = floats between consecutive envs (N * F); rows of envs >= E read 0 through the
-// range-checked buffer descriptor (zero: the x of a front-padding step, bias column only).
+// The rollout buffer as the GRU kernels read it: fp32 rows [..][N][F] or (u8) the env kernel's
+// compact record [..][N][RB] (D2D_OBS_U8: one byte per input, int8 on the columns sgn marks).
+struct ObsView {
+  const uint8_t* base;
+  int64_t rows;          // T * E * N
+  int RB, N, F, u8;      // row bytes (4 F or D2D_RECORD_BYTES(F))
+  const uint32_t* sgn;   // u8: [N][RB / 32] int8-column masks
+};
+
+// agent k's int8-column masks of the record (wave-uniform: scalar registers, not VGPRs the update
+// kernel cannot spare); bit of column col = bit col & 31 of word col >> 5
 template <int IT>
-__device__ __forceinline__ void load_x(float (&x)[IT][4], const float* obs, size_t off0, int64_t total_floats,
-                                       int row_stride, int F, int g, int i, bool env_ok, bool zero) {
-  const size_t row0 = off0;
-  const int64_t rest = (total_floats - (int64_t)row0) * 4;
+struct XSigns {
+  uint32_t w[(IT + 1) / 2];
+  __device__ __forceinline__ XSigns(const ObsView& ov, int k) {
+#pragma unroll
+    for (int c = 0; c < (IT + 1) / 2; ++c) w[c] = ov.u8 ? ov.sgn[(size_t)k * (ov.RB >> 5) + c] : 0u;
+  }
+  __device__ __forceinline__ uint32_t bit(int col) const { return (w[col >> 5] >> (col & 31)) & 1u; }
+};
+
+// x tile of one window step: lane (g, i) <- x[env i][16q + 4g + r] (q < IT, r < 4), the bias
+// column F = 1, columns past F = 0.  `row0` = row index (slot, e0, agent k) of env e0; consecutive
+// envs are N rows apart; rows of envs >= E read 0 through the range-checked buffer descriptor
+// (zero: the x of a front-padding step, bias column only).
+template <int IT>
+__device__ __forceinline__ void load_x(float (&x)[IT][4], const ObsView& ov, size_t row0, const XSigns<IT>& sg, int g,
+                                       int i, bool env_ok, bool zero) {
+  const int64_t rest = (ov.rows - (int64_t)row0) * ov.RB;
   const uint32_t nbytes = zero || rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
   const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(obs + row0), 0, nbytes, 0x00020000);
-  const uint32_t vbase = env_ok ? (uint32_t)(i * row_stride) * 4u : 0x80000000u;
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(ov.base + row0 * ov.RB), 0, nbytes, 0x00020000);
+  const uint32_t vbase = env_ok ? (uint32_t)(i * ov.N * ov.RB) : 0x80000000u;
+  const int F = ov.F;
+  if (ov.u8) {  // wave-uniform; the record row is zero past F
+#pragma unroll
+    for (int q = 0; q < IT; ++q) {
+      const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vbase + (uint32_t)(16 * q + 4 * g), 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = 16 * q + 4 * g + r;
+        const float v = rec_byte(w, r, sg.bit(col));
+        x[q][r] = col == F ? 1.f : v;
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < IT; ++q)
 #pragma unroll
@@ -131,6 +165,19 @@ __device__ __forceinline__ void load_x(float (&x)[IT][4], const float* obs, size
       const float v = uf(__builtin_amdgcn_raw_buffer_load_b32(rsrc, vbase + 4u * (uint32_t)col, 0, 0));
       x[q][r] = col < F ? v : col == F ? 1.f : 0.f;
     }
+}
+
+// One input of the transposed x operand: column col = 16q + i of the row `vb` bytes past rsrc's base
+template <int IT>
+__device__ __forceinline__ float load_xt(const __amdgpu_buffer_rsrc_t& rsrc, uint32_t vb, const ObsView& ov,
+                                         const XSigns<IT>& sg, int q, int col) {
+  if (ov.u8) {
+    const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(rsrc, vb + (uint32_t)col, 0, 0);
+    const float v = sg.bit(col) ? (float)(int8_t)b : (float)b;
+    return col == ov.F ? 1.f : v;
+  }
+  const float v = uf(__builtin_amdgcn_raw_buffer_load_b32(rsrc, vb + 4u * (uint32_t)col, 0, 0));
+  return col < ov.F ? v : col == ov.F ? 1.f : 0.f;
 }
 
 // Pre-activations of one step: rz[T] (T < 2 HT: input + recurrent + both biases of r / z rows),

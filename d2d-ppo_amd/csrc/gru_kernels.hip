@@ -28,8 +28,7 @@ struct GruArgs {
   int T, E, N, F, H, A, L, ep_len, kind;
   int slot0, n_slots, padded, env_tiles;  // tiles: slots [slot0, slot0 + n_slots) x ceil(E / 16)
   GruW w;
-  const float* obs;                       // [T][E][N][F]
-  int64_t obs_floats;                     // T * E * N * F
+  ObsView ov;                             // the rollout buffer [T][E][N]: fp32 rows or compact record
   // ---- policy kernel
   MlpArgs ep;                             // epilogue view: ep.E = n_slots * E (slot-major samples)
   float* value_out;                       // kind 2: [N][n_slots * E]
@@ -71,6 +70,7 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
   const uint32_t rng = (MODE == kModeSample && a.ep.rng_off) ? a.ep.rng_step + *a.ep.rng_off : a.ep.rng_step;
   const SwzOff<IW> oi(g, i);
   const SwzOff<HW> oh(g, i);
+  const XSigns<IT> xsg(a.ov, k);
   __syncthreads();
 
   const int n_tiles = a.n_slots * a.env_tiles;
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
     for (int j = 0; j < pad + S; ++j) {
       const bool zero = j < pad;
       const int row_slot = zero ? lo : lo + (j - pad);
-      load_x<IT>(x, a.obs, (((size_t)row_slot * E + e0) * N + k) * F, a.obs_floats, N * F, F, g, i, ok, zero);
+      load_x<IT>(x, a.ov, ((size_t)row_slot * E + e0) * N + k, xsg, g, i, ok, zero);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
       gru_preact<HT, IT, true>(wih_s + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
@@ -224,6 +224,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   const float* wimg = a.wimg + (size_t)k * 3 * HW * (16 * IT);
   const SwzOff<16 * IT> oi(g, i);  // (unused: W_ih comes from the global image)
   const SwzOff<HW> oh(g, i);
+  const XSigns<IT> xsg(a.ov, k);
   const size_t wave_id = (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave;
   float* hist = a.hist + wave_id * (size_t)L * 64 * 4 * HT;
   float* hacc = a.hacc + wave_id * (size_t)GruHeadAcc<HT>::NV * 64;
@@ -241,7 +242,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     const int lo = slot - S + 1;
     const int pad = L - S;  // training windows: front-zero-padded to L (preprocess_input_for_rnn)
     const GruIn in = load_gru_in<KIND>(a, slot, env, k, ok);
-    auto row_of = [&](int j) { return (((size_t)(j < pad ? lo : lo + j - pad) * E + e0) * N + k) * F; };
+    auto row_of = [&](int j) { return ((size_t)(j < pad ? lo : lo + j - pad) * E + e0) * N + k; };
 
     // ---- forward over the window; h_j (j < L - 1) to the wave's scratch
     float h[HT][4];
@@ -251,7 +252,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       for (int r = 0; r < 4; ++r) h[t][r] = 0.f;
     for (int j = 0; j < L; ++j) {
       float x[IT][4];
-      load_x<IT>(x, a.obs, row_of(j), a.obs_floats, N * F, F, g, i, ok, j < pad);
+      load_x<IT>(x, a.ov, row_of(j), xsg, g, i, ok, j < pad);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
       gru_preact<HT, IT, false>(wimg + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
@@ -367,9 +368,9 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
         }
       }
       const bool zero = j < pad;
-      const size_t xoff = row_of(j);
+      const size_t xrow = row_of(j);
       float x[IT][4];
-      load_x<IT>(x, a.obs, xoff, a.obs_floats, N * F, F, g, i, ok, zero);
+      load_x<IT>(x, a.ov, xrow, xsg, g, i, ok, zero);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
       const float* wh = whh_s + z;
@@ -411,17 +412,13 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
         for (int s4 = 0; s4 < 4; ++s4) {
           const int ee = 4 * s4 + g;
           const bool eok = e0 + ee < E;
-          const int64_t rest = (a.obs_floats - (int64_t)xoff) * 4;
+          const int64_t rest = (a.ov.rows - (int64_t)xrow) * a.ov.RB;
           const uint32_t nbytes = zero || rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
-          const __amdgpu_buffer_rsrc_t rsrc =
-              __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.obs + xoff), 0, nbytes, 0x00020000);
-          const uint32_t vb = eok ? (uint32_t)(ee * N * F) * 4u : 0x80000000u;
+          const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<uint8_t*>(a.ov.base + xrow * a.ov.RB), 0, nbytes, 0x00020000);
+          const uint32_t vb = eok ? (uint32_t)(ee * N * a.ov.RB) : 0x80000000u;
 #pragma unroll
-          for (int U = 0; U < IT; ++U) {
-            const int col = 16 * U + i;
-            const float v = uf(__builtin_amdgcn_raw_buffer_load_b32(rsrc, vb + 4u * (uint32_t)col, 0, 0));
-            xt[U][s4] = col < F ? v : col == F ? 1.f : 0.f;
-          }
+          for (int U = 0; U < IT; ++U) xt[U][s4] = load_xt<IT>(rsrc, vb, a.ov, xsg, U, 16 * U + i);
         }
 #pragma unroll
         for (int T = 0; T < 3 * HT; ++T) {
@@ -637,7 +634,7 @@ static void launch_policy_it(const GruArgs& a, dim3 grid, hipStream_t s) {
   else launch_policy_kind<HT, 4>(a, grid, s);
 }
 
-static int check_gru_desc(const d2d_gru_desc* d) {
+static int check_gru_desc(const d2d_gru_desc* d, const void* obs) {
   if (!d || !d->w_ih || !d->w_hh || !d->b_ih || !d->b_hh || !d->w1 || !d->b1 || !d->w2 || !d->b2) {
     d2d_set_error("d2d_gru: NULL weight");
     return D2D_EINVAL;
@@ -648,27 +645,36 @@ static int check_gru_desc(const d2d_gru_desc* d) {
   if (d->kind < 0 || d->kind > 2) { d2d_set_error("kind=%d outside [0,2]", d->kind); return D2D_EINVAL; }
   if (d->kind != 2 && (d->n_out < 1 || d->n_out > 16)) { d2d_set_error("n_out=%d outside [1,16]", d->n_out); return D2D_EUNSUPPORTED; }
   if (d->history_len < 1 || d->episode_length < 1) { d2d_set_error("history_len / episode_length < 1"); return D2D_EINVAL; }
-  return D2D_OK;
+  const float* f32;
+  const uint8_t* rec;
+  const uint32_t* sgn;
+  return obs_format_args(d->obs_format, d->obs_signed, d->obs_dim, obs, f32, rec, sgn);
 }
 
-static GruArgs make_gru_args(const d2d_gru_desc* d, int T, const float* obs) {
+static GruArgs make_gru_args(const d2d_gru_desc* d, int T, const void* obs) {
   GruArgs a{};
   a.T = T; a.E = d->n_envs; a.N = d->n_agents; a.F = d->obs_dim; a.H = d->hidden;
   a.A = d->kind == 2 ? 1 : d->n_out; a.kind = d->kind;
   a.L = d->history_len; a.ep_len = d->episode_length;
   a.env_tiles = (a.E + 15) / 16;
   a.w = {d->w_ih, d->w_hh, d->b_ih, d->b_hh, d->w1, d->b1, d->w2, d->b2};
-  a.obs = obs;
-  a.obs_floats = (int64_t)T * a.E * a.N * a.F;
+  const float* f32;
+  const uint8_t* rec;
+  const uint32_t* sgn;
+  obs_format_args(d->obs_format, d->obs_signed, d->obs_dim, obs, f32, rec, sgn);  // checked by check_gru_desc
+  a.ov.base = rec ? rec : reinterpret_cast<const uint8_t*>(f32);
+  a.ov.rows = (int64_t)T * a.E * a.N;
+  a.ov.RB = rec ? D2D_RECORD_BYTES(a.F) : 4 * a.F;
+  a.ov.N = a.N; a.ov.F = a.F; a.ov.u8 = rec ? 1 : 0; a.ov.sgn = sgn;
   a.inv_A = 1.f / (float)a.A;
   a.mask_bytes = a.A <= 8 ? 1 : a.A <= 16 ? 2 : 4;
   return a;
 }
 
-extern "C" int d2d_policy_gru(const d2d_gru_desc* d, int32_t T, const float* obs, int32_t slot0, int32_t n_slots,
+extern "C" int d2d_policy_gru(const d2d_gru_desc* d, int32_t T, const void* obs, int32_t slot0, int32_t n_slots,
                               int32_t padded, const void* forced, uint32_t rng_step, int32_t deterministic,
                               void* actions, float* out, void* stream) {
-  int rc = check_gru_desc(d);
+  int rc = check_gru_desc(d, obs);
   if (rc) return rc;
   if (!obs || !out || (d->kind != 2 && !actions)) { d2d_set_error("d2d_policy_gru: NULL buffer"); return D2D_EINVAL; }
   if (T < 1 || slot0 < 0 || n_slots < 0 || slot0 + n_slots > T) {
@@ -729,12 +735,12 @@ static void launch_grad_kind(const GruArgs& a, dim3 grid, hipStream_t s) {
   else hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruValue>), grid, dim3(256), 0, s, a);
 }
 
-extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const float* obs, const void* actions,
+extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, const void* actions,
                             const float* logp_old, const int64_t* logp_strides, const float* weight,
                             const int64_t* weight_strides, float clip, float beta, float scale, float* g_w_ih,
                             float* g_w_hh, float* g_b_ih, float* g_b_hh, float* g_w1, float* g_b1, float* g_w2,
                             float* g_b2, float* stats, float* workspace, int64_t workspace_floats, void* stream) {
-  int rc = check_gru_desc(d);
+  int rc = check_gru_desc(d, obs);
   if (rc) return rc;
   if (d->obs_dim + 1 > 32) { d2d_set_error("d2d_gru_grad: obs_dim=%d > 31", d->obs_dim); return D2D_EUNSUPPORTED; }
   if (!obs || !weight || !weight_strides || !g_w_ih || !g_w_hh || !g_b_ih || !g_b_hh || !g_w1 || !g_b1 || !g_w2 ||

@@ -80,6 +80,12 @@ __device__ __forceinline__ void store_mask(void* base, size_t cell, int mask_byt
   else reinterpret_cast<uint32_t*>(base)[cell] = v;
 }
 
+// Compact obs record (D2D_OBS_U8, env kernel's obs_record): byte j (compile-time) of record word w
+// as a network input, int8 when sgn (the ack columns) else uint8.  v_bfe_i32 / v_cvt_f32_ubyte.
+__device__ __forceinline__ float rec_byte(uint32_t w, int j, bool sgn) {
+  return sgn ? (float)((int32_t)(w << (24 - 8 * j)) >> 24) : (float)((w >> (8 * j)) & 0xFFu);
+}
+
 // Exact bf16 split.  Every fp32 operand v is written EXACTLY as v = vh + vm + vl with
 // three bf16 parts (8 + 8 + 8 significand bits, truncation split: vh = v with the low 16 bits
 // cleared, vm likewise of v - vh, vl = v - vh - vm).  A product w.x is then the sum of the nine

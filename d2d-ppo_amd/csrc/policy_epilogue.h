@@ -16,7 +16,9 @@ struct MlpArgs {
   uint64_t seed, env_base;
   const float *w1, *b1, *w2, *b2, *v1, *c1, *v2, *c2;
   const float* obs;      // [E][N][F]
-  const void* forced;    // NULL or comb mask [E][N] / chsel uint8 [E][N]
+  const uint8_t* rec;    // D2D_OBS_U8: compact record [E][N][32 KC] instead of obs
+  const uint32_t* sgn;   // D2D_OBS_U8: [N][KC] int8-column masks
+  const void* forced;   // NULL or comb mask [E][N] / chsel uint8 [E][N]
   void* act_out;         // comb mask [E][N] / chsel uint8 [E][N]
   float* logp_out;       // [N][E]
   float* value_out;      // [N][E] or NULL

@@ -140,9 +140,13 @@ __global__ __launch_bounds__(256) void policy_mlp_kernel(MlpArgs a) {
 // the columns past F hold the next agent's inputs and are zeroed by stage_inputs().
 // hipcc does not order the DMA's LDS write before the ds_read of the slot, so the waits are
 // explicit, counted s_waitcnt vmcnt (see the loop).
-// ring depth: 6 tiles at KC = 1; 4 at KC = 2 (the counted wait must stay below vmcnt's 63)
-template <int KC>
-constexpr int ring_tiles() { return KC == 1 ? 6 : 4; }
+// ring depth: 6 tiles at KC = 1; 4 at KC = 2 (the counted wait must stay below vmcnt's 63);
+// the compact record (U8) brings a row chunk in 2 DMAs instead of 8: 8 / 6 tiles
+template <int KC, bool U8>
+constexpr int ring_tiles() { return U8 ? (KC == 1 ? 8 : 6) : (KC == 1 ? 6 : 4); }
+// dwords of one lane's row chunk (8 inputs): 8 floats or 8 record bytes
+template <bool U8>
+constexpr int chunk_dwords() { return U8 ? 2 : 8; }
 
 
 // x[c][j] <- slot, then input F := 1.0 (layer-1 bias input) and inputs past F := 0
@@ -160,8 +164,26 @@ __device__ __forceinline__ void stage_inputs(float (&x)[KC][8], const float* slo
     }
 }
 
-// KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even)
-template <int KC, int HT, int KIND, bool CRITIC, int MODE>
+// The same from a ring slot of compact-record words [c][2][lane]: the record row is zero past F
+// (the env kernel pads it), so only the bias input is set; sg[c] = this lane's 8 int8-column bits
+template <int KC>
+__device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* slot, int lane, int F, int g,
+                                             const uint32_t (&sg)[KC]) {
+#pragma unroll
+  for (int c = 0; c < KC; ++c) {
+    const uint32_t d0 = slot[(c * 2) * 64 + lane], d1 = slot[(c * 2 + 1) * 64 + lane];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = 32 * c + 8 * g + j;
+      const float v = rec_byte(j < 4 ? d0 : d1, j & 3, (sg[c] >> j) & 1u);
+      x[c][j] = col == F ? 1.f : v;
+    }
+  }
+}
+
+// KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even);
+// U8: the inputs are the env kernel's compact obs record (D2D_OBS_U8)
+template <int KC, int HT, int KIND, bool CRITIC, int MODE, bool U8>
 __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpArgs a) {  // waves / SIMD
   static_assert(HT % 2 == 0, "layer 2 consumes hidden tiles in pairs");
   // Philox step of the launch, read once before the obs pipeline starts (the optional device
@@ -252,31 +274,43 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
 
   // Two obs register sets alternate (loop unrolled by two), so each tile's loads are issued two
   // tiles ahead of their use without a register copy that would wait on them early.
-  constexpr int RING = ring_tiles<KC>();
-  __shared__ float ring[4][RING][KC][8][64];
-  const float* wbase = a.obs + ((size_t)wave_env0 * N + k) * F;
-  const int64_t total = (int64_t)a.E * N * F * 4, done = ((int64_t)wave_env0 * N + k) * F * 4;
+  constexpr int RING = ring_tiles<KC, U8>();
+  constexpr int DPC = chunk_dwords<U8>();
+  __shared__ float ring[4][RING][KC][DPC][64];
+  // row bytes: F floats, or the record's 32 KC bytes
+  const int RB = U8 ? 32 * KC : 4 * F;
+  const uint8_t* wbase = (U8 ? a.rec : reinterpret_cast<const uint8_t*>(a.obs)) + ((size_t)wave_env0 * N + k) * RB;
+  const int64_t total = (int64_t)a.E * N * RB, done = ((int64_t)wave_env0 * N + k) * RB;
   const int64_t rest = total - done;
   const uint32_t nbytes = rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
-  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(wbase), 0, nbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(wbase), 0, nbytes, 0x00020000);
+  // int8 columns of this lane's record bytes (agent k, columns 32c + 8g + j)
+  uint32_t sg[KC];
+#pragma unroll
+  for (int c = 0; c < KC; ++c) sg[c] = U8 ? (a.sgn[(size_t)k * KC + c] >> (8 * g)) & 0xFFu : 0u;
   auto issue = [&](int t) {
     // look-ahead tiles past this wave's last are still issued (the counted waits need a fixed
     // DMA count) but aimed outside the descriptor's range: no memory traffic, zeros
-    const uint32_t vo = t < tiles ? ((uint32_t)((t * 16 + i) * N * F) + 8 * g) * 4 : 0x80000000u;
+    const uint32_t vo = t < tiles ? (uint32_t)((t * 16 + i) * N * RB) + (U8 ? 8 : 32) * g : 0x80000000u;
 #pragma unroll
     for (int c = 0; c < KC; ++c)
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < DPC; ++j)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rsrc, (__attribute__((address_space(3))) void*)&ring[wave][t % RING][c][j][0], 4,
-            vo + 4 * (32 * c + j), 0, 0, 0);
+            vo + (U8 ? 32 * c + 4 * j : 4 * (32 * c + j)), 0, 0, 0);
   };
   // layers 1-2 of one tile -> (pre-scaled) logits lg and critic value
   auto tile = [&](int tt, f32x4& lg, float& value) {
       float xc[KC][8];
-      stage_inputs<KC>(xc, &ring[wave][tt % RING][0][0][0], lane, F, g);
+      if constexpr (U8)
+        stage_record<KC>(xc, reinterpret_cast<const uint32_t*>(&ring[wave][tt % RING][0][0][0]), lane, F, g, sg);
+      else
+        stage_inputs<KC>(xc, &ring[wave][tt % RING][0][0][0], lane, F, g);
       // bf16 high parts of the inputs; the residual parts only when some input of the tile is
-      // not bf16-exact (wave-uniform branch, rare for env observations)
+      // not bf16-exact (wave-uniform branch, rare for env observations; never for the record,
+      // whose integers in [-128, 255] are bf16-exact)
       bf16x8 xh[KC];
       uint32_t low = 0;
 #pragma unroll
@@ -289,7 +323,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
         }
         xh[c] = as_frag(u);
       }
-      const bool x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;  // wave-uniform
+      const bool x_exact = U8 || __builtin_amdgcn_ballot_w64(low != 0) == 0;  // wave-uniform
 
       // ---- layer 1 (actor, critic), transposed: H^T = W1' . [X | 1]^T; the three weight parts
       // against the high parts of X, then (rarely) the residual terms of X
@@ -353,14 +387,14 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
       }
   };
   // every wave runs the same even number of tiles (tiles past E read zeros and store nothing), so
-  // the DMA count between a tile's issue and its wait is fixed: RING - 2 tiles of KC * 8 DMAs
+  // the DMA count between a tile's issue and its wait is fixed: RING - 2 tiles of KC * DPC DMAs
   // (anything else issued in between -- the stores -- only makes the counted wait stricter)
   static_assert(RING >= 4 && RING % 2 == 0, "two tiles per iteration");
   for (int t = 0; t < RING - 2; ++t) issue(t);
   for (int tt = 0; tt < tiles; tt += 2) {
     issue(tt + RING - 2);
     issue(tt + RING - 1);
-    wait_vmem<(RING - 2) * KC * 8>();  // tiles tt, tt + 1 have landed
+    wait_vmem<(RING - 2) * KC * DPC>();  // tiles tt, tt + 1 have landed
     __builtin_amdgcn_sched_barrier(0);        // no LDS read of the slots moves above the wait
     f32x4 lg0, lg1;
     float v0, v1;
@@ -407,12 +441,18 @@ static int launch_policy_f32(const MlpArgs& a, hipStream_t s) {
   return D2D_OK;
 }
 
+template <int KC, int HT, int KIND, bool CRITIC, bool U8>
+static void launch_split_fmt(const MlpArgs& a, dim3 grid, hipStream_t s) {
+  if (a.forced) hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeForced, U8>), grid, dim3(256), 0, s, a);
+  else if (a.deterministic)
+    hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeDeterministic, U8>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeSample, U8>), grid, dim3(256), 0, s, a);
+}
+
 template <int KC, int HT, int KIND, bool CRITIC>
 static void launch_split_mode(const MlpArgs& a, dim3 grid, hipStream_t s) {
-  if (a.forced) hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeForced>), grid, dim3(256), 0, s, a);
-  else if (a.deterministic)
-    hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeDeterministic>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeSample>), grid, dim3(256), 0, s, a);
+  if (a.rec) launch_split_fmt<KC, HT, KIND, CRITIC, true>(a, grid, s);
+  else launch_split_fmt<KC, HT, KIND, CRITIC, false>(a, grid, s);
 }
 
 template <int KC, int HT>
@@ -428,7 +468,7 @@ static int launch_policy_split(const MlpArgs& a, hipStream_t s) {
   return D2D_OK;
 }
 
-extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const float* obs, const void* forced, uint32_t rng_step,
+extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const void* obs, const void* forced, uint32_t rng_step,
                                    int32_t deterministic, void* actions, float* logp, float* value, void* stream) {
   if (!d || !obs || !actions || !logp || !d->w1 || !d->b1 || !d->w2 || !d->b2) {
     d2d_set_error("d2d_policy_mlp_step: NULL argument");
@@ -450,12 +490,15 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const float* obs, cons
   while (a.envs_per_wave > 32 && (int64_t)d->n_envs * d->n_agents / a.envs_per_wave < 2048) a.envs_per_wave >>= 1;
   a.rng_step = rng_step; a.rng_off = d->rng_offset; a.seed = d->seed; a.env_base = d->env_base;
   a.w1 = d->w1; a.b1 = d->b1; a.w2 = d->w2; a.b2 = d->b2; a.v1 = d->v1; a.c1 = d->c1; a.v2 = d->v2; a.c2 = d->c2;
-  a.obs = obs; a.forced = forced; a.act_out = actions; a.logp_out = logp; a.value_out = value;
+  const int rc = obs_format_args(d->obs_format, d->obs_signed, d->obs_dim, obs, a.obs, a.rec, a.sgn);
+  if (rc) return rc;
+  a.forced = forced; a.act_out = actions; a.logp_out = logp; a.value_out = value;
   a.mask_bytes = d->n_out <= 8 ? 1 : d->n_out <= 16 ? 2 : 4;
   if (a.E == 0 || a.N == 0) return D2D_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int ht = (a.H + 15) / 16;
   if (g_policy_f32_mfma || a.F + 1 > 64) {
+    if (a.rec) { d2d_set_error("the fp32-MFMA policy kernel reads fp32 obs only"); return D2D_EUNSUPPORTED; }
     const int ks = (a.F + 3) / 4;
     if (ks <= 8) return ht <= 2 ? launch_policy_f32<8, 2>(a, s) : launch_policy_f32<8, 4>(a, s);
     return ht <= 2 ? launch_policy_f32<16, 2>(a, s) : launch_policy_f32<16, 4>(a, s);

@@ -57,7 +57,9 @@ struct UpdArgs {
   int tiles_per_t, n_tiles, G, P;
   float inv_A, clip_lo, clip_hi, beta, scale;
   const float *w1, *b1, *w2, *b2;  // actor (Policy) or critic (Value: A = 1)
-  const float* obs;                 // [T][E][N][F]
+  const float* obs;                 // [T][E][N][F] (D2D_OBS_F32)
+  const uint8_t* rec;               // [T][E][N][32 KC] compact record (D2D_OBS_U8)
+  const uint32_t* sgn;              // [N][KC] int8-column masks of the record
   const void* actions;              // [T][E][N] masks (kind 0) / ids (kind 1)
   const float* logp_old;            // actor: element (t, e, k) at t*st[0] + e*st[1] + k*st[2]
   const float* weight;              // actor: advantage / M; critic: return target
@@ -126,32 +128,53 @@ __device__ __forceinline__ float ld_st(const float* base, const int64_t (&st)[3]
 // 32 samples (lane (g, i) of half s: x[sample 16s + i][32c + 8g + j], raw -- columns past F and
 // samples past E are fixed up by stage_tile) and the per-sample action / logp_old / weight of
 // the epilogue lanes (PAIR: lane (g, i) serves sample 16 (g >> 1) + i; else sample 16s + i).
-template <int KC, bool PAIR>
+// Raw input rows of one tile, lane (g, i) of half s: inputs 32c + 8g .. 32c + 8g + 7 of sample
+// 16s + i as 8 fp32 words, or (U8) as the 8 bytes of the compact record (2 words, a quarter of
+// the registers held across the look-ahead)
+template <int KC, bool U8>
+struct XRows {
+  uint32_t v[2][KC][U8 ? 2 : 8];
+  // input j of chunk c of half s; sg[c] = this lane's 8 int8-column bits
+  __device__ __forceinline__ float at(int s, int c, int j, const uint32_t (&sg)[KC]) const {
+    if constexpr (U8) return rec_byte(v[s][c][j >> 2], j & 3, (sg[c] >> j) & 1u);
+    else return uf(v[s][c][j]);
+  }
+};
+
+template <int KC, bool PAIR, bool U8>
 struct ActorIn {
-  float x[2][KC][8];
+  XRows<KC, U8> x;
   uint32_t act[PAIR ? 1 : 2];
   float lo[PAIR ? 1 : 2], w[PAIR ? 1 : 2];
 };
 
 // obs rows of one tile through a range-checked buffer descriptor based at the tile's first row
 // (rows of samples past E, or past the buffer, read as 0)
-template <int KC>
-__device__ __forceinline__ void load_rows(float (&x)[2][KC][8], const UpdArgs& a, int t, int e0, int k, int g,
-                                          int i) {
+template <int KC, bool U8>
+__device__ __forceinline__ void load_rows(XRows<KC, U8>& x, const UpdArgs& a, int t, int e0, int k, int g, int i) {
+  const int RB = U8 ? 32 * KC : 4 * a.F;  // row bytes
   const size_t row0 = ((size_t)t * a.E + e0) * a.N + k;
-  const int64_t rest = ((int64_t)a.T * a.E * a.N - (int64_t)row0) * a.F * 4;
+  const int64_t rest = ((int64_t)a.T * a.E * a.N - (int64_t)row0) * RB;
   const uint32_t nbytes = rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
-  const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.obs + row0 * a.F), 0, nbytes, 0x00020000);
+  const uint8_t* base = (U8 ? a.rec : reinterpret_cast<const uint8_t*>(a.obs)) + row0 * RB;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), 0, nbytes, 0x00020000);
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int e = e0 + 16 * s + i;
-    const uint32_t vo = e < a.E ? ((uint32_t)((16 * s + i) * a.N * a.F) + 8 * g) * 4 : 0x80000000u;
+    const uint32_t vo = e < a.E ? (uint32_t)((16 * s + i) * a.N * RB) + (U8 ? 8 : 32) * g : 0x80000000u;
 #pragma unroll
     for (int c = 0; c < KC; ++c)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[s][c][j] = uf(__builtin_amdgcn_raw_buffer_load_b32(rsrc, vo + 4 * (32 * c + j), 0, 0));
+      for (int j = 0; j < (U8 ? 2 : 8); ++j)
+        x.v[s][c][j] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vo + (U8 ? 32 * c + 4 * j : 4 * (32 * c + j)), 0, 0);
   }
+}
+
+// this lane's int8-column bits of agent k's record (columns 32c + 8g + j, j < 8)
+template <int KC, bool U8>
+__device__ __forceinline__ void record_signs(uint32_t (&sg)[KC], const UpdArgs& a, int k, int g) {
+#pragma unroll
+  for (int c = 0; c < KC; ++c) sg[c] = U8 ? (a.sgn[(size_t)k * KC + c] >> (8 * g)) & 0xFFu : 0u;
 }
 
 __device__ __forceinline__ uint32_t load_action(const UpdArgs& a, int t, int e, int k) {
@@ -160,11 +183,12 @@ __device__ __forceinline__ uint32_t load_action(const UpdArgs& a, int t, int e, 
   return load_mask(a.actions, cell, a.mask_bytes);
 }
 
-template <int KC, bool PAIR>
-__device__ __forceinline__ void load_actor_in(ActorIn<KC, PAIR>& in, const UpdArgs& a, int tile, int k, int g, int i) {
+template <int KC, bool PAIR, bool U8>
+__device__ __forceinline__ void load_actor_in(ActorIn<KC, PAIR, U8>& in, const UpdArgs& a, int tile, int k, int g,
+                                              int i) {
   const int t = tile / a.tiles_per_t;
   const int e0 = (tile - t * a.tiles_per_t) * 32;
-  load_rows<KC>(in.x, a, t, e0, k, g, i);
+  load_rows<KC, U8>(in.x, a, t, e0, k, g, i);
 #pragma unroll
   for (int s = 0; s < (PAIR ? 1 : 2); ++s) {
     const int e = e0 + 16 * (PAIR ? (g >> 1) : s) + i;
@@ -211,7 +235,7 @@ __device__ __forceinline__ void lds_row(float (&v)[8], const float (*xw)[XS], in
 // made once; x is bf16-exact on env observations, so 3 MFMAs per 16x16x32); the logits on
 // v_mfma_f32_16x16x4_f32 (an exact fmaf chain) straight from the accumulator registers; the
 // weight gradients dW1, dW2 on two-way RNE splits of their per-tile operands.
-template <int KC, int HT, int KIND, bool PAIR>
+template <int KC, int HT, int KIND, bool PAIR, bool U8>
 __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(UpdArgs a) {
   constexpr int QT = 2 * KC;  // input tiles of 16 in dW1
   const int lane = threadIdx.x & 63;
@@ -307,11 +331,13 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   const int stride = a.G * 4;
   const int tile0 = by * 4 + wave;
   int e0 = 0;
-  ActorIn<KC, PAIR> cur;  // per-sample scalars of the tile being computed
+  ActorIn<KC, PAIR, U8> cur;  // per-sample scalars of the tile being computed
   bf16x8 xh[2][KC];
+  uint32_t sg[KC];
+  record_signs<KC, U8>(sg, a, k, g);
   // ---- inputs: bias column, zeros past it; bf16 high parts; the tile to LDS for dW1.
   // Returns whether every input of the tile is bf16-exact (wave-uniform).
-  auto stage = [&](const ActorIn<KC, PAIR>& src, int tile) -> bool {
+  auto stage = [&](const ActorIn<KC, PAIR, U8>& src, int tile) -> bool {
     const int t = tile / a.tiles_per_t;
     e0 = (tile - t * a.tiles_per_t) * 32;
 #pragma unroll
@@ -329,14 +355,15 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int col = 32 * c + 8 * g + j;
-          xr[j] = col < F ? src.x[s][c][j] : col == F ? 1.f : 0.f;
+          xr[j] = col < F ? src.x.at(s, c, j, sg) : col == F ? 1.f : 0.f;
           low |= fbits(xr[j]) & 0xFFFFu;
         }
         xh[s][c] = hi_frag(xr);
         *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g]) = f32x4{xr[0], xr[1], xr[2], xr[3]};
         *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g + 4]) = f32x4{xr[4], xr[5], xr[6], xr[7]};
       }
-    return __builtin_amdgcn_ballot_w64(low != 0) == 0;
+    // the record's integers in [-128, 255] are bf16-exact
+    return U8 || __builtin_amdgcn_ballot_w64(low != 0) == 0;
   };
 
   {
@@ -516,12 +543,12 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
     // next tile's loads are issued as soon as this tile is staged); a tile with fractional inputs
     // is deferred to a second pass over the wave's tiles with the general body, so neither body
     // carries the other's live ranges or branches.
-    ActorIn<KC, PAIR> in;
+    ActorIn<KC, PAIR, U8> in;
     bool deferred = false;
-    if (tile0 < a.n_tiles) load_actor_in<KC, PAIR>(in, a, tile0, k, g, i);
+    if (tile0 < a.n_tiles) load_actor_in<KC, PAIR, U8>(in, a, tile0, k, g, i);
     for (int tile = tile0; tile < a.n_tiles; tile += stride) {
       const bool x_exact = stage(in, tile);
-      if (tile + stride < a.n_tiles) load_actor_in<KC, PAIR>(in, a, tile + stride, k, g, i);
+      if (tile + stride < a.n_tiles) load_actor_in<KC, PAIR, U8>(in, a, tile + stride, k, g, i);
       if (x_exact)
         body(std::true_type{});
       else
@@ -530,7 +557,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
     }
     if (deferred) {
       for (int tile = tile0; tile < a.n_tiles; tile += stride) {
-        load_actor_in<KC, PAIR>(in, a, tile, k, g, i);
+        load_actor_in<KC, PAIR, U8>(in, a, tile, k, g, i);
         if (!stage(in, tile)) body(std::false_type{});
         lds_order();
       }
@@ -603,17 +630,17 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
 // Value(x) = V2 relu(V1 x + c1) + c2, loss = mean (v - R)^2 (ippo.py:210-216).  Hidden layer in
 // the sample-on-rows orientation only: the 64 -> 1 layer is a per-lane product + a 16-lane row
 // sum, dV1 = dHv^T . X as in the actor.  a.w2 = V2 [N][1][H], a.b2 = c2 [N][1], a.weight = R.
-template <int KC>
+template <int KC, bool U8>
 struct CriticIn {
-  float x[2][KC][8];
+  XRows<KC, U8> x;
   float R[2][4];  // returns of samples 16s + 4g + r
 };
 
-template <int KC>
-__device__ __forceinline__ void load_critic_in(CriticIn<KC>& in, const UpdArgs& a, int tile, int k, int g, int i) {
+template <int KC, bool U8>
+__device__ __forceinline__ void load_critic_in(CriticIn<KC, U8>& in, const UpdArgs& a, int tile, int k, int g, int i) {
   const int t = tile / a.tiles_per_t;
   const int e0 = (tile - t * a.tiles_per_t) * 32;
-  load_rows<KC>(in.x, a, t, e0, k, g, i);
+  load_rows<KC, U8>(in.x, a, t, e0, k, g, i);
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -623,7 +650,7 @@ __device__ __forceinline__ void load_critic_in(CriticIn<KC>& in, const UpdArgs& 
     }
 }
 
-template <int KC, int HT>
+template <int KC, int HT, bool U8>
 __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(UpdArgs a) {
   constexpr int QT = 2 * KC;
   const int lane = threadIdx.x & 63;
@@ -676,7 +703,9 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
   int e0 = 0;
   float R[2][4];
   bf16x8 xh[2][KC];
-  auto stage = [&](const CriticIn<KC>& src, int tile) -> bool {
+  uint32_t sg[KC];
+  record_signs<KC, U8>(sg, a, k, g);
+  auto stage = [&](const CriticIn<KC, U8>& src, int tile) -> bool {
     const int t = tile / a.tiles_per_t;
     e0 = (tile - t * a.tiles_per_t) * 32;
 #pragma unroll
@@ -692,14 +721,15 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int col = 32 * c + 8 * g + j;
-          xr[j] = col < F ? src.x[s][c][j] : col == F ? 1.f : 0.f;
+          xr[j] = col < F ? src.x.at(s, c, j, sg) : col == F ? 1.f : 0.f;
           low |= fbits(xr[j]) & 0xFFFFu;
         }
         xh[s][c] = hi_frag(xr);
         *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g]) = f32x4{xr[0], xr[1], xr[2], xr[3]};
         *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g + 4]) = f32x4{xr[4], xr[5], xr[6], xr[7]};
       }
-    return __builtin_amdgcn_ballot_w64(low != 0) == 0;
+    // the record's integers in [-128, 255] are bf16-exact
+    return U8 || __builtin_amdgcn_ballot_w64(low != 0) == 0;
   };
   {
     // the tile body (XE: bf16-exact inputs), deferred tiles as in the actor kernel
@@ -786,12 +816,12 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
         }
       }
     };
-    CriticIn<KC> in;
+    CriticIn<KC, U8> in;
     bool deferred = false;
-    if (tile0 < a.n_tiles) load_critic_in<KC>(in, a, tile0, k, g, i);
+    if (tile0 < a.n_tiles) load_critic_in<KC, U8>(in, a, tile0, k, g, i);
     for (int tile = tile0; tile < a.n_tiles; tile += stride) {
       const bool x_exact = stage(in, tile);
-      if (tile + stride < a.n_tiles) load_critic_in<KC>(in, a, tile + stride, k, g, i);
+      if (tile + stride < a.n_tiles) load_critic_in<KC, U8>(in, a, tile + stride, k, g, i);
       lds_order();
       if (x_exact)
         body(std::true_type{});
@@ -801,7 +831,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
     }
     if (deferred) {
       for (int tile = tile0; tile < a.n_tiles; tile += stride) {
-        load_critic_in<KC>(in, a, tile, k, g, i);
+        load_critic_in<KC, U8>(in, a, tile, k, g, i);
         const bool x_exact = stage(in, tile);
         lds_order();
         if (!x_exact) body(std::false_type{});
@@ -892,7 +922,7 @@ extern "C" int64_t d2d_ppo_workspace(int32_t n_agents, int32_t T, int32_t n_envs
   return (int64_t)G * n_agents * P;
 }
 
-static int check_update(const d2d_mlp_desc* d, int T, const float* obs, const void* grads_w1, float* workspace,
+static int check_update(const d2d_mlp_desc* d, int T, const void* obs, const void* grads_w1, float* workspace,
                         int64_t ws, int critic) {
   if (!d || !obs || !d->w1 || !d->b1 || !d->w2 || !d->b2 || !grads_w1 || !workspace) {
     d2d_set_error("NULL argument");
@@ -903,12 +933,17 @@ static int check_update(const d2d_mlp_desc* d, int T, const float* obs, const vo
   if (d->obs_dim < 1 || d->obs_dim + 1 > 64) { d2d_set_error("obs_dim=%d outside [1,63]", d->obs_dim); return D2D_EUNSUPPORTED; }
   if (!critic && (d->n_out < 1 || d->n_out > 16)) { d2d_set_error("n_out=%d outside [1,16]", d->n_out); return D2D_EUNSUPPORTED; }
   if (!critic && d->kind != 0 && d->kind != 1) { d2d_set_error("kind must be 0 or 1"); return D2D_EINVAL; }
+  const float* f32;
+  const uint8_t* rec;
+  const uint32_t* sgn;
+  const int rc = obs_format_args(d->obs_format, d->obs_signed, d->obs_dim, obs, f32, rec, sgn);
+  if (rc) return rc;
   const int64_t need = d2d_ppo_workspace(d->n_agents, T, d->n_envs, d->obs_dim, d->hidden, critic ? 1 : d->n_out);
   if (ws < need) { d2d_set_error("workspace %lld < %lld floats", (long long)ws, (long long)need); return D2D_EINVAL; }
   return D2D_OK;
 }
 
-static UpdArgs make_args(const d2d_mlp_desc* d, int T, const float* obs, float* workspace, int critic) {
+static UpdArgs make_args(const d2d_mlp_desc* d, int T, const void* obs, float* workspace, int critic) {
   UpdArgs a{};
   a.T = T; a.E = d->n_envs; a.N = d->n_agents; a.F = d->obs_dim; a.H = d->hidden;
   a.A = critic ? 1 : d->n_out; a.kind = d->kind;
@@ -919,7 +954,7 @@ static UpdArgs make_args(const d2d_mlp_desc* d, int T, const float* obs, float* 
   a.P = a.H * a.F + a.H + a.A * a.H + a.A + 2;
   a.inv_A = 1.f / (float)a.A;
   a.w1 = d->w1; a.b1 = d->b1; a.w2 = d->w2; a.b2 = d->b2;
-  a.obs = obs;
+  obs_format_args(d->obs_format, d->obs_signed, d->obs_dim, obs, a.obs, a.rec, a.sgn);  // checked by check_update
   a.partial = workspace;
   return a;
 }
@@ -933,17 +968,28 @@ static int launch_reduce(const UpdArgs& a, float* gw1, float* gb1, float* gw2, f
   return D2D_OK;
 }
 
-template <int KC, int HT>
-static void launch_actor(const UpdArgs& a, hipStream_t s) {
+template <int KC, int HT, bool U8>
+static void launch_actor_fmt(const UpdArgs& a, hipStream_t s) {
   dim3 grid(a.N, a.G);
   const bool pair = a.A <= 8;
-  if (a.kind == 0 && pair) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, true>), grid, dim3(256), 0, s, a);
-  else if (a.kind == 0) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, false>), grid, dim3(256), 0, s, a);
-  else if (pair) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, true>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, false>), grid, dim3(256), 0, s, a);
+  if (a.kind == 0 && pair) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, true, U8>), grid, dim3(256), 0, s, a);
+  else if (a.kind == 0) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, false, U8>), grid, dim3(256), 0, s, a);
+  else if (pair) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, true, U8>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, false, U8>), grid, dim3(256), 0, s, a);
+}
+template <int KC, int HT>
+static void launch_actor(const UpdArgs& a, hipStream_t s) {
+  if (a.rec) launch_actor_fmt<KC, HT, true>(a, s);
+  else launch_actor_fmt<KC, HT, false>(a, s);
+}
+template <int KC, int HT>
+static void launch_critic(const UpdArgs& a, hipStream_t s) {
+  dim3 grid(a.N, a.G);
+  if (a.rec) hipLaunchKernelGGL((ppo_critic_grad_kernel<KC, HT, true>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((ppo_critic_grad_kernel<KC, HT, false>), grid, dim3(256), 0, s, a);
 }
 
-extern "C" int d2d_ppo_actor_grad(const d2d_mlp_desc* d, int32_t T, const float* obs, const void* actions,
+extern "C" int d2d_ppo_actor_grad(const d2d_mlp_desc* d, int32_t T, const void* obs, const void* actions,
                                   const float* logp_old, const int64_t* logp_strides, const float* weight,
                                   const int64_t* weight_strides, float clip, float beta, float scale, float* gw1,
                                   float* gb1, float* gw2, float* gb2, float* stats, float* workspace,
@@ -977,7 +1023,7 @@ extern "C" int d2d_ppo_actor_grad(const d2d_mlp_desc* d, int32_t T, const float*
   return launch_reduce(a, gw1, gb1, gw2, gb2, stats, s);
 }
 
-extern "C" int d2d_ppo_critic_grad(const d2d_mlp_desc* d, int32_t T, const float* obs, const float* returns,
+extern "C" int d2d_ppo_critic_grad(const d2d_mlp_desc* d, int32_t T, const void* obs, const float* returns,
                                    const int64_t* return_strides, float scale, float* gw1, float* gb1, float* gw2,
                                    float* gb2, float* stats, float* workspace, int64_t workspace_floats,
                                    void* stream) {
@@ -999,13 +1045,10 @@ extern "C" int d2d_ppo_critic_grad(const d2d_mlp_desc* d, int32_t T, const float
     return launch_reduce(a, gw1, gb1, gw2, gb2, stats, s);
   }
   const int ht = (a.H + 15) / 16;
-  dim3 grid(a.N, a.G);
   if (a.F + 1 <= 32) {
-    if (ht <= 2) hipLaunchKernelGGL((ppo_critic_grad_kernel<1, 2>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((ppo_critic_grad_kernel<1, 4>), grid, dim3(256), 0, s, a);
+    if (ht <= 2) launch_critic<1, 2>(a, s); else launch_critic<1, 4>(a, s);
   } else {
-    if (ht <= 2) hipLaunchKernelGGL((ppo_critic_grad_kernel<2, 2>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((ppo_critic_grad_kernel<2, 4>), grid, dim3(256), 0, s, a);
+    if (ht <= 2) launch_critic<2, 2>(a, s); else launch_critic<2, 4>(a, s);
   }
   D2D_CHECK_HIP(hipGetLastError());
   return launch_reduce(a, gw1, gb1, gw2, gb2, stats, s);

@@ -36,7 +36,8 @@ def refuse_ablation(what):
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 4
+ABI_VERSION = 5
+D2D_OBS_F32, D2D_OBS_U8 = 0, 1
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
 
@@ -57,7 +58,12 @@ class EnvState(ctypes.Structure):
 
 
 class EnvOut(ctypes.Structure):
-    _fields_ = [("obs", _p), ("state", _p), ("reward", _p), ("ack", _p), ("success", _p)]
+    _fields_ = [("obs", _p), ("state", _p), ("reward", _p), ("ack", _p), ("success", _p), ("obs_record", _p)]
+
+
+def record_bytes(obs_dim):
+    """D2D_RECORD_BYTES: row bytes of the compact obs record (32 per chunk of 32 network inputs)."""
+    return 32 * ((int(obs_dim) + 32) // 32)
 
 
 class EnvReplay(ctypes.Structure):
@@ -68,7 +74,8 @@ class MlpDesc(ctypes.Structure):
     _fields_ = [("n_agents", ctypes.c_int32), ("n_envs", ctypes.c_int32), ("obs_dim", ctypes.c_int32),
                 ("hidden", ctypes.c_int32), ("n_out", ctypes.c_int32), ("kind", ctypes.c_int32),
                 ("w1", _p), ("b1", _p), ("w2", _p), ("b2", _p), ("v1", _p), ("c1", _p), ("v2", _p), ("c2", _p),
-                ("seed", ctypes.c_uint64), ("env_base", ctypes.c_uint64), ("rng_offset", _p)]
+                ("seed", ctypes.c_uint64), ("env_base", ctypes.c_uint64), ("rng_offset", _p),
+                ("obs_format", ctypes.c_int32), ("reserved", ctypes.c_int32), ("obs_signed", _p)]
 
 
 class GruDesc(ctypes.Structure):
@@ -76,7 +83,8 @@ class GruDesc(ctypes.Structure):
                 ("hidden", ctypes.c_int32), ("n_out", ctypes.c_int32), ("kind", ctypes.c_int32),
                 ("history_len", ctypes.c_int32), ("episode_length", ctypes.c_int32),
                 ("w_ih", _p), ("w_hh", _p), ("b_ih", _p), ("b_hh", _p), ("w1", _p), ("b1", _p), ("w2", _p), ("b2", _p),
-                ("seed", ctypes.c_uint64), ("env_base", ctypes.c_uint64), ("rng_offset", _p)]
+                ("seed", ctypes.c_uint64), ("env_base", ctypes.c_uint64), ("rng_offset", _p),
+                ("obs_format", ctypes.c_int32), ("reserved", ctypes.c_int32), ("obs_signed", _p)]
 
 
 # name -> (restype, argtypes)

@@ -9,6 +9,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from .record import ObsRecord, signed_masks
 from .spec import COMB, SINGLE, EnvSpec
 
 _KIND_ID = {COMB: _lib.D2D_ENV_COMBINATORIAL, "chsel": _lib.D2D_ENV_CHANNEL_SELECTION, SINGLE: _lib.D2D_ENV_SINGLE}
@@ -55,6 +56,10 @@ class EnvBatch:
         self._state = None
         self._ack = None
         self._success = None
+        self._record = None
+        # int8-column masks of the compact obs record (combinatorial env only)
+        self._signed_host = signed_masks(s).view(np.int32) if s.kind == COMB else None
+        self.signed = torch.from_numpy(self._signed_host).to(dev) if s.kind == COMB else None
         self.gather = torch.from_numpy(spec.gather_map(self.lib)).to(dev) if s.kind == SINGLE else None
         # device word added to rng_step by every kernel of this batch (and by the learner's policy
         # kernel): 0 for eager calls, set before replaying a captured rollout graph
@@ -89,6 +94,21 @@ class EnvBatch:
             else:
                 self._ack = torch.zeros((self.E, s.C + 1), dtype=torch.float64, device=self.device)
         return self._ack
+
+    @property
+    def record(self):
+        """Persistent compact obs record [E][N][R] (ObsRecord, combinatorial env only)."""
+        if self._record is None:
+            self._record = self.record_buffer(())
+        return self._record
+
+    def record_buffer(self, lead):
+        """A zeroed ObsRecord [*lead][E][N][R] for rollout buffers (slice [t] per step)."""
+        if self.signed is None:
+            raise NotImplementedError("the compact obs record exists for the combinatorial env only")
+        r = ObsRecord.empty(tuple(lead) + (self.E,), self.spec, self.signed, self.device)
+        r._host = self._signed_host
+        return r
 
     @property
     def success(self):
@@ -129,8 +149,17 @@ class EnvBatch:
             keep.append(arrivals)
         return _lib.EnvReplay(fp, ap), keep
 
-    def _out(self, want_obs, want_state, want_ack, want_success, out_obs, out_state, out_reward):
+    def _out(self, want_obs, want_state, want_ack, want_success, out_obs, out_state, out_reward, out_record=None):
         s = self.spec
+        if isinstance(out_obs, ObsRecord):
+            out_obs, out_record = None, out_obs
+        rec = None
+        if out_record is not None:
+            if out_record.signed is not self.signed and not np.array_equal(out_record.signed_host(), self._signed_host):
+                raise ValueError("out_record carries another env's signed-column masks")
+            self._check_out(out_record.data, (self.E, s.N, _lib.record_bytes(s.F)), torch.uint8, "out_record")
+            rec = out_record.data
+            want_obs = False
         obs = out_obs if out_obs is not None else (self.obs if want_obs else None)
         state = out_state if out_state is not None else (self.state if want_state else None)
         reward = out_reward if out_reward is not None else self.reward
@@ -139,8 +168,8 @@ class EnvBatch:
         self._check_out(reward, (self.E,), torch.int32, "reward")
         ack = self.ack if want_ack else None
         succ = self.success if want_success else None
-        o = _lib.EnvOut(*(None if t is None else t.data_ptr() for t in (obs, state, reward, ack, succ)))
-        return o, dict(obs=obs, state=state, reward=reward, ack=ack, success=succ)
+        o = _lib.EnvOut(*(None if t is None else t.data_ptr() for t in (obs, state, reward, ack, succ, rec)))
+        return o, dict(obs=obs if rec is None else out_record, state=state, reward=reward, ack=ack, success=succ)
 
     # ---------------------------------------------------------- reset/step
     def reset(self, want_obs=True, want_state=False, replay_arrivals=None, out_obs=None, out_state=None,

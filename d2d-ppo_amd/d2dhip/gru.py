@@ -6,6 +6,7 @@ import ctypes
 import torch
 
 from . import _lib
+from .record import set_format
 
 KIND = {"sigmoid": 0, "softmax": 1, None: 2}
 
@@ -27,14 +28,13 @@ def desc(params, n_envs, kind, history_len, episode_length, seed=0, env_base=0, 
 
 def policy(params, obs, kind, history_len, episode_length, slot0, n_slots, padded=False, forced=None, rng_step=0,
            deterministic=False, seed=0, env_base=0, rng_offset=None, actions_out=None, out=None):
-    """obs [T][E][N][F] (the rollout buffer).  kind 'sigmoid' / 'softmax' (actors): returns
+    """obs [T][E][N][F] (the rollout buffer: fp32, or the env kernel's ObsRecord).  kind 'sigmoid' / 'softmax' (actors): returns
     (actions [n_slots][E][N], logp [N][n_slots * E]); kind None (value): returns values [N][n_slots * E]."""
     lib = _lib.require_gpu()
     T, E, N, F = obs.shape
-    if obs.dtype != torch.float32 or not obs.is_contiguous():
-        raise ValueError("obs must be a contiguous float32 [T][E][N][F] tensor")
     k = KIND[kind]
     d = desc(params, E, k, history_len, episode_length, seed, env_base, rng_offset)
+    optr = set_format(d, obs)
     dev = obs.device
     if out is None:
         out = torch.empty((N, n_slots * E), dtype=torch.float32, device=dev)
@@ -44,7 +44,7 @@ def policy(params, obs, kind, history_len, episode_length, slot0, n_slots, padde
         mb = 1 if (k == 1 or A <= 8) else 2 if A <= 16 else 4
         dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[mb]
         act = actions_out if actions_out is not None else torch.empty((n_slots, E, N), dtype=dt, device=dev)
-    rc = lib.d2d_policy_gru(ctypes.byref(d), T, obs.data_ptr(), int(slot0), int(n_slots), 1 if padded else 0,
+    rc = lib.d2d_policy_gru(ctypes.byref(d), T, optr, int(slot0), int(n_slots), 1 if padded else 0,
                             None if forced is None else forced.data_ptr(), int(rng_step) & 0xFFFFFFFF,
                             1 if deterministic else 0, None if act is None else act.data_ptr(), out.data_ptr(),
                             _lib.stream_ptr())
@@ -87,6 +87,7 @@ def grads(params, obs, kind, history_len, episode_length, weight, actions=None, 
     T, E, N, F = obs.shape
     k = KIND[kind]
     d = desc(params, E, k, history_len, episode_length)
+    optr = set_format(d, obs)
     dev = obs.device
     grads = grads if grads is not None else {n: torch.empty_like(v) for n, v in params.items()}
     if stats is None:
@@ -94,7 +95,7 @@ def grads(params, obs, kind, history_len, episode_length, weight, actions=None, 
     scale = 1.0 / (T * E) if scale is None else scale
     ws = _ws.get(lib.d2d_gru_grad_workspace(ctypes.byref(d), T), dev)
     lo_st = _arr(_strides3(logp_old, T, E, N)) if logp_old is not None else None
-    rc = lib.d2d_gru_grad(ctypes.byref(d), T, obs.data_ptr(), None if actions is None else actions.data_ptr(),
+    rc = lib.d2d_gru_grad(ctypes.byref(d), T, optr, None if actions is None else actions.data_ptr(),
                           None if logp_old is None else logp_old.data_ptr(), lo_st, weight.data_ptr(),
                           _arr(_strides3(weight, T, E, N)), float(clip), float(beta), float(scale),
                           *(grads[n].data_ptr() for n in ("w_ih", "w_hh", "b_ih", "b_hh", "w1", "b1", "w2", "b2")),

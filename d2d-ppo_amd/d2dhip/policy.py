@@ -2,19 +2,20 @@
 import torch
 
 from . import _lib
+from .record import set_format
 
 
 def policy_mlp_step(actor, obs, kind, critic=None, forced=None, rng_step=0, deterministic=False, seed=0,
                     env_base=0, actions=None, logp=None, value=None):
     """actor/critic: dicts of agent-stacked fp32 tensors w1 [N][H][F], b1 [N][H], w2 [N][A][H], b2 [N][A]
-    (critic: A = 1).  obs [E][N][F] fp32.  kind 'comb' (Bernoulli, masks out) or 'chsel' (Categorical, ids out).
+    (critic: A = 1).  obs [E][N][F] fp32, or the env kernel's ObsRecord of that shape.  kind 'comb' (Bernoulli, masks out) or 'chsel' (Categorical, ids out).
     Returns (actions [E][N], logp [N][E], value [N][E] or None)."""
     lib = _lib.require_gpu()
     N, H, F = actor["w1"].shape
     A = actor["w2"].shape[1]
     E = obs.shape[0]
     dev = obs.device
-    assert tuple(obs.shape) == (E, N, F) and obs.dtype == torch.float32 and obs.is_contiguous()
+    assert tuple(obs.shape) == (E, N, F) and obs.is_contiguous()
     for t in list(actor.values()) + (list(critic.values()) if critic else []):
         assert t.dtype == torch.float32 and t.is_contiguous() and t.device == dev
     k = 0 if kind == "comb" else 1
@@ -33,7 +34,8 @@ def policy_mlp_step(actor, obs, kind, critic=None, forced=None, rng_step=0, dete
                         p(critic["w1"]) if critic else None, p(critic["b1"]) if critic else None,
                         p(critic["w2"]) if critic else None, p(critic["b2"]) if critic else None, int(seed),
                         int(env_base))
-    rc = lib.d2d_policy_mlp_step(desc, obs.data_ptr(), None if forced is None else forced.contiguous().data_ptr(),
+    optr = set_format(desc, obs)
+    rc = lib.d2d_policy_mlp_step(desc, optr, None if forced is None else forced.contiguous().data_ptr(),
                                  int(rng_step), 1 if deterministic else 0, actions.data_ptr(), logp.data_ptr(),
                                  None if value is None else value.data_ptr(), _lib.stream_ptr())
     _lib.check(rc, "d2d_policy_mlp_step")

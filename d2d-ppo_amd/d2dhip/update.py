@@ -8,6 +8,7 @@ import ctypes
 import torch
 
 from . import _lib
+from .record import set_format
 
 
 def _strides3(t, T, E, N):
@@ -56,13 +57,13 @@ def _grads_like(net, grads):
 def actor_grads(net, obs, actions, logp_old, weight, kind, clip=0.1, beta=0.01, scale=None, grads=None,
                 stats=None, workspace=None):
     """net: dict w1 [N][H][F], b1 [N][H], w2 [N][A][H], b2 [N][A] (fp32, contiguous).
-    obs [T][E][N][F]; actions [T][E][N] masks (kind 'comb') or uint8 ids ('chsel');
+    obs [T][E][N][F] fp32 or an ObsRecord of that shape; actions [T][E][N] masks (kind 'comb') or uint8 ids ('chsel');
     logp_old / weight: [T][E][N] or [N][E*T] (env-major), any strides.
     Returns (grads dict like net, stats [N][2] = (sum min-surrogate, sum entropy))."""
     lib = _lib.require_gpu()
     T, E, N, F = obs.shape
     dev = obs.device
-    assert obs.dtype == torch.float32 and obs.is_contiguous()
+    assert obs.is_contiguous()
     assert actions.shape == (T, E, N) and actions.is_contiguous()
     for t in net.values():
         assert t.dtype == torch.float32 and t.is_contiguous() and t.device == dev
@@ -78,7 +79,8 @@ def actor_grads(net, obs, actions, logp_old, weight, kind, clip=0.1, beta=0.01, 
     need = lib.d2d_ppo_workspace(N, T, E, F, H, A)
     ws = (workspace or _ws).get(need, dev)
     desc = _desc(net, E, k)
-    rc = lib.d2d_ppo_actor_grad(desc, T, obs.data_ptr(), actions.data_ptr(), logp_old.data_ptr(),
+    optr = set_format(desc, obs)
+    rc = lib.d2d_ppo_actor_grad(desc, T, optr, actions.data_ptr(), logp_old.data_ptr(),
                                 _arr(_strides3(logp_old, T, E, N)), weight.data_ptr(),
                                 _arr(_strides3(weight, T, E, N)), float(clip), float(beta), float(scale),
                                 grads["w1"].data_ptr(), grads["b1"].data_ptr(), grads["w2"].data_ptr(),
@@ -94,7 +96,7 @@ def critic_grads(net, obs, returns, scale=None, grads=None, stats=None, workspac
     lib = _lib.require_gpu()
     T, E, N, F = obs.shape
     dev = obs.device
-    assert obs.dtype == torch.float32 and obs.is_contiguous()
+    assert obs.is_contiguous()
     for t in net.values():
         assert t.dtype == torch.float32 and t.is_contiguous() and t.device == dev
     B = T * E
@@ -106,7 +108,8 @@ def critic_grads(net, obs, returns, scale=None, grads=None, stats=None, workspac
     need = lib.d2d_ppo_workspace(N, T, E, F, H, 1)
     ws = (workspace or _ws).get(need, dev)
     desc = _desc(net, E, 0, critic=True)
-    rc = lib.d2d_ppo_critic_grad(desc, T, obs.data_ptr(), returns.data_ptr(), _arr(_strides3(returns, T, E, N)),
+    optr = set_format(desc, obs)
+    rc = lib.d2d_ppo_critic_grad(desc, T, optr, returns.data_ptr(), _arr(_strides3(returns, T, E, N)),
                                  float(scale), grads["w1"].data_ptr(), grads["b1"].data_ptr(),
                                  grads["w2"].data_ptr(), grads["b2"].data_ptr(), stats.data_ptr(), ws.data_ptr(),
                                  ws.numel(), _lib.stream_ptr())

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 4  /* 4: GRU entry points (d2d_policy_gru, d2d_gru_grad) */
+#define D2D_ABI_VERSION 5  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format) */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -105,7 +105,17 @@ typedef struct d2d_env_out {  /* any field may be NULL */
     int32_t* reward;    /* [E]  |successful users| (single: the ack); broadcast to all agents by the host */
     void* ack;          /* comb int8 [E][C] in {-1,0,1}; chsel double [E][C+1]; single int8 [E] */
     uint8_t* success;   /* [E][N] 1 if agent k delivered a packet this slot */
+    /* comb only: the compact obs record [E][N][D2D_RECORD_BYTES(obs_dim)] (16-byte aligned), the obs
+     * row above one byte per column: packet counts and channel bits as uint8, the acks (columns
+     * [w_k + C, w_k + 2C)) as int8, zeros past the row.  Every obs value of this env is an integer
+     * in those ranges, so the record is exact; consumers take it with obs_format = D2D_OBS_U8. */
+    uint8_t* obs_record;
 } d2d_env_out;
+
+/* Row bytes of the compact obs record: 32 per chunk of 32 network inputs (obs columns + the
+ * layer-1 bias input), the chunking of the MLP / GRU kernels. */
+#define D2D_RECORD_BYTES(obs_dim) (32 * (((obs_dim) + 32) / 32))
+enum { D2D_OBS_F32 = 0, D2D_OBS_U8 = 1 };
 
 typedef struct d2d_env_replay {  /* parity mode; both NULL = Philox production stream */
     const void* flips;        /* comb mask [E][N]; chsel uint32 [E] */
@@ -218,9 +228,15 @@ typedef struct d2d_mlp_desc {
     const float *v1, *c1, *v2, *c2;
     uint64_t seed, env_base;
     const uint32_t* rng_offset;  /* optional device uint32 added to rng_step (graph replays), as in d2d_env_desc */
+    /* obs_format D2D_OBS_F32: every `obs` argument below is float [..][N][obs_dim];
+     * D2D_OBS_U8: it is the env kernel's compact record [..][N][D2D_RECORD_BYTES(obs_dim)] and
+     * obs_signed (device uint32 [N][D2D_RECORD_BYTES(obs_dim) / 32]) marks agent k's int8 columns:
+     * bit b of word c = column 32c + b is signed (the acks), every other byte is uint8. */
+    int32_t obs_format, reserved;
+    const uint32_t* obs_signed;
 } d2d_mlp_desc;
 
-int d2d_policy_mlp_step(const d2d_mlp_desc* desc, const float* obs, const void* forced, uint32_t rng_step,
+int d2d_policy_mlp_step(const d2d_mlp_desc* desc, const void* obs, const void* forced, uint32_t rng_step,
                         int32_t deterministic, void* actions, float* logp, float* value, void* stream);
 
 /* ---- fused PPO update: per-agent gradients of the MLP learners' losses ----
@@ -241,12 +257,12 @@ int d2d_policy_mlp_step(const d2d_mlp_desc* desc, const float* obs, const void* 
  * workspace: d2d_ppo_workspace(...) floats of device scratch.  Deterministic (fixed-order sums). */
 int64_t d2d_ppo_workspace(int32_t n_agents, int32_t T, int32_t n_envs, int32_t obs_dim, int32_t hidden,
                           int32_t n_out);
-int d2d_ppo_actor_grad(const d2d_mlp_desc* desc, int32_t T, const float* obs, const void* actions,
+int d2d_ppo_actor_grad(const d2d_mlp_desc* desc, int32_t T, const void* obs, const void* actions,
                        const float* logp_old, const int64_t* logp_strides, const float* weight,
                        const int64_t* weight_strides, float clip, float beta, float scale, float* gw1, float* gb1,
                        float* gw2, float* gb2, float* stats, float* workspace, int64_t workspace_floats,
                        void* stream);
-int d2d_ppo_critic_grad(const d2d_mlp_desc* desc, int32_t T, const float* obs, const float* returns,
+int d2d_ppo_critic_grad(const d2d_mlp_desc* desc, int32_t T, const void* obs, const float* returns,
                         const int64_t* return_strides, float scale, float* gw1, float* gb1, float* gw2, float* gb2,
                         float* stats, float* workspace, int64_t workspace_floats, void* stream);
 
@@ -267,13 +283,15 @@ typedef struct d2d_gru_desc {
     const float *w_ih, *w_hh, *b_ih, *b_hh, *w1, *b1, *w2, *b2;
     uint64_t seed, env_base;
     const uint32_t* rng_offset;  /* optional device uint32 added to rng_step (graph replays) */
+    int32_t obs_format, reserved;  /* as in d2d_mlp_desc: D2D_OBS_U8 = obs is the compact record */
+    const uint32_t* obs_signed;
 } d2d_gru_desc;
 
 /* Behaviour policy / value over slots [slot0, slot0 + n_slots) of the buffer (ippo.py:154-191 per agent,
  * batch 1, replaced for all agents and envs): kinds 0/1 write actions [n_slots][n_envs][N] (masks / ids;
  * forced != NULL: evaluate these instead of sampling; deterministic: p > 0.5 / argmax) and log-probs
  * out [N][n_slots * n_envs]; kind 2 writes the values to out [N][n_slots * n_envs]. */
-int d2d_policy_gru(const d2d_gru_desc* desc, int32_t T, const float* obs, int32_t slot0, int32_t n_slots,
+int d2d_policy_gru(const d2d_gru_desc* desc, int32_t T, const void* obs, int32_t slot0, int32_t n_slots,
                    int32_t padded, const void* forced, uint32_t rng_step, int32_t deterministic, void* actions,
                    float* out, void* stream);
 
@@ -283,7 +301,7 @@ int d2d_policy_gru(const d2d_gru_desc* desc, int32_t T, const float* obs, int32_
  * or (sum (V - R)^2, 0).  actions / logp_old / weight strides as d2d_ppo_actor_grad; weight = advantage
  * or M (kinds 0, 1), return target (kind 2).  obs_dim <= 31.  workspace: d2d_gru_grad_workspace floats. */
 int64_t d2d_gru_grad_workspace(const d2d_gru_desc* desc, int32_t T);
-int d2d_gru_grad(const d2d_gru_desc* desc, int32_t T, const float* obs, const void* actions, const float* logp_old,
+int d2d_gru_grad(const d2d_gru_desc* desc, int32_t T, const void* obs, const void* actions, const float* logp_old,
                  const int64_t* logp_strides, const float* weight, const int64_t* weight_strides, float clip,
                  float beta, float scale, float* g_w_ih, float* g_w_hh, float* g_b_ih, float* g_b_hh, float* g_w1,
                  float* g_b1, float* g_w2, float* g_b2, float* stats, float* workspace, int64_t workspace_floats,

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     for fn in fns:
         assert hasattr(lib, fn), fn
         assert fn in d2dhip.EXPORTED, f"{fn} has no ctypes signature"
-    assert lib.d2d_abi_version() == 4
+    assert lib.d2d_abi_version() == 5
     assert [lib.d2d_mask_bytes(c) for c in (1, 8, 9, 16, 17, 32)] == [1, 1, 2, 2, 4, 4]
     assert [lib.d2d_buffer_words(d) for d in (1, 4, 5, 8, 12, 14, 16, 17, 32)] == [1, 1, 2, 2, 3, 4, 4, 8, 8]
     assert lib.d2d_colstats_workspace(1000, 64) >= 64
@@ -39,10 +39,14 @@ def test_ctypes_structs_match_header_layout():
     from d2dhip.spec import AGENT_DTYPE
     assert AGENT_DTYPE.itemsize == 32
     assert ctypes.sizeof(_lib.EnvDesc) == 8 * 4 + 8 * 2 + 8 * 7
-    assert ctypes.sizeof(_lib.MlpDesc) == 6 * 4 + 8 * 8 + 8 * 2 + 8
-    assert ctypes.sizeof(_lib.EnvState) == 6 * 8 and ctypes.sizeof(_lib.EnvOut) == 5 * 8
+    assert ctypes.sizeof(_lib.MlpDesc) == 6 * 4 + 8 * 8 + 8 * 2 + 8 + 2 * 4 + 8
+    assert ctypes.sizeof(_lib.EnvState) == 6 * 8 and ctypes.sizeof(_lib.EnvOut) == 6 * 8
     assert ctypes.sizeof(_lib.EnvReplay) == 2 * 8
-    assert ctypes.sizeof(_lib.GruDesc) == 8 * 4 + 8 * 8 + 8 * 2 + 8
+    assert ctypes.sizeof(_lib.GruDesc) == 8 * 4 + 8 * 8 + 8 * 2 + 8 + 2 * 4 + 8
+    # D2D_RECORD_BYTES(obs_dim) of the header and its Python mirror
+    txt = open(HEADER).read()
+    assert "#define D2D_RECORD_BYTES(obs_dim) (32 * (((obs_dim) + 32) / 32))" in txt
+    assert [_lib.record_bytes(f) for f in (1, 30, 31, 32, 63, 64)] == [32, 32, 32, 64, 64, 96]
 
 
 def test_library_validates_arguments_without_gpu():
@@ -55,6 +59,53 @@ def test_library_validates_arguments_without_gpu():
     desc = _lib.EnvDesc(0, 2000, 8, 7, 23, 0, 0, 1, 0, 0, None, None, None, None, None, None, None)
     assert lib.d2d_env_reset(ctypes.byref(desc), None, None, None, 0, None) == -2
     assert lib.d2d_gae_scan(10, 1, 0, 1, None, None, None, 0.9, 0.97, 1, None, None, None) == -1
+    # obs_format checks (before any HIP call)
+    w = ctypes.c_void_p(16)
+    md = _lib.MlpDesc(4, 32, 30, 64, 8, 0, w, w, w, w, None, None, None, None, 0, 0, None, 7, 0, None)
+    assert lib.d2d_policy_mlp_step(ctypes.byref(md), w, None, 0, 0, w, w, None, None) == -1
+    assert b"obs_format" in lib.d2d_last_error()
+    md.obs_format = _lib.D2D_OBS_U8
+    assert lib.d2d_policy_mlp_step(ctypes.byref(md), w, None, 0, 0, w, w, None, None) == -1
+    assert b"obs_signed" in lib.d2d_last_error()
+    md.obs_signed = w
+    assert lib.d2d_policy_mlp_step(ctypes.byref(md), ctypes.c_void_p(24), None, 0, 0, w, w, None, None) == -1
+    assert b"aligned" in lib.d2d_last_error()
+    # the record is a combinatorial-env output only
+    dsc = _lib.EnvDesc(1, 4, 3, 7, 11, 0, 0, 1, 0, 0, w, w, w, w, w, None, None)
+    st = _lib.EnvState(w, w, w, w, w, w)
+    out = _lib.EnvOut(None, None, None, None, None, 16)
+    assert lib.d2d_env_reset(ctypes.byref(dsc), ctypes.byref(st), None, ctypes.byref(out), 0, None) == -2
+    assert b"obs_record" in lib.d2d_last_error()
+
+
+def test_record_signed_masks_and_decode():
+    """The int8-column masks mark exactly the ACK columns [w_k + C, w_k + 2C) of every agent's row
+    (combinatorial_env.py:199-206), and ObsRecord.decode maps bytes back to the fp32 obs values."""
+    import torch
+    from d2dhip.record import ObsRecord, signed_masks
+    from d2dhip.spec import EnvSpec
+    d = [7, 14, 3, 14]
+    for homog, C in ((True, 8), (False, 8), (False, 16)):
+        s = EnvSpec("comb", 4, C, d, [0.5] * 4, 2, [1] * 4, [0] * 4, 10, "aperiodic", [], homog, None)
+        m = signed_masks(s)
+        R = 32 * ((s.F + 32) // 32)
+        assert m.shape == (4, R // 32) and m.dtype == np.uint32
+        for k in range(4):
+            cols = [c for c in range(R) if (int(m[k, c // 32]) >> (c % 32)) & 1]
+            assert cols == list(range(int(s.w[k]) + C, int(s.w[k]) + 2 * C))
+        rng = np.random.default_rng(C)
+        obs = np.zeros((3, 4, s.F), dtype=np.float32)
+        for k in range(4):
+            w = int(s.w[k])
+            obs[:, k, :w] = rng.integers(0, 256, size=(3, w))
+            obs[:, k, w:w + C] = rng.integers(0, 2, size=(3, C))
+            obs[:, k, w + C:w + 2 * C] = rng.integers(-1, 2, size=(3, C))
+        raw = np.zeros((3, 4, R), dtype=np.uint8)
+        raw[..., : s.F] = obs.astype(np.int16).astype(np.uint8)
+        rec = ObsRecord(torch.from_numpy(raw), s.F, torch.from_numpy(m.view(np.int32)))
+        assert rec.shape == (3, 4, s.F)
+        assert torch.equal(rec.decode(), torch.from_numpy(obs))
+        assert torch.equal(rec[1:].decode(), torch.from_numpy(obs[1:]))
 
 
 def test_gpu_required_loudly():

@@ -95,7 +95,7 @@ def test_learner_matches_reference(name, E):
     ro = lr._rollout(n_ep, teacher=teacher)
     assert ro.E == E and ro.waves * E == n_ep
     s = env.spec
-    obs = ro.obs.permute(1, 0, 2, 3).reshape(E * ro.T, N, -1).cpu().numpy()      # env-major = reference order
+    obs = ro.obs_f32.permute(1, 0, 2, 3).reshape(E * ro.T, N, -1).cpu().numpy()      # env-major = reference order
     for k in range(N):
         assert np.array_equal(obs[:, k, : s.obs_len[k]], z[f"ro/obs{k}"]), k
     logp = lr._seq(ro.logp).t().cpu().numpy()
@@ -240,7 +240,7 @@ def test_graph_rollout_equals_eager(algo, kind):
         res = []
         for _ in range(3):  # 2 waves each; capture on the first, replay after (buffers are reused)
             ro = lr._rollout(60)
-            res.append((ro.obs.clone(), ro.actions.clone(), ro.logp.clone(), ro.rewards.clone(),
+            res.append((ro.obs_f32.clone(), ro.actions.clone(), ro.logp.clone(), ro.rewards.clone(),
                         None if ro.values is None else ro.values.clone(),
                         None if ro.states is None else ro.states[..., :env.state_space.shape[0]].clone(),  # no pad
                         list(ro.scores), list(ro.ep_rewards)))

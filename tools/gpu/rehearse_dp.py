@@ -48,7 +48,7 @@ def run(algo, n_envs):
     lr = iPPO(env, **kw) if algo == "ippo" else D2DPPO(env, beta_entropy=0.02, **kw)
     assert lr._fused_update_ok()
     ro = lr._rollout(n_envs)
-    out = {"obs": ro.obs, "actions": ro.actions, "logp": ro.logp}
+    out = {"obs": ro.obs_f32, "actions": ro.actions, "logp": ro.logp}
     if algo == "ippo":
         out["adv"], out["ret"] = ro.adv_tne, ro.ret_tne
     else:
