@@ -8,9 +8,12 @@ channel_switch_8 tiled to 64 rows, deadlines [7,14]x32, heterogeneous traffic
 (periodic = {k : k mod 6 < 3}, load 1/2), 65,536 envs per GPU (weak scaling:
 rank r owns envs [r*E, (r+1)*E) with its own Philox counters, no data-path
 collective).  One step = one slot for every env: synthetic actions (Philox
-Bernoulli(0.1) per agent-channel) + the env-step kernel, fp32 obs emitted to
-HBM; every episode_length slots the envs reset (inside the timed loop).
-Inputs are HBM-resident before timing starts.
+Bernoulli(0.1) per agent-channel) + the env-step kernel emitting the observation
+to HBM as the learners consume it: the compact obs record (32 B per agent-step,
+d2dhip/record.py, bit-exact decode to the fp32 obs).  The same K steps with fp32 obs
+rows (the reference-API layout, 120 B per agent-step) are reported as `fp32_obs`.
+Every episode_length slots the envs reset (inside the timed loop).  Inputs are
+HBM-resident before timing starts.
 
 More legs are reported in the same JSON line (they do not change `value`):
   rollout : the iPPO behaviour-policy slot at the same 65,536 envs — agent-stacked
@@ -46,7 +49,8 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "env-steps/sec (agents×envs) + PPO updates/sec, 64 agents × 8 ch, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-BYTES_PER_AGENT_STEP = 172.0   # B_as = 6D + 11C at D=14, C=8
+BYTES_PER_AGENT_STEP = 172.0   # B_as = 6D + 11C at D=14, C=8 (fp32 obs: 4F = 120 B of it)
+RECORD_BYTES_PER_AGENT_STEP = BYTES_PER_AGENT_STEP - 120.0 + 32.0  # the 120 B of fp32 obs -> a 32 B record row
 
 
 def config3_params(episode_length=200):
@@ -208,8 +212,8 @@ class PhaseTimer:
         return out
 
 
-def load_pmc_traffic():
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def load_pmc_traffic(mode="fp32"):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json" if mode == "fp32" else f"pmc_traffic_{mode}.json")
     if not os.path.exists(p):
         return None
     try:
@@ -225,7 +229,9 @@ def rollout_leg(env, args, world):
     lr = iPPO(env, hidden_size=64, gamma=0.6, policy_lr=3e-4, value_lr=1e-3, device=env.batch().device,
               useRNN=False, combinatorial=True)
     b = env.batch()
-    ring = torch.empty((2,) + tuple(b.obs.shape), dtype=torch.float32, device=b.device)
+    # the rollout buffer format the learner runs on (the compact record by default)
+    ring = b.record_buffer((2,)) if lr._record_ok() else torch.empty((2,) + tuple(b.obs.shape), dtype=torch.float32,
+                                                                       device=b.device)
     rew = torch.empty((b.E,), dtype=torch.int32, device=b.device)
     act = b.action_buffer()
     logp = torch.empty((b.spec.N, b.E), dtype=torch.float32, device=b.device)
@@ -268,6 +274,7 @@ def rollout_leg(env, args, world):
     tflops = flop * b.E * b.spec.N / (pol_ms / 1e3) / 1e12
     return {"env_steps_per_s": v, "agent_steps_per_s": v * b.spec.N, "ms_per_step": el / K * 1e3, "steps": K,
             "policy": f"iPPO MLP H=64 actor+critic, 64 agents, Bernoulli sampling, fp32; {path}",
+            "obs_format": "compact record (u8)" if lr._record_ok() else "fp32",
             "policy_kernel_us": pol_ms * 1e3, "env_kernel_us": env_ms * 1e3,
             "policy_flop_per_agent_step": flop, "policy_tflops_fp32_equiv": tflops,
             "policy_frac_of_fp32_matrix_peak": tflops / 157.3}
@@ -672,6 +679,8 @@ def main():
     ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
     ap.add_argument("--ppo-epochs", type=int, default=6)
     ap.add_argument("--train-epochs", type=int, default=4, help="n_epoch of the train leg")
+    ap.add_argument("--env-mode", default="both", choices=["both", "record", "fp32"],
+                    help="obs output of the headline env steps (value = the first of record, fp32)")
     args = ap.parse_args()
 
     params = config3_params(args.episode_length)
@@ -691,47 +700,65 @@ def main():
     b = env.batch()
     N, C = params["n_agents"], params["n_channels"]
     act = b.action_buffer()
-
-    def one_step(ev=None):
-        if b.timestep >= params["episode_length"]:
-            b.reset(want_obs=True)
-        b.sample_actions(0.1, out=act)
-        if ev is not None:
-            ev[0].record()
-        b.step(act, want_obs=True)
-        if ev is not None:
-            ev[1].record()
-
-    b.reset(want_obs=True)
-    for _ in range(args.warmup):
-        one_step()
-    torch.cuda.synchronize()
     K = args.steps
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-    t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier(world)
-    torch.cuda.synchronize()
-    w0 = time.perf_counter()
-    t_start.record()
-    for i in range(K):
-        one_step(evs[i])
-    t_end.record()
-    torch.cuda.synchronize()
-    barrier(world)
-    wall = time.perf_counter() - w0
-    gpu_s = t_start.elapsed_time(t_end) / 1e3
-    kern_ms = np.array([a.elapsed_time(bb) for a, bb in evs])
-    t = max_over_ranks(max(wall, gpu_s), world)
-    kern_avg_ms = max_over_ranks(float(kern_ms.mean()), world)
+
+    def env_phase(mode):
+        """warmup + K timed steps emitting the record ('record') or fp32 obs rows ('fp32')."""
+        out = b.record if mode == "record" else b.obs
+
+        def one_step(ev=None):
+            if b.timestep >= params["episode_length"]:
+                b.reset(want_obs=True, out_obs=out)
+            b.sample_actions(0.1, out=act)
+            if ev is not None:
+                ev[0].record()
+            b.step(act, want_obs=True, out_obs=out)
+            if ev is not None:
+                ev[1].record()
+
+        b.reset(want_obs=True, out_obs=out)
+        for _ in range(args.warmup):
+            one_step()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        barrier(world)
+        torch.cuda.synchronize()
+        w0 = time.perf_counter()
+        t_start.record()
+        for i in range(K):
+            one_step(evs[i])
+        t_end.record()
+        torch.cuda.synchronize()
+        barrier(world)
+        wall = time.perf_counter() - w0
+        gpu_s = t_start.elapsed_time(t_end) / 1e3
+        kern_ms = np.array([a.elapsed_time(bb) for a, bb in evs])
+        t = max_over_ranks(max(wall, gpu_s), world)
+        kern_avg_ms = max_over_ranks(float(kern_ms.mean()), world)
+        bpas = RECORD_BYTES_PER_AGENT_STEP if mode == "record" else BYTES_PER_AGENT_STEP
+        bytes_per_launch = bpas * N * E
+        achieved = bytes_per_launch / (kern_avg_ms / 1e3) / 1e9
+        pmc = load_pmc_traffic(mode)
+        traffic = None
+        if pmc and pmc.get("kernel_prefix") and pmc.get("envs") == E and pmc.get("agents") == N:
+            traffic = pmc.get("bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "d2d::comb_kernel<uint8_t, 4, false, 8, false>", "kernel_avg_us": kern_avg_ms * 1e3,
+                "bytes_per_launch": bytes_per_launch, "bytes_per_agent_step": bpas}
+        return total_envs * K / t, t, roof
 
     total_envs = E * world
-    env_steps_per_s = total_envs * K / t
-    bytes_per_launch = BYTES_PER_AGENT_STEP * N * E
-    achieved = bytes_per_launch / (kern_avg_ms / 1e3) / 1e9
-    pmc = load_pmc_traffic()
-    traffic = None
-    if pmc and pmc.get("kernel_prefix") and pmc.get("envs") == E and pmc.get("agents") == N:
-        traffic = pmc.get("bytes_per_launch")
+    modes = ["record", "fp32"] if args.env_mode == "both" else [args.env_mode]
+    env_res = {m: env_phase(m) for m in modes}
+    env_steps_per_s, t, roofline = env_res[modes[0]]
+    fp32_obs = None
+    if len(modes) > 1:
+        v32, t32, r32 = env_res["fp32"]
+        fp32_obs = {"env_steps_per_s": v32, "agent_steps_per_s": v32 * N, "ms_per_step": t32 / K * 1e3,
+                    "roofline": r32,
+                    "what": "the same K steps emitting fp32 obs rows [E][N][F] (the reference-API layout)"}
 
     legs = set(args.legs.split(","))
     rollout = ppo = None
@@ -757,19 +784,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
+            "obs_format": modes[0],
             "data": "synthetic (Philox actions/channels/arrivals; reference channel_switch_8 tiled to 64 agents)",
             "config": {"workload": "combinatorial_env 64 agents x 8 channels, 65536 envs per GPU (BASELINE.json "
-                                   "configs[2]); step = synthetic-action sampling + env-step kernel with fp32 obs",
+                                   "configs[2]); step = synthetic-action sampling + env-step kernel emitting "
+                                   + ("the compact obs record" if modes[0] == "record" else "fp32 obs rows"),
                        "agents": N, "channels": C, "envs_per_gpu": E, "global_envs": total_envs,
                        "episode_length": args.episode_length, "parallelism": f"dp{world} (env shards, no collective)"},
             "agent_steps_per_s": env_steps_per_s * N,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "d2d::comb_kernel<uint8_t, 4, false>",
-                         "kernel_avg_us": kern_avg_ms * 1e3,
-                         "bytes_per_launch": bytes_per_launch,
-                         "bytes_per_agent_step": BYTES_PER_AGENT_STEP},
+            "roofline": roofline,
         }
+        if fp32_obs is not None:
+            res["fp32_obs"] = fp32_obs
         if rollout is not None:
             res["rollout"] = rollout
         if ppo is not None:

@@ -384,13 +384,14 @@ class BatchedLearnerBase(DataParallelMixin):
 
     # ------------------------------------------------------- HIP-graph rollout
     graph_rollout = os.environ.get("D2D_GRAPH_ROLLOUT", "1") != "0"
-    GRAPH_ROLLOUT_MAX_BYTES = 4 << 30
+    GRAPH_ROLLOUT_MAX_BYTES = 32 << 30
 
     def _graph_ok(self, train, b, T):
         """Training rollouts of the fused MLP policy replay one captured HIP graph (reset + L x
         (policy kernel, env kernel) per wave + the statistics): at small batches the slot loop is
-        bound by per-launch host work, not the GPU.  Large rollouts (obs buffer > 4 GiB, where the
-        kernels dominate) stay eager rather than pinning a second copy of the buffers."""
+        bound by per-launch host work, not the GPU.  The graph keeps its rollout buffers (reused by every
+        replay); rollouts whose obs buffer exceeds 32 GiB (of the 288 GB HBM) stay eager.  The compact
+        record puts the headline rollout (65,536 envs x 200 slots x 64 agents x 32 B = 27 GB) inside."""
         if not (self.graph_rollout and train and (self._gru_ok() or (not self.useRNN and self._fused_ok()))
                 and (self.kind == "comb") == bool(self.combinatorial)):
             return False

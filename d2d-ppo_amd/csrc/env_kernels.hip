@@ -470,13 +470,14 @@ __global__ __launch_bounds__(kMaxAgents) void comb_kernel(EnvArgs a) {
   if (a.rec && L.active) {
     const int w = ag.obs_width;
     const uint32_t ack_neg = ~(ack_one | ack_zero) & cmask;
-    // byte value of obs column p >= w (channel bits, acks, padding)
+    // byte value of obs column p >= w (channel bits, acks, padding; column F: the constant 1 the
+    // network kernels take as their layer-1 bias input)
     auto tail_byte = [&](int p) -> uint32_t {
       const int m = p - w;
       if (m < C) return (h_pre >> m) & 1u;
       const int c = m - C;
       if (c < C) return ((ack_one >> c) & 1u) | (((ack_neg >> c) & 1u) * 0xFFu);
-      return 0u;
+      return p == F ? 1u : 0u;
     };
     uint4* dst = reinterpret_cast<uint4*>(a.rec + row * (size_t)a.rec_bytes);
     uint32_t v[8];

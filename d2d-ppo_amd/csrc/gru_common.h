@@ -129,6 +129,8 @@ struct XSigns {
     for (int c = 0; c < (IT + 1) / 2; ++c) w[c] = ov.u8 ? ov.sgn[(size_t)k * (ov.RB >> 5) + c] : 0u;
   }
   __device__ __forceinline__ uint32_t bit(int col) const { return (w[col >> 5] >> (col & 31)) & 1u; }
+  // flags of columns col .. col + 3 (col % 4 == 0)
+  __device__ __forceinline__ uint32_t bits4(int col) const { return (w[col >> 5] >> (col & 31)) & 0xFu; }
 };
 
 // x tile of one window step: lane (g, i) <- x[env i][16q + 4g + r] (q < IT, r < 4), the bias
@@ -144,16 +146,14 @@ __device__ __forceinline__ void load_x(float (&x)[IT][4], const ObsView& ov, siz
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(ov.base + row0 * ov.RB), 0, nbytes, 0x00020000);
   const uint32_t vbase = env_ok ? (uint32_t)(i * ov.N * ov.RB) : 0x80000000u;
   const int F = ov.F;
-  if (ov.u8) {  // wave-uniform; the record row is zero past F
+  if (ov.u8) {  // wave-uniform; the record row holds the bias input 1 at column F, zeros past it
+    // (a padding step reads nothing: its bias input is set here)
 #pragma unroll
     for (int q = 0; q < IT; ++q) {
       const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vbase + (uint32_t)(16 * q + 4 * g), 0, 0);
+      const uint32_t m = sign_bytes(sg.bits4(16 * q + 4 * g));
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = 16 * q + 4 * g + r;
-        const float v = rec_byte(w, r, sg.bit(col));
-        x[q][r] = col == F ? 1.f : v;
-      }
+      for (int r = 0; r < 4; ++r) x[q][r] = (zero && 16 * q + 4 * g + r == F) ? 1.f : rec_byte(w, r, m);
     }
     return;
   }
@@ -170,11 +170,10 @@ __device__ __forceinline__ void load_x(float (&x)[IT][4], const ObsView& ov, siz
 // One input of the transposed x operand: column col = 16q + i of the row `vb` bytes past rsrc's base
 template <int IT>
 __device__ __forceinline__ float load_xt(const __amdgpu_buffer_rsrc_t& rsrc, uint32_t vb, const ObsView& ov,
-                                         const XSigns<IT>& sg, int q, int col) {
-  if (ov.u8) {
+                                         const XSigns<IT>& sg, int q, int col, bool zero) {
+  if (ov.u8) {  // the record's bias byte at column F; a padding step (zero) reads nothing
     const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(rsrc, vb + (uint32_t)col, 0, 0);
-    const float v = sg.bit(col) ? (float)(int8_t)b : (float)b;
-    return col == ov.F ? 1.f : v;
+    return (zero && col == ov.F) ? 1.f : sg.bit(col) ? (float)(int8_t)b : (float)b;
   }
   const float v = uf(__builtin_amdgcn_raw_buffer_load_b32(rsrc, vb + 4u * (uint32_t)col, 0, 0));
   return col < ov.F ? v : col == ov.F ? 1.f : 0.f;

@@ -418,7 +418,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
               const_cast<uint8_t*>(a.ov.base + xrow * a.ov.RB), 0, nbytes, 0x00020000);
           const uint32_t vb = eok ? (uint32_t)(ee * N * a.ov.RB) : 0x80000000u;
 #pragma unroll
-          for (int U = 0; U < IT; ++U) xt[U][s4] = load_xt<IT>(rsrc, vb, a.ov, xsg, U, 16 * U + i);
+          for (int U = 0; U < IT; ++U) xt[U][s4] = load_xt<IT>(rsrc, vb, a.ov, xsg, U, 16 * U + i, zero);
         }
 #pragma unroll
         for (int T = 0; T < 3 * HT; ++T) {

@@ -81,9 +81,16 @@ __device__ __forceinline__ void store_mask(void* base, size_t cell, int mask_byt
 }
 
 // Compact obs record (D2D_OBS_U8, env kernel's obs_record): byte j (compile-time) of record word w
-// as a network input, int8 when sgn (the ack columns) else uint8.  v_bfe_i32 / v_cvt_f32_ubyte.
-__device__ __forceinline__ float rec_byte(uint32_t w, int j, bool sgn) {
-  return sgn ? (float)((int32_t)(w << (24 - 8 * j)) >> 24) : (float)((w >> (8 * j)) & 0xFFu);
+// as a network input.  m = 0x80 in the bytes that are int8 (the ack columns), 0 in the uint8 ones:
+// int8 b = (b ^ 0x80) - 128, so every byte is one v_cvt_f32_ubyte of w ^ m minus a per-lane
+// constant (0 or 128, loop-invariant) -- no per-element select.  The record's byte obs_dim holds
+// the constant 1 of the layer-1 bias input and the bytes past it are 0, so no column masking either.
+__device__ __forceinline__ float rec_byte(uint32_t w, int j, uint32_t m) {
+  return (float)(((w ^ m) >> (8 * j)) & 0xFFu) - (float)((m >> (8 * j)) & 0xFFu);
+}
+// 0x80-per-byte masks of 4 int8 flags (bit r of `bits` -> byte r)
+__device__ __forceinline__ uint32_t sign_bytes(uint32_t bits) {
+  return ((bits & 1u) << 7) | ((bits & 2u) << 14) | ((bits & 4u) << 21) | ((bits & 8u) << 28);
 }
 
 // Exact bf16 split.  Every fp32 operand v is written EXACTLY as v = vh + vm + vl with

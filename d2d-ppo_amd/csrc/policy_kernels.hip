@@ -164,20 +164,17 @@ __device__ __forceinline__ void stage_inputs(float (&x)[KC][8], const float* slo
     }
 }
 
-// The same from a ring slot of compact-record words [c][2][lane]: the record row is zero past F
-// (the env kernel pads it), so only the bias input is set; sg[c] = this lane's 8 int8-column bits
+// The same from a ring slot of compact-record words [c][2][lane]: the record row already holds the
+// bias input 1 at column F and zeros past it (the env kernel writes them); sm[c][h] = this lane's
+// int8 byte masks of words h = 0, 1 (rec_byte)
 template <int KC>
-__device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* slot, int lane, int F, int g,
-                                             const uint32_t (&sg)[KC]) {
+__device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* slot, int lane,
+                                             const uint32_t (&sm)[KC][2]) {
 #pragma unroll
   for (int c = 0; c < KC; ++c) {
     const uint32_t d0 = slot[(c * 2) * 64 + lane], d1 = slot[(c * 2 + 1) * 64 + lane];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int col = 32 * c + 8 * g + j;
-      const float v = rec_byte(j < 4 ? d0 : d1, j & 3, (sg[c] >> j) & 1u);
-      x[c][j] = col == F ? 1.f : v;
-    }
+    for (int j = 0; j < 8; ++j) x[c][j] = rec_byte(j < 4 ? d0 : d1, j & 3, sm[c][j >> 2]);
   }
 }
 
@@ -285,10 +282,14 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
   const uint32_t nbytes = rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(wbase), 0, nbytes, 0x00020000);
-  // int8 columns of this lane's record bytes (agent k, columns 32c + 8g + j)
-  uint32_t sg[KC];
+  // int8 byte masks of this lane's record words (agent k, columns 32c + 8g + 4h + r)
+  uint32_t sm[KC][2];
 #pragma unroll
-  for (int c = 0; c < KC; ++c) sg[c] = U8 ? (a.sgn[(size_t)k * KC + c] >> (8 * g)) & 0xFFu : 0u;
+  for (int c = 0; c < KC; ++c) {
+    const uint32_t sg = U8 ? (a.sgn[(size_t)k * KC + c] >> (8 * g)) & 0xFFu : 0u;
+    sm[c][0] = sign_bytes(sg & 0xFu);
+    sm[c][1] = sign_bytes(sg >> 4);
+  }
   auto issue = [&](int t) {
     // look-ahead tiles past this wave's last are still issued (the counted waits need a fixed
     // DMA count) but aimed outside the descriptor's range: no memory traffic, zeros
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
   auto tile = [&](int tt, f32x4& lg, float& value) {
       float xc[KC][8];
       if constexpr (U8)
-        stage_record<KC>(xc, reinterpret_cast<const uint32_t*>(&ring[wave][tt % RING][0][0][0]), lane, F, g, sg);
+        stage_record<KC>(xc, reinterpret_cast<const uint32_t*>(&ring[wave][tt % RING][0][0][0]), lane, sm);
       else
         stage_inputs<KC>(xc, &ring[wave][tt % RING][0][0][0], lane, F, g);
       // bf16 high parts of the inputs; the residual parts only when some input of the tile is

@@ -134,9 +134,9 @@ __device__ __forceinline__ float ld_st(const float* base, const int64_t (&st)[3]
 template <int KC, bool U8>
 struct XRows {
   uint32_t v[2][KC][U8 ? 2 : 8];
-  // input j of chunk c of half s; sg[c] = this lane's 8 int8-column bits
-  __device__ __forceinline__ float at(int s, int c, int j, const uint32_t (&sg)[KC]) const {
-    if constexpr (U8) return rec_byte(v[s][c][j >> 2], j & 3, (sg[c] >> j) & 1u);
+  // input j of chunk c of half s (U8: sm[c][h] = this lane's int8 byte masks of word h, rec_byte)
+  __device__ __forceinline__ float at(int s, int c, int j, const uint32_t (&sm)[KC][2]) const {
+    if constexpr (U8) return rec_byte(v[s][c][j >> 2], j & 3, sm[c][j >> 2]);
     else return uf(v[s][c][j]);
   }
 };
@@ -170,11 +170,15 @@ __device__ __forceinline__ void load_rows(XRows<KC, U8>& x, const UpdArgs& a, in
   }
 }
 
-// this lane's int8-column bits of agent k's record (columns 32c + 8g + j, j < 8)
+// this lane's int8 byte masks of agent k's record words (columns 32c + 8g + 4h + r, rec_byte)
 template <int KC, bool U8>
-__device__ __forceinline__ void record_signs(uint32_t (&sg)[KC], const UpdArgs& a, int k, int g) {
+__device__ __forceinline__ void record_signs(uint32_t (&sm)[KC][2], const UpdArgs& a, int k, int g) {
 #pragma unroll
-  for (int c = 0; c < KC; ++c) sg[c] = U8 ? (a.sgn[(size_t)k * KC + c] >> (8 * g)) & 0xFFu : 0u;
+  for (int c = 0; c < KC; ++c) {
+    const uint32_t sg = U8 ? (a.sgn[(size_t)k * KC + c] >> (8 * g)) & 0xFFu : 0u;
+    sm[c][0] = sign_bytes(sg & 0xFu);
+    sm[c][1] = sign_bytes(sg >> 4);
+  }
 }
 
 __device__ __forceinline__ uint32_t load_action(const UpdArgs& a, int t, int e, int k) {
@@ -333,8 +337,8 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   int e0 = 0;
   ActorIn<KC, PAIR, U8> cur;  // per-sample scalars of the tile being computed
   bf16x8 xh[2][KC];
-  uint32_t sg[KC];
-  record_signs<KC, U8>(sg, a, k, g);
+  uint32_t sm[KC][2];
+  record_signs<KC, U8>(sm, a, k, g);
   // ---- inputs: bias column, zeros past it; bf16 high parts; the tile to LDS for dW1.
   // Returns whether every input of the tile is bf16-exact (wave-uniform).
   auto stage = [&](const ActorIn<KC, PAIR, U8>& src, int tile) -> bool {
@@ -355,7 +359,8 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int col = 32 * c + 8 * g + j;
-          xr[j] = col < F ? src.x.at(s, c, j, sg) : col == F ? 1.f : 0.f;
+          // the record carries the bias input at column F and zeros past it
+          xr[j] = U8 ? src.x.at(s, c, j, sm) : col < F ? src.x.at(s, c, j, sm) : col == F ? 1.f : 0.f;
           low |= fbits(xr[j]) & 0xFFFFu;
         }
         xh[s][c] = hi_frag(xr);
@@ -703,8 +708,8 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
   int e0 = 0;
   float R[2][4];
   bf16x8 xh[2][KC];
-  uint32_t sg[KC];
-  record_signs<KC, U8>(sg, a, k, g);
+  uint32_t sm[KC][2];
+  record_signs<KC, U8>(sm, a, k, g);
   auto stage = [&](const CriticIn<KC, U8>& src, int tile) -> bool {
     const int t = tile / a.tiles_per_t;
     e0 = (tile - t * a.tiles_per_t) * 32;
@@ -721,7 +726,8 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int col = 32 * c + 8 * g + j;
-          xr[j] = col < F ? src.x.at(s, c, j, sg) : col == F ? 1.f : 0.f;
+          // the record carries the bias input at column F and zeros past it
+          xr[j] = U8 ? src.x.at(s, c, j, sm) : col < F ? src.x.at(s, c, j, sm) : col == F ? 1.f : 0.f;
           low |= fbits(xr[j]) & 0xFFFFu;
         }
         xh[s][c] = hi_frag(xr);

@@ -107,8 +107,9 @@ typedef struct d2d_env_out {  /* any field may be NULL */
     uint8_t* success;   /* [E][N] 1 if agent k delivered a packet this slot */
     /* comb only: the compact obs record [E][N][D2D_RECORD_BYTES(obs_dim)] (16-byte aligned), the obs
      * row above one byte per column: packet counts and channel bits as uint8, the acks (columns
-     * [w_k + C, w_k + 2C)) as int8, zeros past the row.  Every obs value of this env is an integer
-     * in those ranges, so the record is exact; consumers take it with obs_format = D2D_OBS_U8. */
+     * [w_k + C, w_k + 2C)) as int8, then byte obs_dim = 1 (the networks' layer-1 bias input) and
+     * zeros.  Every obs value of this env is an integer in those ranges, so the record is exact;
+     * consumers take it with obs_format = D2D_OBS_U8. */
     uint8_t* obs_record;
 } d2d_env_out;
 

@@ -67,7 +67,8 @@ def test_env_record_decodes_to_fp32_obs(case):
     obs, rec, _, b = lockstep(params, E, 2 * params["episode_length"])
     s = b.spec
     assert torch.equal(rec.decode(), obs)
-    assert int(rec.data[..., s.F:].abs().sum()) == 0            # zero padding past the row
+    assert bool((rec.data[..., s.F] == 1).all())                 # the bias input byte
+    assert int(rec.data[..., s.F + 1:].sum()) == 0               # zero padding past it
     # values in range: counts / channel bits as uint8, acks in {-1, 0, 1}
     assert float(obs.min()) >= -1 and float(obs.max()) <= 255
 
