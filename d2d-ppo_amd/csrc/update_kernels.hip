@@ -43,6 +43,13 @@
 #ifndef D2D_UPD_ABLATE
 #define D2D_UPD_ABLATE 0  // != 0 only in tools/gpu/ablate_update.py's timing builds
 #endif
+#ifndef D2D_CRITIC_MASK
+// critic dV1 = sum_s dHv_s x_s^T with dHv = relu'(HV) * dv * v2 factored as
+//   dV1[h][:] = v2[h] * sum_s M[s][h] (dv_s x_s),   M = relu'(HV) in {0, 1}
+// M is exact in bf16 (no split); dv_s x_s is split two ways once per tile (16 values per lane)
+// instead of dHv (32), the relu' select and the dv * v2 products go, and v2 scales the sums once
+#define D2D_CRITIC_MASK 1
+#endif
 #ifndef D2D_LOGITS_BF16
 // logits Z^T = W2 . relu(HT) on bf16 MFMAs: W2's three-way split against a two-way RNE split of
 // relu(HT) (<= 2^-17 relative per product), 3 x 16 instead of 4 x 32 MFMA cycles per hidden tile
@@ -64,6 +71,7 @@ struct UpdArgs {
   const float* logp_old;            // actor: element (t, e, k) at t*st[0] + e*st[1] + k*st[2]
   const float* weight;              // actor: advantage / M; critic: return target
   int64_t lo_st[3], w_st[3];
+  int64_t lo_ext, w_ext;            // 1 + the largest element offset of logp_old / weight (floats)
   float* partial;                   // [G][N][P]
 };
 
@@ -112,6 +120,16 @@ __device__ __forceinline__ Parts2x4 split2_4(const float (&v)[4]) {
   return o;
 }
 
+// bf16 1.0 / 0.0 for h > 0 (the relu derivative, torch's convention at 0) of two values, packed; from
+// relu(h) (relu() above: the bit pattern is > 0 exactly when h > 0), one v_min_u32 each
+// (asm: the compiler turns a plain min into a float compare + select, two instructions)
+__device__ __forceinline__ uint32_t relu_mask_pair(float r0, float r1) {
+  uint32_t m0, m1;
+  asm("v_min_u32 %0, %1, 1" : "=v"(m0) : "v"(r0));
+  asm("v_min_u32 %0, %1, 1" : "=v"(m1) : "v"(r1));
+  return (m0 | (m1 << 16)) * 0x3F80u;
+}
+
 // high parts only (bf16-exact values)
 __device__ __forceinline__ bf16x8 hi_frag(const float (&v)[8]) {
   uint32_t u[4];
@@ -120,8 +138,19 @@ __device__ __forceinline__ bf16x8 hi_frag(const float (&v)[8]) {
   return as_frag(u);
 }
 
-__device__ __forceinline__ float ld_st(const float* base, const int64_t (&st)[3], int t, int e, int k) {
-  return base[(int64_t)t * st[0] + (int64_t)e * st[1] + (int64_t)k * st[2]];
+// Per-sample scalars of one tile (slot t, envs e0 .., agent k) through a range-checked buffer
+// descriptor based at the tile's first element: the 64-bit offset math is scalar (once per tile),
+// each load is one buffer_load with a loop-invariant lane offset d * st[1] (d = the lane's sample
+// within the tile).  Samples past the tensor read 0; those past E are masked by the callers.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sample_rsrc(const float* base, const int64_t (&st)[3], int64_t ext,
+                                                              int t, int e0, int k) {
+  const int64_t off = (int64_t)t * st[0] + (int64_t)e0 * st[1] + (int64_t)k * st[2];
+  const int64_t rest = (ext - off) * 4;
+  const uint32_t n = rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base + off), 0, n, 0x00020000);
+}
+__device__ __forceinline__ float ld_sample(const __amdgpu_buffer_rsrc_t& r, const int64_t (&st)[3], int d) {
+  return uf(__builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(d * (int)st[1]) * 4u, 0, 0));
 }
 
 // Per-tile inputs of the actor kernel, loaded one tile ahead (registers): the obs rows of the
@@ -181,25 +210,30 @@ __device__ __forceinline__ void record_signs(uint32_t (&sm)[KC][2], const UpdArg
   }
 }
 
-__device__ __forceinline__ uint32_t load_action(const UpdArgs& a, int t, int e, int k) {
-  const size_t cell = ((size_t)t * a.E + e) * a.N + k;
-  if (a.kind == 1) return reinterpret_cast<const unsigned char*>(a.actions)[cell];
-  return load_mask(a.actions, cell, a.mask_bytes);
-}
-
 template <int KC, bool PAIR, bool U8>
 __device__ __forceinline__ void load_actor_in(ActorIn<KC, PAIR, U8>& in, const UpdArgs& a, int tile, int k, int g,
                                               int i) {
   const int t = tile / a.tiles_per_t;
   const int e0 = (tile - t * a.tiles_per_t) * 32;
   load_rows<KC, U8>(in.x, a, t, e0, k, g, i);
+  const __amdgpu_buffer_rsrc_t rl = sample_rsrc(a.logp_old, a.lo_st, a.lo_ext, t, e0, k);
+  const __amdgpu_buffer_rsrc_t rw = sample_rsrc(a.weight, a.w_st, a.w_ext, t, e0, k);
+  // actions [T][E][N] (ids: 1 byte, masks: mask_bytes): byte offset of the tile's first cell
+  const int mb = a.kind == 1 ? 1 : a.mask_bytes;
+  const int64_t cell0 = ((int64_t)t * a.E + e0) * a.N + k;
+  const int64_t arest = ((int64_t)a.T * a.E * a.N - cell0) * mb;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(reinterpret_cast<const uint8_t*>(a.actions) + cell0 * mb), 0,
+      arest <= 0 ? 0u : arest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)arest, 0x00020000);
 #pragma unroll
   for (int s = 0; s < (PAIR ? 1 : 2); ++s) {
-    const int e = e0 + 16 * (PAIR ? (g >> 1) : s) + i;
-    const int ec = e < a.E ? e : a.E - 1;
-    in.act[s] = load_action(a, t, ec, k);
-    in.lo[s] = ld_st(a.logp_old, a.lo_st, t, ec, k);
-    in.w[s] = ld_st(a.weight, a.w_st, t, ec, k);
+    const int d = 16 * (PAIR ? (g >> 1) : s) + i;  // the lane's sample in the tile
+    const uint32_t ao = (uint32_t)(d * a.N * mb);
+    in.act[s] = mb == 1 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(ra, ao, 0, 0)
+              : mb == 2 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(ra, ao, 0, 0)
+                        : __builtin_amdgcn_raw_buffer_load_b32(ra, ao, 0, 0);
+    in.lo[s] = ld_sample(rl, a.lo_st, d);
+    in.w[s] = ld_sample(rw, a.w_st, d);
   }
 }
 
@@ -475,6 +509,8 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
 #pragma unroll
         for (int r = 0; r < 4; ++r) dzn[r] = zb[s][4 * g + r][i];
         // dW2^T operand B: dZ (k = sample 4g + j of this half, column = action i), two-way split
+        // (v_mfma_f32_16x16x4_f32 on the unsplit operands -- four chains of 4 per hidden tile -- removes
+        // 120 VALU per tile but measured 13 % slower: the fp32 MFMAs' issue cost outweighs the VALU)
         const Parts2x4 zn = split2_4(dzn);
         const uint32_t zz[2] = {0u, 0u};
         const bf16x8 bz1 = cat(zn.h, zn.h), bz2 = cat(zn.m, zz);
@@ -646,13 +682,11 @@ __device__ __forceinline__ void load_critic_in(CriticIn<KC, U8>& in, const UpdAr
   const int t = tile / a.tiles_per_t;
   const int e0 = (tile - t * a.tiles_per_t) * 32;
   load_rows<KC, U8>(in.x, a, t, e0, k, g, i);
+  const __amdgpu_buffer_rsrc_t rw = sample_rsrc(a.weight, a.w_st, a.w_ext, t, e0, k);
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int e = e0 + 16 * s + 4 * g + r;
-      in.R[s][r] = ld_st(a.weight, a.w_st, t, e < a.E ? e : a.E - 1, k);
-    }
+    for (int r = 0; r < 4; ++r) in.R[s][r] = ld_sample(rw, a.w_st, 16 * s + 4 * g + r);
 }
 
 template <int KC, int HT, bool U8>
@@ -741,6 +775,10 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
     // the tile body (XE: bf16-exact inputs), deferred tiles as in the actor kernel
     auto body = [&](auto xe) {
       constexpr bool XE = decltype(xe)::value;
+#if D2D_CRITIC_MASK
+      uint32_t mk[HT][2][2];  // relu' of HV as bf16 pairs [t2][half][r pair]
+      float dvh[2][4];        // dL/dv of samples 16s + 4g + r
+#endif
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         // HV = X . V1^T (sample 16s + 4g + r on rows, hidden 16t + i on lanes)
@@ -785,6 +823,44 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
           if (ok && i == 0) loss_acc += d * d;
           dc2 += i == 0 ? dvs[r] : 0.f;
         }
+#if D2D_CRITIC_MASK
+#pragma unroll
+        for (int t2 = 0; t2 < HT; ++t2) {
+          float hr[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            hr[r] = relu(hv[t2][r]);
+            dv2[t2] = fmaf(dvs[r], hr[r], dv2[t2]);
+          }
+#pragma unroll
+          for (int p = 0; p < 2; ++p) mk[t2][s][p] = relu_mask_pair(hr[2 * p], hr[2 * p + 1]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dvh[s][r] = dvs[r];
+      }
+      // dV1 / v2 += M^T . (dv x): k-slots of lane group g = (half s, r) <-> sample 16s + 4g + r
+#pragma unroll
+      for (int q = 0; q < QT; ++q) {
+        float bv[8];
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) bv[4 * s + r] = dvh[s][r] * xw[16 * s + 4 * g + r][16 * q + i];
+        const float b0[4] = {bv[0], bv[1], bv[2], bv[3]}, b1[4] = {bv[4], bv[5], bv[6], bv[7]};
+        const Parts2x4 p0 = split2_4(b0), p1 = split2_4(b1);
+        const bf16x8 bh = cat(p0.h, p1.h), bm = cat(p0.m, p1.m);
+#pragma unroll
+        for (int t2 = 0; t2 < HT; ++t2) {
+          const uint32_t m01[2] = {mk[t2][0][0], mk[t2][0][1]}, m23[2] = {mk[t2][1][0], mk[t2][1][1]};
+          const bf16x8 am = cat(m01, m23);
+          dv1[t2][q] = mfma_bf16(am, bm, dv1[t2][q]);
+#if D2D_UPD_ABLATE != 5  // timing ablation 5: no dV1 products
+          dv1[t2][q] = mfma_bf16(am, bh, dv1[t2][q]);
+#endif
+        }
+      }
+      (void)XE;
+#else
         // X sample-on-k for this half: B fragments with the split parts paired to dHv's
         bf16x8 bx1[QT], bx2[QT];
 #pragma unroll
@@ -821,6 +897,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
           }
         }
       }
+#endif
     };
     CriticIn<KC, U8> in;
     bool deferred = false;
@@ -854,7 +931,14 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
 #pragma unroll
       for (int q = 0; q < QT; ++q)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[n++] = dv1[t][q][r];
+        for (int r = 0; r < 4; ++r) {
+#if D2D_CRITIC_MASK
+          const int hid = 16 * t + 4 * g + r;  // accumulator row: the factored-out v2[hid]
+          acc[n++] = dv1[t][q][r] * (hid < H ? a.w2[(size_t)k * H + hid] : 0.f);
+#else
+          acc[n++] = dv1[t][q][r];
+#endif
+        }
 #pragma unroll
     for (int t = 0; t < HT; ++t) acc[n++] = dv2[t];
     acc[n++] = dc2;
@@ -912,6 +996,13 @@ __global__ void update_reduce_kernel(const float* __restrict__ partial, int G, i
 }  // namespace d2d
 
 using namespace d2d;
+
+// 1 + the largest element offset of a [T][E][N] view with these strides (-1: a negative stride)
+static int64_t tensor_extent(const int64_t (&st)[3], int T, int E, int N) {
+  if (st[0] < 0 || st[1] < 0 || st[2] < 0) return -1;
+  if (T <= 0 || E <= 0 || N <= 0) return 0;
+  return 1 + (int64_t)(T - 1) * st[0] + (int64_t)(E - 1) * st[1] + (int64_t)(N - 1) * st[2];
+}
 
 static int update_blocks(int N, int64_t n_tiles) {
   // about 4 workgroups per CU over the whole grid, at least one tile per wave
@@ -1011,6 +1102,9 @@ extern "C" int d2d_ppo_actor_grad(const d2d_mlp_desc* d, int32_t T, const void* 
   a.logp_old = logp_old;
   a.weight = weight;
   for (int q = 0; q < 3; ++q) { a.lo_st[q] = logp_strides[q]; a.w_st[q] = weight_strides[q]; }
+  a.lo_ext = tensor_extent(a.lo_st, a.T, a.E, a.N);
+  a.w_ext = tensor_extent(a.w_st, a.T, a.E, a.N);
+  if (a.lo_ext < 0 || a.w_ext < 0) { d2d_set_error("negative logp / weight strides"); return D2D_EINVAL; }
   a.clip_lo = 1.f - clip; a.clip_hi = 1.f + clip; a.beta = beta; a.scale = scale;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (a.N == 0) return D2D_OK;
@@ -1042,6 +1136,8 @@ extern "C" int d2d_ppo_critic_grad(const d2d_mlp_desc* d, int32_t T, const void*
   UpdArgs a = make_args(d, T, obs, workspace, 1);
   a.weight = returns;
   for (int q = 0; q < 3; ++q) a.w_st[q] = return_strides[q];
+  a.w_ext = tensor_extent(a.w_st, a.T, a.E, a.N);
+  if (a.w_ext < 0) { d2d_set_error("negative return strides"); return D2D_EINVAL; }
   a.scale = scale;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (a.N == 0) return D2D_OK;
