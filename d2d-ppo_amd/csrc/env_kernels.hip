@@ -481,6 +481,43 @@ __global__ __launch_bounds__(kMaxAgents) void comb_kernel(EnvArgs a) {
     };
     uint4* dst = reinterpret_cast<uint4*>(a.rec + row * (size_t)a.rec_bytes);
     uint32_t v[8];
+    bool built = false;
+    if constexpr (CT != 0 && 2 * CT <= 16 && 4 * DW <= 16) {
+      if (a.rec_bytes == 32) {  // wave-uniform: the whole row (F <= 31) in one 32-byte record
+        // word-level build: the buffer words as they are (their bytes >= w_k are zero), the channel
+        // bits and ack codes expanded 4 bits -> 4 bytes by one multiply (bit k of a nibble lands on
+        // bit 8k of n * 0x204081, the other copies are masked off), the 2C-byte block funnel-shifted
+        // to byte w_k, and the bias byte at column F
+        constexpr int NB = CT / 2;  // block words: CT/4 channel words, CT/4 ack words
+        auto expand4 = [](uint32_t n) { return (n * 0x204081u) & 0x01010101u; };
+        uint32_t blk[NB];
+#pragma unroll
+        for (int u = 0; u < CT / 4; ++u) {
+          blk[u] = expand4((h_pre >> (4 * u)) & 0xFu);
+          blk[CT / 4 + u] = expand4((ack_one >> (4 * u)) & 0xFu) | expand4((ack_neg >> (4 * u)) & 0xFu) * 0xFFu;
+        }
+        const int ws = w >> 2, bs = w & 3;
+        uint32_t sh[NB + 1];  // the block shifted up by bs bytes
+#pragma unroll
+        for (int j = 0; j <= NB; ++j) {
+          const uint32_t hi = j < NB ? blk[j] : 0u, lo = j > 0 ? blk[j - 1] : 0u;
+          sh[j] = bs == 0 ? hi : __builtin_amdgcn_alignbyte(hi, lo, 4 - bs);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          uint32_t word = q < DW ? b.w[q < DW ? q : 0] : 0u;
+#pragma unroll
+          for (int c = 0; c <= 16 / 4; ++c)  // w_k <= 4 DW <= 16: word shift 0 .. 4
+            if (q - c >= 0 && q - c <= NB) word |= ws == c ? sh[q - c] : 0u;
+          word |= (q == (F >> 2)) ? (1u << (8 * (F & 3))) : 0u;
+          v[q] = word;
+        }
+        dst[0] = make_uint4(v[0], v[1], v[2], v[3]);
+        dst[1] = make_uint4(v[4], v[5], v[6], v[7]);
+        built = true;
+      }
+    }
+    if (!built) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       uint32_t word = 0;
@@ -504,6 +541,7 @@ __global__ __launch_bounds__(kMaxAgents) void comb_kernel(EnvArgs a) {
       }
       dst[2 * q32] = make_uint4(v[0], v[1], v[2], v[3]);
       dst[2 * q32 + 1] = make_uint4(v[4], v[5], v[6], v[7]);
+    }
     }
   }
   // state = [concat_k B'[k,:d_k], channel_state (post-evolve).flatten(), acknack] (207-209)
