@@ -44,6 +44,8 @@ struct GruArgs {
   float* wimg;                            // [N][3 * 16 HT][16 IT] input images (gru_wih_image_kernel)
   float* hacc;                            // [G * N * 4 waves][GruHeadAcc::NV][64] head-gradient sums
   float* himg;                            // [N][HeadImg::SIZE] padded head images (gru_images_kernel)
+  float* ghist;                           // [G * N * 4 waves][L][5 HW][16] per-step dgi / dgh_n / h_{j-1} rows
+  float* gpart;                           // [G * N * 4 waves][(3 HT (HT + IT)) * 4][64] dW_hh / dW_ih sums
   int G, P;
 };
 
@@ -174,6 +176,32 @@ struct GruAcc {
   }
 };
 
+// Register partial sums that stay in the BPTT loop: dL/db_hn lanes and the loss sums (dW_ih, dW_hh
+// are per-tile GEMMs over the step history, GruWAcc).
+template <int HT>
+struct GruSAcc {
+  float bhn[HT][4];
+  float st[2];
+  static constexpr int NV = HT * 4 + 2;
+  template <class Fn>
+  __device__ __forceinline__ void each(Fn fn) {
+    int v = 0;
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) fn(v++, bhn[t][r]);
+    fn(v++, st[0]);
+    fn(v++, st[1]);
+  }
+};
+// Per-wave global sums of the recurrent / input weight gradients, [v][64 lanes]: dW_hh tiles
+// D[gate row 16T + 4g + r][unit 16U + i] at v = (T HT + U) 4 + r, then dW_ih tiles D[gate row][input
+// 16U + i] at WI + (T IT + U) 4 + r (the bias column F included).
+template <int HT, int IT>
+struct GruWAcc {
+  static constexpr int WI = 3 * HT * HT * 4, NV = WI + 3 * HT * IT * 4;
+};
+
 // Head gradients of one wave in global memory, [v][64 lanes] (coalesced): dW1 tiles
 // D[unit 16t + 4g + r][unit 16U + i], dW2 tiles D[output 4g + r][unit 16U + i], and per-sample-lane
 // partial sums of db1 (unit 16t + 4g + r) and db2 (output 4g + r).
@@ -192,14 +220,20 @@ struct GruOff {
   }
 };
 
-// Workgroup = agent k x a strided set of 16-sample tiles; 4 waves (one per SIMD: ~400 VGPRs).
-// LDS (H = 64): W_hh image 48 KB + dW_hh accumulator 48 KB + 4 x 16 KB wave scratch = 160 KB.
+// Workgroup = agent k x a strided set of 16-sample tiles; 4 waves (one per SIMD).
+// LDS (H = 64): W_hh image 48 KB (forward A fragments) + its transpose 49 KB (the A fragments of
+// dh = W_hh^T dg, one ds_read_b128 per 4 MFMAs) + 4 x 12 KB wave scratch = 145 KB.
+// The weight gradients dW_hh = sum_j dgh_j h_{j-1}^T and dW_ih = sum_j dgi_j x_j^T are not summed
+// step by step (that took one LDS atomic per element per step, ~40 % of the LDS issue): every step
+// writes its dgi / dgh_n / h_{j-1} rows (sample-on-k layout, through the wave's LDS scratch) to a
+// per-wave global history, and after the window one GEMM per tile with K = L x 16 accumulates them
+// in registers and adds them into the wave's global sums -- deterministic (no atomics anywhere).
 template <int HT, int IT, int KIND>
 __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
-  constexpr int HW = 16 * HT, R3 = 3 * HW, SROWS = R3 + HW;
+  constexpr int HW = 16 * HT, R3 = 3 * HW, RT = R3 + 4, SROWS = R3;
   __shared__ float whh_s[R3 * HW];
-  __shared__ float dwhh_s[R3 * HW];
-  __shared__ float scr[4][SROWS * 16];
+  __shared__ __attribute__((aligned(16))) float whhT_s[HW * RT];  // [unit u][gate row R], row stride R3 + 4
+  __shared__ __attribute__((aligned(16))) float scr[4][SROWS * 16];
   const int k = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -209,13 +243,14 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     const float* Whh = a.w.w_hh + (size_t)k * 3 * H * H;
     for (int idx = tid; idx < R3 * HW; idx += blockDim.x) {
       const int R = idx / HW, c = idx - R * HW, G = R / HW, u = R - G * HW;
-      whh_s[swz<HW>(R, c)] = (u < H && c < H) ? Whh[(size_t)(G * H + u) * H + c] : 0.f;
-      dwhh_s[idx] = 0.f;
+      const float v = (u < H && c < H) ? Whh[(size_t)(G * H + u) * H + c] : 0.f;
+      whh_s[swz<HW>(R, c)] = v;
+      whhT_s[c * RT + R] = v;
     }
   }
   f32x4 bhn[HT];
   load_bhn<HT>(bhn, a.w, k, H, g);
-  GruAcc<HT, IT> acc;
+  GruSAcc<HT> acc;
   acc.each([](int, float& x) { x = 0.f; });
   using HI = HeadImg<HT>;
   const float* himg = a.himg + (size_t)k * HI::SIZE;  // padded head image (gru_images_kernel)
@@ -229,6 +264,10 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   float* hist = a.hist + wave_id * (size_t)L * 64 * 4 * HT;
   float* hacc = a.hacc + wave_id * (size_t)GruHeadAcc<HT>::NV * 64;
   for (int v = 0; v < GruHeadAcc<HT>::NV; ++v) hacc[v * 64 + lane] = 0.f;
+  using WA = GruWAcc<HT, IT>;
+  float* ghist = a.ghist + wave_id * (size_t)L * 5 * HW * 16;
+  float* gpart = a.gpart + wave_id * (size_t)WA::NV * 64;
+  for (int v = 0; v < WA::NV; ++v) gpart[v * 64 + lane] = 0.f;
   __syncthreads();
 
   const int n_tiles = a.T * a.env_tiles;
@@ -392,7 +431,9 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
           gz[t][r] = gv * zz;
           acc.bhn[t][r] += dghn[t][r];
         }
-      // dgi (r, z, n_in rows) and h_{j-1} to the scratch
+      // this step's rows of the weight-gradient GEMMs, through the wave's scratch (sample-on-k layout)
+      // to the global history: dgi (r, z, n_in rows), then dgh_n (= dn_pre * r) and h_{j-1}
+      float* hrow = ghist + (size_t)j * 5 * HW * 16;
 #pragma unroll
       for (int t = 0; t < HT; ++t)
 #pragma unroll
@@ -401,12 +442,77 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
           sc[u * 16 + c] = drp[t][r];
           sc[(HW + u) * 16 + c] = dzp[t][r];
           sc[(2 * HW + u) * 16 + c] = dnp[t][r];
-          sc[(R3 + u) * 16 + c] = hp[t][r];
         }
       lds_order();
+#pragma unroll
+      for (int v = 0; v < R3 * 4 / 64; ++v)
+        reinterpret_cast<f32x4*>(hrow)[v * 64 + lane] = reinterpret_cast<const f32x4*>(sc)[v * 64 + lane];
+      lds_order();
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int u = 16 * t + 4 * g + r, c = pcol(i);
+          sc[u * 16 + c] = dghn[t][r];
+          sc[(HW + u) * 16 + c] = hp[t][r];
+        }
+      lds_order();
+#pragma unroll
+      for (int v = 0; v < 2 * HW * 4 / 64; ++v)
+        reinterpret_cast<f32x4*>(hrow + R3 * 16)[v * 64 + lane] = reinterpret_cast<const f32x4*>(sc)[v * 64 + lane];
+      lds_order();
       __builtin_amdgcn_sched_barrier(0);
-      // dW_ih += dgi x^T: x^T operand sample-on-k from global (sample 4 s4 + g, input 16U + i)
-      {
+      // dh_{j-1} = g z + W_hh^T dgh: A fragments from the transposed image, 4 k-steps per ds_read_b128
+      const float* wt = whhT_s + z;
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        f32x4 dh = {gz[t][0], gz[t][1], gz[t][2], gz[t][3]};
+#pragma unroll
+        for (int T = 0; T < 3 * HT; ++T) {
+          const f32x4 wv = *reinterpret_cast<const f32x4*>(wt + (16 * t + i) * RT + 16 * T + 4 * g);
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4) {
+            const float bv = T < HT ? drp[T][s4] : T < 2 * HT ? dzp[T - HT][s4] : dghn[T - 2 * HT][s4];
+            dh = mfma4(wv[s4], bv, dh);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gcur[t][r] = dh[r];
+      }
+    }
+
+    // ---- the tile's weight-gradient GEMMs over the history, K = L steps x 16 samples, one hidden
+    // tile tb (its r, z, n gate tiles) at a time: dW_hh += dgh h_{j-1}^T, dW_ih += dgi x^T
+#pragma unroll 1
+    for (int tb = 0; tb < HT; ++tb) {
+      f32x4 dwh[3][HT], dwi[3][IT];
+#pragma unroll
+      for (int g3 = 0; g3 < 3; ++g3) {
+#pragma unroll
+        for (int U = 0; U < HT; ++U) dwh[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int U = 0; U < IT; ++U) dwi[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll 1
+      for (int j = 0; j < L; ++j) {
+        const float* hrow = ghist + (size_t)j * 5 * HW * 16;
+        f32x4 ai[3], an;
+#pragma unroll
+        for (int g3 = 0; g3 < 3; ++g3) ai[g3] = sc_frag(hrow, 16 * (g3 * HT + tb) + i, g);
+        an = sc_frag(hrow, R3 + 16 * tb + i, g);
+#pragma unroll
+        for (int U = 0; U < HT; ++U) {
+          const f32x4 bh = sc_frag(hrow, R3 + HW + 16 * U + i, g);
+#pragma unroll
+          for (int g3 = 0; g3 < 3; ++g3) {
+            const f32x4 af = g3 < 2 ? ai[g3] : an;
+#pragma unroll
+            for (int s4 = 0; s4 < 4; ++s4) dwh[g3][U] = mfma4(af[s4], bh[s4], dwh[g3][U]);
+          }
+        }
+        // x^T operand sample-on-k from the rollout buffer (sample 4 s4 + g, input 16U + i)
+        const bool zero = j < pad;
+        const size_t xrow = row_of(j);
         float xt[IT][4];
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) {
@@ -421,59 +527,30 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
           for (int U = 0; U < IT; ++U) xt[U][s4] = load_xt<IT>(rsrc, vb, a.ov, xsg, U, 16 * U + i, zero);
         }
 #pragma unroll
-        for (int T = 0; T < 3 * HT; ++T) {
-          const f32x4 af = sc_frag(sc, 16 * T + i, g);
+        for (int g3 = 0; g3 < 3; ++g3)
 #pragma unroll
           for (int U = 0; U < IT; ++U)
 #pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) acc.wih[T][U] = mfma4(af[s4], xt[U][s4], acc.wih[T][U]);
-        }
+            for (int s4 = 0; s4 < 4; ++s4) dwi[g3][U] = mfma4(ai[g3][s4], xt[U][s4], dwi[g3][U]);
       }
-      lds_order();
-      // n rows of dgh = dn_pre * r
 #pragma unroll
-      for (int t = 0; t < HT; ++t)
+      for (int g3 = 0; g3 < 3; ++g3) {
+        const int T = g3 * HT + tb;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) sc[(2 * HW + 16 * t + 4 * g + r) * 16 + pcol(i)] = dghn[t][r];
-      lds_order();
-      __builtin_amdgcn_sched_barrier(0);
-      // dW_hh += dgh h_{j-1}^T, accumulated in LDS by the four waves
+        for (int U = 0; U < HT; ++U)
 #pragma unroll
-      for (int T = 0; T < 3 * HT; ++T) {
-        const f32x4 af = sc_frag(sc, 16 * T + i, g);
+          for (int r = 0; r < 4; ++r) gpart[((T * HT + U) * 4 + r) * 64 + lane] += dwh[g3][U][r];
 #pragma unroll
-        for (int U = 0; U < HT; ++U) {
-          const f32x4 bf = sc_frag(sc, R3 + 16 * U + i, g);
-          f32x4 d = {0.f, 0.f, 0.f, 0.f};
+        for (int U = 0; U < IT; ++U)
 #pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) d = mfma4(af[s4], bf[s4], d);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) atomicAdd(&dwhh_s[(16 * T + 4 * g + r) * HW + 16 * U + i], d[r]);
-        }
+          for (int r = 0; r < 4; ++r) gpart[(WA::WI + (T * IT + U) * 4 + r) * 64 + lane] += dwi[g3][U][r];
       }
-      __builtin_amdgcn_sched_barrier(0);
-      // dh_{j-1} = g z + W_hh^T dgh
-#pragma unroll
-      for (int t = 0; t < HT; ++t) {
-        f32x4 dh = {gz[t][0], gz[t][1], gz[t][2], gz[t][3]};
-#pragma unroll
-        for (int T = 0; T < 3 * HT; ++T)
-#pragma unroll
-          for (int s4 = 0; s4 < 4; ++s4) {
-            const float wv = wh[16 * T * HW + oh.tr[t][s4]];
-            const float bv = T < HT ? drp[T][s4] : T < 2 * HT ? dzp[T - HT][s4] : dghn[T - 2 * HT][s4];
-            dh = mfma4(wv, bv, dh);
-          }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) gcur[t][r] = dh[r];
-      }
-      lds_order();
     }
   }
 
   // ---- cross-wave sum of the register partials (fixed order, through the scratch), then the
-  // workgroup's partial: registers of wave 0 + the LDS dW_hh
-  constexpr int NV = GruAcc<HT, IT>::NV;
+  // workgroup's partial: registers of wave 0 + the four waves' global weight-gradient sums
+  constexpr int NV = GruSAcc<HT>::NV;
   float* red = &scr[0][0];
   static_assert(NV * 64 <= 4 * SROWS * 16, "reduction buffer");
 #pragma unroll 1
@@ -486,20 +563,31 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   __syncthreads();
   const GruOff o(H, F, A);
   float* part = a.partial + ((size_t)blockIdx.y * N + k) * a.P;
-  for (int idx = tid; idx < R3 * HW; idx += blockDim.x) {
-    const int R = idx / HW, c = idx - R * HW, G = R / HW, u = R - G * HW;
-    if (u < H && c < H) part[o.whh + (G * H + u) * H + c] = dwhh_s[idx];
-  }
   if (wave == 0) {
+    const float* wb = a.gpart + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 * WA::NV * 64;
+    auto wsum = [&](int v) {
+      return ((wb[v * 64 + lane] + wb[(WA::NV + v) * 64 + lane]) + wb[(2 * WA::NV + v) * 64 + lane]) +
+             wb[(3 * WA::NV + v) * 64 + lane];
+    };
+#pragma unroll 1
+    for (int T = 0; T < 3 * HT; ++T)
 #pragma unroll
+      for (int U = 0; U < HT; ++U)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int R = 16 * T + 4 * g + r, G = R / HW, u = R - G * HW, c = 16 * U + i;
+          const float v = wsum((T * HT + U) * 4 + r);
+          if (u < H && c < H) part[o.whh + (G * H + u) * H + c] = v;
+        }
+#pragma unroll 1
     for (int T = 0; T < 3 * HT; ++T)
 #pragma unroll
       for (int U = 0; U < IT; ++U)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int R = 16 * T + 4 * g + r, G = R / HW, u = R - G * HW, c = 16 * U + i;
+          const float v = wsum(WA::WI + (T * IT + U) * 4 + r);
           if (u >= H) continue;
-          const float v = acc.wih[T][U][r];
           if (c < F) part[o.wih + (G * H + u) * F + c] = v;
           else if (c == F) {
             part[o.bih + G * H + u] = v;
@@ -713,18 +801,34 @@ static int gru_grad_blocks(int N, int64_t n_tiles) {
   return (int)std::max<int64_t>(1, std::min<int64_t>((256 + N - 1) / N, (n_tiles + 3) / 4));
 }
 
+// Float offsets of the grad kernel's workspace pieces (each rounded to 64 floats: 16-byte vector
+// accesses stay aligned): partials, h history, input images, head sums, head images, the per-step
+// gradient-row history, the weight-gradient sums.
+struct GruWs {
+  int64_t partial, hist, wimg, hacc, himg, ghist, gpart, total;
+};
+static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, int itp) {
+  auto up = [](int64_t v) { return (v + 63) / 64 * 64; };
+  const int64_t waves = G * N * 4, HW = 16 * htp;
+  GruWs w;
+  w.partial = 0;
+  w.hist = up(G * N * P);
+  w.wimg = w.hist + up(waves * L * 64 * 4 * htp);
+  w.hacc = w.wimg + up(N * 3 * HW * 32);
+  w.himg = w.hacc + up(waves * 64 * (htp * htp * 4 + htp * 8 + 4));
+  w.ghist = w.himg + up(N * (HW * HW + 16 * HW + HW + 16));
+  w.gpart = w.ghist + up(waves * L * 5 * HW * 16);
+  w.total = w.gpart + up(waves * 64 * (3 * htp * (htp + itp) * 4));
+  return w;
+}
+
 extern "C" int64_t d2d_gru_grad_workspace(const d2d_gru_desc* d, int32_t T) {
   if (!d || d->n_agents <= 0 || T <= 0 || d->n_envs <= 0 || d->hidden < 1 || d->history_len < 1) return 0;
   const int A = d->kind == 2 ? 1 : d->n_out, H = d->hidden, ht = H <= 16 ? 1 : H <= 32 ? 2 : 4;
   const int64_t tiles = (int64_t)T * ((d->n_envs + 15) / 16);
   const int G = gru_grad_blocks(d->n_agents, tiles);
   const GruOff o(H, d->obs_dim, A);
-  const int64_t partial = (int64_t)G * d->n_agents * o.P;
-  const int64_t hist = (int64_t)G * d->n_agents * 4 * d->history_len * 64 * 4 * ht;
-  const int64_t img = (int64_t)d->n_agents * 3 * 16 * ht * 32;
-  const int64_t hacc = (int64_t)G * d->n_agents * 4 * 64 * (ht * ht * 4 + ht * 8 + 4);
-  const int64_t himg = (int64_t)d->n_agents * (16 * ht * 16 * ht + 16 * 16 * ht + 16 * ht + 16);
-  return partial + hist + img + hacc + himg;
+  return gru_ws_layout(G, d->n_agents, o.P, d->history_len, ht, d->obs_dim + 1 <= 16 ? 1 : 2).total;
 }
 
 template <int HT, int IT>
@@ -768,12 +872,15 @@ extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, c
   a.G = gru_grad_blocks(a.N, tiles);
   const GruOff o(a.H, a.F, a.A);
   a.P = o.P;
-  a.partial = workspace;
-  a.hist = workspace + (int64_t)a.G * a.N * a.P;
   const int ht = (a.H + 15) / 16, htp = ht <= 1 ? 1 : ht <= 2 ? 2 : 4, itp = a.F + 1 <= 16 ? 1 : 2;
-  a.wimg = a.hist + (int64_t)a.G * a.N * 4 * a.L * 64 * 4 * htp;
-  a.hacc = a.wimg + (int64_t)a.N * 3 * 16 * htp * 32;
-  a.himg = a.hacc + (int64_t)a.G * a.N * 4 * 64 * (htp * htp * 4 + htp * 8 + 4);
+  const GruWs ws = gru_ws_layout(a.G, a.N, a.P, a.L, htp, itp);
+  a.partial = workspace + ws.partial;
+  a.hist = workspace + ws.hist;
+  a.wimg = workspace + ws.wimg;
+  a.hacc = workspace + ws.hacc;
+  a.himg = workspace + ws.himg;
+  a.ghist = workspace + ws.ghist;
+  a.gpart = workspace + ws.gpart;
   if (a.N == 0) return D2D_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   {
