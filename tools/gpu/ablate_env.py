@@ -6,6 +6,9 @@ Variants (timed with HIP events around each env-step launch, median of rounds):
   noobs     no obs emission (diagnostic: cost of the obs write stream)
   replay    obs, draws read from pre-generated buffers (diagnostic: Philox cost)
   state     obs + D2D state emission
+  rec       the compact obs record instead of fp32 rows (the learners' and the bench's default)
+  rec_replay  record, draws read from pre-generated buffers (Philox cost on the record path)
+  rec_none    record path without any obs output (state / counters only)
 plus torch fill_/copy_ of comparable sizes as write / copy bandwidth anchors.
 """
 import json
@@ -34,6 +37,7 @@ def main():
     g = torch.Generator(device="cuda").manual_seed(0)
     flips = torch.randint(0, 256, (E, 64), device="cuda", dtype=torch.int32, generator=g).to(torch.uint8)
     arrs = torch.randint(0, 2, (E, 64), device="cuda", dtype=torch.int32, generator=g).to(torch.uint8)
+    rec = b.record
     b.reset(want_obs=True)
 
     def run(variant, n=40):
@@ -51,6 +55,12 @@ def main():
                 b.step(act, want_obs=True, replay=(flips, arrs))
             elif variant == "state":
                 b.step(act, want_obs=True, want_state=True)
+            elif variant == "rec":
+                b.step(act, out_obs=rec)
+            elif variant == "rec_replay":
+                b.step(act, out_obs=rec, replay=(flips, arrs))
+            elif variant == "rec_none":
+                b.step(act, want_obs=False, replay=(flips, arrs))
             else:
                 b.step(act, want_obs=True)
             e1.record()
@@ -58,7 +68,7 @@ def main():
         torch.cuda.synchronize()
         return statistics.median(a.elapsed_time(c) for a, c in evs) * 1e3
 
-    variants = ["base", "nt", "noobs", "replay", "state"]
+    variants = ["base", "nt", "noobs", "replay", "state", "rec", "rec_replay", "rec_none"]
     res = {v: [] for v in variants}
     for v in variants:
         run(v, 10)
@@ -80,7 +90,9 @@ def main():
     out = {v: {"median_us": statistics.median(t), "min_us": min(t)} for v, t in res.items()}
     alg = 172.0 * 64 * E
     for v in out:
-        out[v]["alg_GBps"] = alg / (out[v]["median_us"] * 1e-6) / 1e9
+        a_v = (alg - 120.0 * 64 * E + (32.0 * 64 * E if v.startswith("rec") and v != "rec_none" else 0.0)
+               if v.startswith("rec") or v == "noobs" else alg)
+        out[v]["alg_GBps"] = a_v / (out[v]["median_us"] * 1e-6) / 1e9
     out["torch_fill_obs_sized"] = {"us": statistics.median(fill), "GBps": nbytes / statistics.median(fill) / 1e3}
     out["torch_copy_obs_sized"] = {"us": statistics.median(copy), "GBps": 2 * nbytes / statistics.median(copy) / 1e3}
     print(json.dumps(out, indent=1))
