@@ -344,9 +344,11 @@ def update_kernel_roofline(lr, ro, F, H, A, reps=4):
         ta += ev[0].elapsed_time(ev[1]) / reps
         tc += ev[1].elapsed_time(ev[2]) / reps
     # MFMA pipe time per 32-sample tile from the kernels' static instruction mix (F + 1 <= 32,
-    # H <= 64, A <= 8: csrc/update_kernels.hip, bf16 logits): 128 (actor) / 40 (critic)
-    # v_mfma_f32_16x16x32_bf16 at 16 cycles/SIMD (MI355X_MICROARCH.md cycle table), 2.4 GHz peak clock
-    pipe = {"actor": 128 * 16, "critic": 40 * 16}
+    # H <= 64, A <= 8: csrc/update_kernels.hip, bf16 logits): 104 (actor on the compact record: no
+    # HN recompute) or 128 (fp32 rows) / 40 (critic) v_mfma_f32_16x16x32_bf16 at 16 cycles/SIMD
+    # (MI355X_MICROARCH.md cycle table), 2.4 GHz peak clock
+    from d2dhip.record import ObsRecord
+    pipe = {"actor": (104 if isinstance(ro.obs, ObsRecord) else 128) * 16, "critic": 40 * 16}
     simds, clock = 1024, 2.4e9
     tiles = ro.T * ((ro.E + 31) // 32) * N
     res = {}

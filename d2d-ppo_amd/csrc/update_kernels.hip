@@ -43,6 +43,13 @@
 #ifndef D2D_UPD_ABLATE
 #define D2D_UPD_ABLATE 0  // != 0 only in tools/gpu/ablate_update.py's timing builds
 #endif
+#ifndef D2D_ACTOR_TR
+// actor on the compact record: the sample-on-rows layer 1 (HN = X . W1^T: 3 MFMAs per hidden tile
+// per half, its relu, the relu mask and the two-way split of relu(HN) for dW2) is not recomputed --
+// relu(HT)'s split parts, already made for the logits, are transposed through LDS with
+// ds_read_b64_tr_b16 into the dW2 operand layout, and their high part is the relu mask
+#define D2D_ACTOR_TR 1
+#endif
 #ifndef D2D_CRITIC_MASK
 // critic dV1 = sum_s dHv_s x_s^T with dHv = relu'(HV) * dv * v2 factored as
 //   dV1[h][:] = v2[h] * sum_s M[s][h] (dv_s x_s),   M = relu'(HV) in {0, 1}
@@ -102,6 +109,7 @@ __device__ __forceinline__ bf16x8 cat(const uint32_t (&a)[2], const uint32_t (&b
 // outweighs its MFMAs; the weight gradients then carry ~2^-17 relative error per product term,
 // below the fp32 accumulation error of their 10^5-10^6-sample sums)
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint32_t rne2(float a, float b) {
   const bf16x2_t v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32
   return __builtin_bit_cast(uint32_t, v);
@@ -282,6 +290,9 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   xcd_block(k, by);  // k = agent, by = sample-chunk group
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int H = a.H, A = a.A, F = a.F;
+  // the transposed-relu(HT) path (D2D_ACTOR_TR): record inputs only (always bf16-exact, so the
+  // fractional-input body never runs) and the bf16 logits, whose split parts it transposes
+  constexpr bool TR = U8 && D2D_LOGITS_BF16 && D2D_ACTOR_TR;
 
   // ---- weights of agent k: the W1 split in registers; the two W2 operand sets (used once per
   // half per hidden tile) in LDS, shared by the workgroup's four waves
@@ -290,9 +301,10 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   // dH's three B operands [l|h], [m|h], [h|m], stored whole so one ds_read_b128 lands each in
   // the four consecutive registers the MFMA reads (no operand assembly moves)
   __shared__ __attribute__((aligned(16))) bf16x8 w2b_s[HT][3][64];
-  __shared__ __attribute__((aligned(16))) float w2f_s[HT][64][4];        // Z^T's fp32 A operand
 #if D2D_LOGITS_BF16
   __shared__ __attribute__((aligned(16))) bf16x8 w2z_s[HT][3][64];       // Z^T's bf16 A operands [h|h], [m|m], [l|0]
+#else
+  __shared__ __attribute__((aligned(16))) float w2f_s[HT][64][4];        // Z^T's fp32 A operand
 #endif
   {
     const float* W1 = a.w1 + (size_t)k * H * F;
@@ -323,17 +335,18 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
       w2b_s[t][0][lane] = cat(p4.l, p4.h);
       w2b_s[t][1][lane] = cat(p4.m, p4.h);
       w2b_s[t][2][lane] = cat(p4.h, p4.m);
-      // A operand of Z^T = W2 . relu(HT) (fp32 16x16x4): row = action i, k = hidden 16t + 4g + r
+      // A operand of Z^T = W2 . relu(HT): row = action i, k = hidden 16t + 4g + r
+      float wz[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int hid = 16 * t + 4 * g + r;
-        w2f_s[t][lane][r] = (i < A && hid < H) ? W2[(size_t)i * H + hid] : 0.f;
+        wz[r] = (i < A && hid < H) ? W2[(size_t)i * H + hid] : 0.f;
       }
-#if D2D_LOGITS_BF16
-      {
-        float wz[4];
+#if !D2D_LOGITS_BF16
 #pragma unroll
-        for (int r = 0; r < 4; ++r) wz[r] = w2f_s[t][lane][r];
+      for (int r = 0; r < 4; ++r) w2f_s[t][lane][r] = wz[r];
+#else
+      {
         const Parts4 pz = split3_4(wz);
         const uint32_t zero2[2] = {0u, 0u};
         w2z_s[t][0][lane] = cat(pz.h, pz.h);
@@ -357,13 +370,22 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   f32x4 db2 = {0.f, 0.f, 0.f, 0.f};
   float surr_acc = 0.f, ent_acc = 0.f;
 
-  // per-wave LDS: the obs tile row-major and the dZ transpose (row stride 20)
-  constexpr int XS = 32 * KC + 4;  // row stride = 4 mod 16 floats: sample-on-k reads hit 64 banks
-  __shared__ __attribute__((aligned(16))) float xs[4][32][XS];
+  // per-wave LDS: the obs tile row-major (fp32; TR: its bf16 high parts, exact for the record) and
+  // the dZ transpose (row stride 20)
+  constexpr int XS = 32 * KC + 4;    // fp32 row stride = 4 mod 16 floats: sample-on-k reads hit 64 banks
+  constexpr int XS16 = 32 * KC + 4;  // bf16 rows of 8-byte multiples, 8 banks apart per 4 rows
+  __shared__ __attribute__((aligned(16))) unsigned char xs_raw[TR ? 4 * 32 * XS16 * 2 : 4 * 32 * XS * 4];
   __shared__ __attribute__((aligned(16))) float dzt[4][2][16][20];
   constexpr int NV = HT * QT * 4 + HT * 4 + 4 + 2;
-  __shared__ float red[NV * 64];
-  float(*xw)[XS] = xs[wave];
+  // TR: relu(HT)'s split parts [wave][half][hidden tile][part][16 samples][16 hidden] bf16; the
+  // cross-wave reduction buffer (used only after the tile loop) shares the space
+  constexpr int TRU16 = TR ? 4 * 2 * HT * 2 * 16 * 16 : 0;
+  constexpr int RAWB = TRU16 * 2 > NV * 64 * 4 ? TRU16 * 2 : NV * 64 * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char tr_raw[RAWB];
+  float* red = reinterpret_cast<float*>(tr_raw);
+  uint16_t* trimg = reinterpret_cast<uint16_t*>(tr_raw);
+  float(*xw)[XS] = reinterpret_cast<float(*)[XS]>(xs_raw + (TR ? 0 : wave * 32 * XS * 4));
+  uint16_t(*xw16)[XS16] = reinterpret_cast<uint16_t(*)[XS16]>(xs_raw + (TR ? wave * 32 * XS16 * 2 : 0));
   float(*zb)[16][20] = dzt[wave];
 
   const int stride = a.G * 4;
@@ -398,8 +420,14 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
           low |= fbits(xr[j]) & 0xFFFFu;
         }
         xh[s][c] = hi_frag(xr);
-        *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g]) = f32x4{xr[0], xr[1], xr[2], xr[3]};
-        *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g + 4]) = f32x4{xr[4], xr[5], xr[6], xr[7]};
+        if constexpr (TR) {  // the bf16 high parts (exact) as two 8-byte stores
+          const u32x4v hv = __builtin_bit_cast(u32x4v, xh[s][c]);
+          *reinterpret_cast<uint2*>(&xw16[16 * s + i][32 * c + 8 * g]) = make_uint2(hv[0], hv[1]);
+          *reinterpret_cast<uint2*>(&xw16[16 * s + i][32 * c + 8 * g + 4]) = make_uint2(hv[2], hv[3]);
+        } else {
+          *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g]) = f32x4{xr[0], xr[1], xr[2], xr[3]};
+          *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * c + 8 * g + 4]) = f32x4{xr[4], xr[5], xr[6], xr[7]};
+        }
       }
     // the record's integers in [-128, 255] are bf16-exact
     return U8 || __builtin_amdgcn_ballot_w64(low != 0) == 0;
@@ -442,17 +470,16 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
         f32x4 z = b2i;
 #pragma unroll
         for (int t2 = 0; t2 < HT; ++t2) {
+#if !D2D_LOGITS_BF16
           const f32x4 w2f = *reinterpret_cast<const f32x4*>(&w2f_s[t2][lane][0]);
 #pragma unroll
           for (int r = 0; r < 4; ++r)
 #if D2D_UPD_ABLATE == 2  // timing ablation: logits without the fp32 MFMAs
             z[r] += w2f[r] * relu(ht[t2][r]);
-#elif D2D_LOGITS_BF16
-            (void)w2f;
 #else
             z = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[r], relu(ht[t2][r]), z, 0, 0, 0);
 #endif
-#if D2D_LOGITS_BF16
+#else
           {  // relu(HT) on a two-way RNE split in the k-slots [h_h | h_m] against W2's h, m, l parts
             float hv[4];
 #pragma unroll
@@ -462,6 +489,12 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
             z = mfma_bf16(w2z_s[t2][2][lane], bh, z);
             z = mfma_bf16(w2z_s[t2][1][lane], bh, z);
             z = mfma_bf16(w2z_s[t2][0][lane], bh, z);
+            if constexpr (TR) {
+              // the split parts to this half's image [part][sample i][hidden 4g .. 4g + 3]
+              uint16_t* im = trimg + (((wave * 2 + s) * HT + t2) * 2) * 256 + i * 16 + 4 * g;
+              *reinterpret_cast<uint2*>(im) = make_uint2(hp.h[0], hp.h[1]);
+              *reinterpret_cast<uint2*>(im + 256) = make_uint2(hp.m[0], hp.m[1]);
+            }
           }
 #endif
         }
@@ -517,6 +550,15 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
         bf16x8 bx1[QT], bx2[QT];
 #pragma unroll
         for (int q = 0; q < QT; ++q) {
+          if constexpr (TR) {  // the bf16 image holds the (exact) inputs already as operand halves
+            uint32_t xh2[2];
+#pragma unroll
+            for (int p2 = 0; p2 < 2; ++p2)
+              xh2[p2] = (uint32_t)xw16[16 * s + 4 * g + 2 * p2][16 * q + i] |
+                        ((uint32_t)xw16[16 * s + 4 * g + 2 * p2 + 1][16 * q + i] << 16);
+            bx1[q] = cat(xh2, xh2);
+            continue;
+          }
           float xc[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) xc[r] = xw[16 * s + 4 * g + r][16 * q + i];
@@ -535,6 +577,35 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
         const bf16x8 a_hm = cat(zp.h, zp.m), a_hl = cat(zp.h, zp.l);
 #pragma unroll
         for (int t2 = 0; t2 < HT; ++t2) {
+          if constexpr (TR) {
+            // relu(HT)'s split parts of hidden tile t2, transposed: lane (g, i) <- samples 4g .. 4g + 3
+            // (element r) of hidden unit 16 t2 + i; lane 4q + p of each 16-lane group addresses
+            // row (sample) 4g + q, columns 4p .. 4p + 3 of the [sample][hidden] image
+            uint16_t* im = trimg + (((wave * 2 + s) * HT + t2) * 2) * 256 + (4 * g + (i >> 2)) * 16 + 4 * (i & 3);
+            typedef __attribute__((address_space(3))) v4i16* lds_v4i16;
+            const v4i16 th = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(im));
+            const v4i16 tm = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(im + 256));
+            const uint32_t hh[2] = {(uint16_t)th[0] | ((uint32_t)(uint16_t)th[1] << 16),
+                                    (uint16_t)th[2] | ((uint32_t)(uint16_t)th[3] << 16)};
+            const uint32_t mm[2] = {(uint16_t)tm[0] | ((uint32_t)(uint16_t)tm[1] << 16),
+                                    (uint16_t)tm[2] | ((uint32_t)(uint16_t)tm[3] << 16)};
+            f32x4 acc = mfma_bf16(a_hl, w2b_s[t2][0][lane], f32x4{0.f, 0.f, 0.f, 0.f});
+            acc = mfma_bf16(a_hm, w2b_s[t2][1][lane], acc);
+            acc = mfma_bf16(a_hm, w2b_s[t2][2][lane], acc);
+            // relu' from the high part: nonzero exactly when relu(h) is (down to bf16's underflow at
+            // ~1e-40, far below any pre-activation of normal-magnitude weights and inputs)
+            float dh[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dh[r] = th[r] != 0 ? acc[r] : 0.f;
+            const bf16x8 h_hm = cat(hh, mm);
+            dw2[t2] = mfma_bf16(h_hm, bz2, dw2[t2]);
+            dw2[t2] = mfma_bf16(h_hm, bz1, dw2[t2]);
+            const Parts2x4 dp = split2_4(dh);
+            const bf16x8 d_hm = cat(dp.h, dp.m);
+#pragma unroll
+            for (int q = 0; q < QT; ++q) dw1[t2][q] = mfma_bf16(d_hm, bx1[q], dw1[t2][q]);
+            continue;
+          }
           f32x4 hn = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int c = 0; c < KC; ++c) {
