@@ -26,6 +26,17 @@
 namespace d2d {
 
 constexpr int kBlock = 256;
+// comb_kernel register budget and the lane count of a record-only step (no LDS staging): 7 waves
+// per SIMD (<= 72 VGPRs, no spills; unhinted the allocator takes 91 and runs 5) in 256-lane blocks
+// (512-lane blocks would fit only 3 per SIMD pair of waves): record step 68.5 -> 64.9 us at
+// 64 x 8 x 65,536; 8 waves spill (76 us).  Ablation builds override both
+// (tools/gpu/build_ablate_env.sh).
+#ifndef D2D_COMB_WAVES_PER_EU
+#define D2D_COMB_WAVES_PER_EU 7
+#endif
+#ifndef D2D_COMB_REC_BLOCK
+#define D2D_COMB_REC_BLOCK 256
+#endif
 constexpr int kMaxAgents = 1024;
 
 struct EnvArgs {
@@ -35,6 +46,7 @@ struct EnvArgs {
   uint64_t env_base, seed;
   const d2d_agent_entry* agents;
   const uint64_t* flip_thr;
+  const uint32_t* pois_cdf;  // [N][256] inverse-CDF thresholds of the Poisson arrival draw
   uint32_t* buf;
   void* chan;
   uint32_t* recv;
@@ -159,7 +171,7 @@ __device__ __forceinline__ uint32_t arrival_value(const EnvArgs& a, const d2d_ag
                                                   uint64_t genv) {
   if (a.arrivals) return a.arrivals[row];
   const u32x4 r = philox((uint32_t)genv, (uint32_t)k, rng_of(a), kStreamArrival << 24, a.seed);
-  if (ag.arrival_kind == D2D_ARRIVAL_POISSON) return poisson_inv(r.x, ag.lam, ag.pois_p0);
+  if (ag.arrival_kind == D2D_ARRIVAL_POISSON) return poisson_lookup(r.x, a.pois_cdf + (size_t)k * 256);
   return (uint64_t)r.x < ag.arrival_thr ? 1u : 0u;
 }
 
@@ -301,7 +313,7 @@ __device__ __forceinline__ void wave_flush(float* __restrict__ dst, const float*
 //   N  > 64 : state of the block's single env staged per block.
 // =====================================================================
 template <typename MaskT, int DW, bool LARGE, int CT, bool RESET>
-__global__ __launch_bounds__(kMaxAgents) void comb_kernel(EnvArgs a) {
+__global__ __launch_bounds__(kMaxAgents) __attribute__((amdgpu_waves_per_eu(D2D_COMB_WAVES_PER_EU))) void comb_kernel(EnvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const Lane L = lane_geometry<LARGE>(a);
   const int N = a.N, F = a.F;
@@ -953,8 +965,9 @@ int check_desc(const d2d_env_desc* d) {
     if (d->max_deadline < 1 || d->max_deadline > 32) { d2d_set_error("max_deadline=%d outside [1,32]", d->max_deadline); return D2D_EUNSUPPORTED; }
     if (d->n_envs < 0) { d2d_set_error("n_envs < 0"); return D2D_EINVAL; }
     if (d->obs_dim < 2 || d->state_dim != 0 && d->state_stride < d->state_dim) { d2d_set_error("bad obs/state dims"); return D2D_EINVAL; }
-    if (!d->agents || !d->flip_thr || !d->arrival_kind_host || !d->period_host || !d->offset_host || !d->gather) {
-      d2d_set_error("desc tables (incl. the gather map) must be non-NULL"); return D2D_EINVAL;
+    if (!d->agents || !d->flip_thr || !d->arrival_kind_host || !d->period_host || !d->offset_host || !d->gather ||
+        !d->poisson_cdf) {
+      d2d_set_error("desc tables (incl. the gather map and poisson_cdf) must be non-NULL"); return D2D_EINVAL;
     }
     return D2D_OK;
   }
@@ -965,8 +978,8 @@ int check_desc(const d2d_env_desc* d) {
   const int F = comb ? d->max_deadline + 2 * d->n_channels : d->max_deadline + d->n_channels + 1;
   if (d->obs_dim != F) { d2d_set_error("obs_dim=%d, expected %d", d->obs_dim, F); return D2D_EINVAL; }
   if (d->state_stride < d->state_dim) { d2d_set_error("state_stride < state_dim"); return D2D_EINVAL; }
-  if (!d->agents || !d->flip_thr || !d->arrival_kind_host || !d->period_host || !d->offset_host) {
-    d2d_set_error("desc tables must be non-NULL"); return D2D_EINVAL;
+  if (!d->agents || !d->flip_thr || !d->arrival_kind_host || !d->period_host || !d->offset_host || !d->poisson_cdf) {
+    d2d_set_error("desc tables (incl. poisson_cdf) must be non-NULL"); return D2D_EINVAL;
   }
   return D2D_OK;
 }
@@ -1080,6 +1093,7 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
   a.E = d->n_envs; a.N = d->n_agents; a.C = d->n_channels; a.D = d->max_deadline; a.F = d->obs_dim;
   a.S = d->state_dim; a.state_stride = d->state_stride; a.reset = reset; a.rng_step = rng_step;
   a.env_base = d->env_base; a.seed = d->seed; a.agents = d->agents; a.flip_thr = d->flip_thr;
+  a.pois_cdf = d->poisson_cdf;
   a.buf = st->buffers; a.chan = st->channels; a.recv = st->received; a.disc = st->discarded;
   a.selq = st->sel_quality; a.seln = st->sel_count; a.actions = actions;
   if (rp) { a.flips = rp->flips; a.arrivals = rp->arrivals; }
@@ -1107,7 +1121,7 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
   // 512: 125 us, 1024: 134 us per 65,536 x 64-agent step)
   // 512-lane blocks (8 envs of 64 agents): comb 64 x 8 x 65,536 141 -> 137 us against 256-lane
   // blocks; single: 8 envs per gather-table read (256: 130 us, 512: 125 us, 1024: 134 us)
-  int block = large ? a.seg : 512;
+  int block = large ? a.seg : (comb && !a.obs && !a.state) ? D2D_COMB_REC_BLOCK : 512;
   a.cnt_words = cnt_words(large ? 1 : block / a.seg);
   while (!large && block > kWave && block > a.seg && lds_need(a, block, kind) > 65536) {
     block >>= 1;

@@ -36,7 +36,7 @@ def refuse_ablation(what):
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 5
+ABI_VERSION = 6
 D2D_OBS_F32, D2D_OBS_U8 = 0, 1
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
@@ -49,7 +49,8 @@ class EnvDesc(ctypes.Structure):
                 ("max_deadline", ctypes.c_int32), ("obs_dim", ctypes.c_int32), ("state_dim", ctypes.c_int32),
                 ("state_stride", ctypes.c_int32), ("n_envs", ctypes.c_int32), ("env_base", ctypes.c_uint64),
                 ("seed", ctypes.c_uint64), ("agents", _p), ("flip_thr", _p), ("arrival_kind_host", _p),
-                ("period_host", _p), ("offset_host", _p), ("gather", _p), ("rng_offset", _p)]
+                ("period_host", _p), ("offset_host", _p), ("gather", _p), ("rng_offset", _p),
+                ("poisson_cdf", _p)]
 
 
 class EnvState(ctypes.Structure):

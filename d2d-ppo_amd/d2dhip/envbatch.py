@@ -31,6 +31,7 @@ class EnvBatch:
         tab = spec.agent_table(self.kinds)
         self.agents = torch.from_numpy(tab.view(np.uint8).copy()).to(dev)
         self.flip_thr = torch.from_numpy(spec.flip_thresholds().view(np.int64).copy()).to(dev)
+        self.poisson_cdf = torch.from_numpy(spec.poisson_table(self.kinds).view(np.int32).copy()).to(dev)
         self._kinds_host = np.ascontiguousarray(self.kinds, dtype=np.uint8)
         self._period_host = np.ascontiguousarray(spec.period, dtype=np.float64)
         self._offset_host = np.ascontiguousarray(spec.offsets, dtype=np.float64)
@@ -68,7 +69,8 @@ class EnvBatch:
             _KIND_ID[s.kind], s.N, s.C, s.D, s.F, s.S, s.state_stride, E, int(env_base),
             int(seed) & 0xFFFFFFFFFFFFFFFF, self.agents.data_ptr(), self.flip_thr.data_ptr(),
             self._kinds_host.ctypes.data, self._period_host.ctypes.data, self._offset_host.ctypes.data,
-            None if self.gather is None else self.gather.data_ptr(), self.rng_off.data_ptr())
+            None if self.gather is None else self.gather.data_ptr(), self.rng_off.data_ptr(),
+            self.poisson_cdf.data_ptr())
         self.st = _lib.EnvState(self.buffers.data_ptr(), self.channels.data_ptr(), self.received.data_ptr(),
                                 self.discarded.data_ptr(),
                                 None if self.sel_quality is None else self.sel_quality.data_ptr(),

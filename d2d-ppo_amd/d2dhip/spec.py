@@ -28,6 +28,39 @@ def bernoulli_threshold(p):
     return np.floor(p * 4294967296.0).astype(np.uint64)
 
 
+POISSON_TABLE = 256
+
+
+def poisson_cdf_table(lam, kinds):
+    """Inverse-CDF thresholds of the Philox-mode Poisson arrival draw, uint32 [N][256].
+
+    The draw is the sequential inversion "x = 0; p = F = exp(-lam); while u >= F and x < 255:
+    x += 1; p = p * lam / x; F += p" of u = r * 2^-32 (d2d_hip.h, oracle/philox.py
+    poisson_inversion).  For an integer word r, u >= F_x  <=>  r >= ceil(F_x * 2^32), so with
+    t[x] = min(ceil(F_x * 2^32), 2^32) - 1 the result is the number of leading entries with
+    r > t[x]: the F_x are accumulated here in the same IEEE double operations, the table is
+    nondecreasing, and t[255] = 2^32 - 1 stops every search at the cap.  Rows of agents that do
+    not draw Poisson arrivals are all 2^32 - 1 (never read).
+    """
+    lam = np.asarray(lam, dtype=np.float64)
+    N = lam.shape[0]
+    t = np.full((N, POISSON_TABLE), 0xFFFFFFFF, dtype=np.uint64)
+    pois = np.asarray(kinds) == POISSON
+    if pois.any():
+        lp = lam[pois]
+        p = np.exp(-lam)[pois]  # the agent table's pois_p0, computed over the same array
+        F = p.copy()
+        cols = [F.copy()]
+        for x in range(1, POISSON_TABLE - 1):
+            p = (p * lp) / float(x)
+            F = F + p
+            cols.append(F.copy())
+        Fx = np.stack(cols, axis=1)                                   # [n][255]: F_0 .. F_254
+        ce = np.minimum(np.ceil(Fx * 4294967296.0), 4294967296.0)     # exact: power-of-two scaling
+        t[pois, :POISSON_TABLE - 1] = ce.astype(np.uint64) - np.uint64(1)
+    return t.astype(np.uint32)
+
+
 def buffer_words(D):
     return 1 if D <= 4 else 2 if D <= 8 else 3 if D <= 12 else 4 if D <= 16 else 8
 
@@ -148,6 +181,9 @@ class EnvSpec:
         t["pois_p0"] = np.exp(-self.lam)
         t["arrival_thr"] = bernoulli_threshold(self.q)
         return t
+
+    def poisson_table(self, kinds):
+        return poisson_cdf_table(self.lam, kinds)
 
     def gather_map(self, lib):
         """D2DEnv obs/state gather codes (d2d_env_single_gather_map, host-only)."""

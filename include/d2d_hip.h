@@ -43,7 +43,8 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 5  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format) */
+#define D2D_ABI_VERSION 6  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
+                              6: d2d_env_desc.poisson_cdf */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -88,6 +89,13 @@ typedef struct d2d_env_desc {
      * a captured HIP graph of reset/step calls replays with fresh Philox counters by
      * updating this one word instead of the baked launch arguments */
     const uint32_t* rng_offset;
+    /* device uint32 [N][256]: inverse-CDF thresholds of the Philox-mode Poisson arrival draw,
+     * t[k][x] = min(ceil(F_k(x) * 2^32), 2^32) - 1 with F_k(x) the running double sum
+     * exp(-lam), p = p * lam / x, F += p (x <= 254), t[k][255] = 2^32 - 1; the draw of word r is the
+     * number of leading entries with r > t[k][x] -- bitwise the sequential inversion of the reference
+     * oracle (oracle/philox.py poisson_inversion), without a double division per step.  Rows of
+     * non-Poisson agents are never read.  Required (spec.py poisson_cdf_table builds it). */
+    const uint32_t* poisson_cdf;
 } d2d_env_desc;
 
 typedef struct d2d_env_state {

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     for fn in fns:
         assert hasattr(lib, fn), fn
         assert fn in d2dhip.EXPORTED, f"{fn} has no ctypes signature"
-    assert lib.d2d_abi_version() == 5
+    assert lib.d2d_abi_version() == 6
     assert [lib.d2d_mask_bytes(c) for c in (1, 8, 9, 16, 17, 32)] == [1, 1, 2, 2, 4, 4]
     assert [lib.d2d_buffer_words(d) for d in (1, 4, 5, 8, 12, 14, 16, 17, 32)] == [1, 1, 2, 2, 3, 4, 4, 8, 8]
     assert lib.d2d_colstats_workspace(1000, 64) >= 64
@@ -38,7 +38,7 @@ def test_ctypes_structs_match_header_layout():
     from d2dhip import _lib
     from d2dhip.spec import AGENT_DTYPE
     assert AGENT_DTYPE.itemsize == 32
-    assert ctypes.sizeof(_lib.EnvDesc) == 8 * 4 + 8 * 2 + 8 * 7
+    assert ctypes.sizeof(_lib.EnvDesc) == 8 * 4 + 8 * 2 + 8 * 8
     assert ctypes.sizeof(_lib.MlpDesc) == 6 * 4 + 8 * 8 + 8 * 2 + 8 + 2 * 4 + 8
     assert ctypes.sizeof(_lib.EnvState) == 6 * 8 and ctypes.sizeof(_lib.EnvOut) == 6 * 8
     assert ctypes.sizeof(_lib.EnvReplay) == 2 * 8
@@ -56,7 +56,7 @@ def test_library_validates_arguments_without_gpu():
     lib = d2dhip.load()
     rc = lib.d2d_env_step(None, None, None, None, None, 1, 0, None)
     assert rc == -1 and b"desc" in lib.d2d_last_error()
-    desc = _lib.EnvDesc(0, 2000, 8, 7, 23, 0, 0, 1, 0, 0, None, None, None, None, None, None, None)
+    desc = _lib.EnvDesc(0, 2000, 8, 7, 23, 0, 0, 1, 0, 0, None, None, None, None, None, None, None, None)
     assert lib.d2d_env_reset(ctypes.byref(desc), None, None, None, 0, None) == -2
     assert lib.d2d_gae_scan(10, 1, 0, 1, None, None, None, 0.9, 0.97, 1, None, None, None) == -1
     # obs_format checks (before any HIP call)
@@ -71,7 +71,7 @@ def test_library_validates_arguments_without_gpu():
     assert lib.d2d_policy_mlp_step(ctypes.byref(md), ctypes.c_void_p(24), None, 0, 0, w, w, None, None) == -1
     assert b"aligned" in lib.d2d_last_error()
     # the record is a combinatorial-env output only
-    dsc = _lib.EnvDesc(1, 4, 3, 7, 11, 0, 0, 1, 0, 0, w, w, w, w, w, None, None)
+    dsc = _lib.EnvDesc(1, 4, 3, 7, 11, 0, 0, 1, 0, 0, w, w, w, w, w, None, None, w)
     st = _lib.EnvState(w, w, w, w, w, w)
     out = _lib.EnvOut(None, None, None, None, None, 16)
     assert lib.d2d_env_reset(ctypes.byref(dsc), ctypes.byref(st), None, ctypes.byref(out), 0, None) == -2

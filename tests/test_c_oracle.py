@@ -30,6 +30,36 @@ def test_poisson_inversion_moments():
         assert abs(x.var() - lam) < 0.05 * max(lam, 0.3)
 
 
+def test_poisson_cdf_table_equals_inversion():
+    """The kernels' Poisson draw searches spec.poisson_cdf_table (d2d_env_desc.poisson_cdf); it must
+    equal the oracle's sequential inversion for every word r.  Checked on Philox words, on every
+    threshold t and t + 1 (both sides of each boundary), on 0 / 2^32 - 1, and for the chunked
+    four-entry search the kernel runs (common.h poisson_lookup)."""
+    from d2dhip.spec import POISSON, SCHEDULED, poisson_cdf_table
+    lams = np.array([1 / 14, 1 / 3.5, 0.5, 2.5, 9.0, 33.0, 64.0, 0.25])
+    kinds = np.array([POISSON] * 7 + [SCHEDULED])
+    t = poisson_cdf_table(lams, kinds)
+    assert t.shape == (8, 256) and t.dtype == np.uint32
+    assert (t[7] == 0xFFFFFFFF).all() and (t[:, 255] == 0xFFFFFFFF).all()
+    assert (np.diff(t.astype(np.int64), axis=1) >= 0).all()
+    rnd = philox.words(np.arange(50000, dtype=np.uint64), 3, 0, 1, 1, 7)[..., 0]
+    for k in range(7):
+        tk = t[k].astype(np.uint64)
+        edge = np.concatenate([tk[:255], np.minimum(tk[:255] + 1, 0xFFFFFFFF)])
+        r = np.concatenate([rnd, edge, np.array([0, 0xFFFFFFFF], dtype=np.uint64)])
+        want = philox.poisson_inversion(r, lams[k], np.exp(-lams)[k])
+        got = np.searchsorted(tk, r, side="left")                   # count of entries t[x] < r
+        assert (got == want).all(), k
+        x = np.zeros(r.shape, dtype=np.int64)                       # the kernel's chunked search
+        live = np.ones(r.shape, dtype=bool)
+        while live.any():
+            q = np.stack([tk[np.minimum(x + i, 255)] for i in range(4)], axis=1)
+            n = (r[:, None] > q).sum(axis=1)
+            x = np.where(live, x + n, x)
+            live &= n == 4
+        assert (x == want).all(), k
+
+
 @pytest.mark.parametrize("name", env_fixture_names())
 def test_c_oracle_replays_reference(name):
     z = np.load(os.path.join(GOLDEN, f"env_{name}.npz"))
