@@ -135,7 +135,8 @@ __device__ __forceinline__ uint32_t relu_mask_pair(float r0, float r1) {
   uint32_t m0, m1;
   asm("v_min_u32 %0, %1, 1" : "=v"(m0) : "v"(r0));
   asm("v_min_u32 %0, %1, 1" : "=v"(m1) : "v"(r1));
-  return (m0 | (m1 << 16)) * 0x3F80u;
+  // 24-bit multiply (v_mul_u32_u24, full rate; a 32-bit constant multiply is v_mul_lo_u32, quarter rate)
+  return __umul24(m0 | (m1 << 16), 0x3F80u);
 }
 
 // high parts only (bf16-exact values)
