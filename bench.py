@@ -569,7 +569,11 @@ def gru_leg(args, rank, world, local):
       (2) the BPTT update kernel (PPO.train_step's evaluate + loss + backward through the padded
           training windows) over a 200-slot rollout of --gru-envs envs;
       (3) one whole D2D-PPO iteration (rollout + 5 epochs) at --gru-envs envs.
-    Roofline: fp32 MFMA (the kernels compute in v_mfma_f32_16x16x4_f32).  Algorithmic FLOP per
+    Roofline: the update kernel computes in v_mfma_f32_16x16x4_f32 (fraction of the fp32 MFMA
+    peak); the policy kernel's step runs v_mfma_f32_16x16x32_bf16 on exact three-way splits, so its
+    algorithmic rate is reported beside the MFMA pipe's busy fraction (its static instruction mix:
+    per 16-sample tile and window step 12 gate tiles x (3 input + 2 chunks x 6 recurrent) bf16 MFMAs
+    of 16 cycles, plus the head's 80 fp32 MFMAs of 32 cycles once per window).  Algorithmic FLOP per
     agent-sample and window step: GRU cell 2*3H*(F+1) + 2*3H*H (input + recurrent products); the
     update counts the forward and the two backward products (dW, dh) of every step: 3x that."""
     from algorithms.d2d_ppo import D2DPPO
@@ -614,6 +618,8 @@ def gru_leg(args, rank, world, local):
     cell = 2 * 3 * H * (F + 1) + 2 * 3 * H * H
     head = 2 * (H * H + H * 8)
     pol_flop = (L * cell + head) * E * N
+    pol_tiles = (E + 15) // 16 * N
+    pol_pipe = pol_tiles * (L * 12 * (3 + 2 * 6) * 16 + 80 * 32) / (1024 * 2.4e9) / (pol_ms / 1e3)
     del buf, lr, env, b
     torch.cuda.empty_cache()
     # (2) + (3) at --gru-envs envs
@@ -648,11 +654,13 @@ def gru_leg(args, rank, world, local):
     it_s = max_over_ranks(time.perf_counter() - t0, world)
     peak = 157.3
     out = {"config": f"xp_load.py learner: D2D-PPO, GRU H={H}, history_len={L}, {N} agents x 8 channels",
-           "policy_slot": {"envs_per_gpu": E, "window": L, "kernel": "d2d::gru_policy_kernel<4, 2, 0, sample>",
+           "policy_slot": {"envs_per_gpu": E, "window": L,
+                           "kernel": "d2d::gru_policy_kernel<4, 2, 0, sample, split>",
                            "ms": pol_ms, "agent_steps_per_s": E * world * N / (pol_ms / 1e3),
                            "env_steps_per_s": E * world / (pol_ms / 1e3),
-                           "flop": pol_flop, "achieved_tflops": pol_flop / (pol_ms / 1e3) / 1e12,
-                           "peak_tflops_fp32_mfma": peak, "frac": pol_flop / (pol_ms / 1e3) / 1e12 / peak},
+                           "flop": pol_flop, "achieved_tflops_fp32_equiv": pol_flop / (pol_ms / 1e3) / 1e12,
+                           "peak_tflops_fp32_mfma": peak, "frac_of_fp32_peak": pol_flop / (pol_ms / 1e3) / 1e12 / peak,
+                           "mfma_pipe_busy_frac": pol_pipe, "bound": "mfma"},
            "update": {"envs_per_gpu": E2, "slots": ro.T, "agent_samples": samples,
                       "kernel": "d2d::gru_grad_kernel<4, 2, 0>", "ms": grad_ms,
                       "agent_samples_per_s": samples * world / (grad_ms / 1e3), "flop": grad_flop,

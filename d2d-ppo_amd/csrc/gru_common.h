@@ -234,6 +234,152 @@ __device__ __forceinline__ void gru_gates(const f32x4 (&rz)[2 * HT], const f32x4
     }
 }
 
+// ---- exact-split bf16 variant of the step (the behaviour-policy kernel): v_mfma_f32_16x16x32_bf16
+// on three-way bf16 splits of the weights and of h (mlp_common.h split3 / mfma_split: the six part
+// products of weight >= 2^-16, fp32-accurate), 3.2x fewer MFMA cycles per step than the fp32
+// 16x16x4 products; policy slot 95 -> 50 ms at 65,536 envs x 64 agents x 64-step windows.
+//
+// K chunk c of a 16-row tile covers two accumulator tiles: lane (g, i) holds x[q][r] / h[t][r] for
+// q, t in {2c, 2c + 1}, so its B fragment takes k-slot 8g + j <-> input / unit 16 (2c + (j >> 2)) +
+// 4g + (j & 3) -- the h of one step is the next step's B operand without any data movement -- and
+// the weight images store each A fragment with the same permuted columns: fragment (T, c, part) of
+// lane (g, i) = the 8 k-slots of row 16T + i, as one 16-byte word ([T][c][part][lane], conflict-free
+// ds_read_b128).  Odd tile counts leave the upper half of the last chunk zero on both sides.
+// bf16 high parts of 8 floats (their exact value when the inputs are bf16-exact)
+__device__ __forceinline__ bf16x8 hi_frag_(const float (&v)[8]) {
+  uint32_t u[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) u[q] = pack_hi(v[2 * q], v[2 * q + 1]);
+  return as_frag(u);
+}
+__device__ __forceinline__ int chunk_col(int c, int g, int j) { return 16 * (2 * c + (j >> 2)) + 4 * g + (j & 3); }
+
+template <int HT, int IT>
+struct GruSplit {
+  static constexpr int HW = 16 * HT, NT = 3 * HT, CH = (HT + 1) / 2, CI = (IT + 1) / 2;
+  static constexpr int WIH = NT * CI * 3 * 64, WHH = NT * CH * 3 * 64;  // bf16x8 words
+};
+
+// Fill agent k's split images (all threads of the workgroup): the input image carries the summed r /
+// z biases and b_in at column F (x_F = 1), as load_gru_images does for the fp32 image.
+template <int HT, int IT>
+__device__ void load_gru_split_images(bf16x8* wih_b, bf16x8* whh_b, const GruW& w, int k, int H, int F, int tid,
+                                      int nthr) {
+  using S = GruSplit<HT, IT>;
+  const float* Wih = w.w_ih + (size_t)k * 3 * H * F;
+  const float* Whh = w.w_hh + (size_t)k * 3 * H * H;
+  const float* bih = w.b_ih + (size_t)k * 3 * H;
+  const float* bhh = w.b_hh + (size_t)k * 3 * H;
+  for (int idx = tid; idx < S::NT * (S::CI + S::CH) * 64; idx += nthr) {
+    const bool inp = idx < S::NT * S::CI * 64;
+    const int rel = inp ? idx : idx - S::NT * S::CI * 64, NC = inp ? S::CI : S::CH;
+    const int T = rel / (NC * 64), c = (rel / 64) % NC, lane = rel & 63, g = lane >> 4, i = lane & 15;
+    const int R = 16 * T + i, G = R / S::HW, u = R - G * S::HW, src = G * H + u;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int col = chunk_col(c, g, j);
+      v[j] = 0.f;
+      if (u < H) {
+        if (inp) {
+          if (col < F) v[j] = Wih[(size_t)src * F + col];
+          else if (col == F) v[j] = G < 2 ? bih[src] + bhh[src] : bih[src];
+        } else if (col < H) {
+          v[j] = Whh[(size_t)src * H + col];
+        }
+      }
+      if (2 * c + (j >> 2) >= (inp ? IT : HT)) v[j] = 0.f;
+    }
+    const Parts p = split3(v);
+    bf16x8* dst = (inp ? wih_b : whh_b) + ((T * NC + c) * 3) * 64 + lane;
+    dst[0] = p.h;
+    dst[64] = p.m;
+    dst[128] = p.l;
+  }
+}
+
+// chunk c of a lane's two accumulator-layout tiles as 8 k-slot values
+template <int NTL>
+__device__ __forceinline__ void chunk_vals(float (&v)[8], const float (&t)[NTL][4], int c) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = 2 * c + (j >> 2) < NTL ? t[2 * c + (j >> 2)][j & 3] : 0.f;
+}
+
+// acc += W.X with all split products of weight >= 2^-24 (mfma_split's six plus m.l and l.m; only
+// l.l dropped): ~2^-32 relative per product.  Ablation D2D_GRU_SPLIT8: measured 12 % slower per
+// policy slot than the default six terms (2^-23 per product, the MLP kernels' choice) with the same
+// worst-case log-prob error in tests/test_gru_gpu.py (tools/gpu/gru_diag.py: the window's fp32 gate
+// math and the fp32 Bernoulli probabilities dominate, not the product split).
+__device__ __forceinline__ f32x4 mfma_split8(const Parts& w, const Parts& x, f32x4 acc) {
+  acc = mfma_bf16(w.m, x.l, acc);
+  acc = mfma_bf16(w.l, x.m, acc);
+  acc = mfma_bf16(w.h, x.l, acc);
+  acc = mfma_bf16(w.m, x.m, acc);
+  acc = mfma_bf16(w.l, x.h, acc);
+  acc = mfma_bf16(w.h, x.m, acc);
+  acc = mfma_bf16(w.m, x.h, acc);
+  acc = mfma_bf16(w.h, x.h, acc);
+  return acc;
+}
+
+// gru_preact on the split images.  x_exact (wave-uniform): every input of the step is bf16-exact
+// (always for the compact record), so the input products need only the three weight parts.
+template <int HT, int IT>
+__device__ __forceinline__ void gru_preact_split(const bf16x8* wih_b, const bf16x8* whh_b, int lane,
+                                                 const float (&x)[IT][4], bool x_exact, const float (&h)[HT][4],
+                                                 const f32x4 (&bhn)[HT], f32x4 (&rz)[2 * HT], f32x4 (&ni)[HT],
+                                                 f32x4 (&nh)[HT], bool h_zero) {
+  using S = GruSplit<HT, IT>;
+  Parts xp[S::CI];
+#pragma unroll
+  for (int c = 0; c < S::CI; ++c) {
+    float v[8];
+    chunk_vals<IT>(v, x, c);
+    if (x_exact) {
+      xp[c].h = hi_frag_(v);
+      xp[c].m = xp[c].l = bf16x8{};
+    } else {
+      xp[c] = split3(v);
+    }
+  }
+#pragma unroll
+  for (int T = 0; T < S::NT; ++T) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < S::CI; ++c) {
+      const bf16x8* wf = wih_b + ((T * S::CI + c) * 3) * 64 + lane;
+      acc = mfma_split(Parts{wf[0], wf[64], wf[128]}, xp[c], x_exact, acc);
+    }
+    if (T < 2 * HT) rz[T] = acc;
+    else ni[T - 2 * HT] = acc;
+  }
+#pragma unroll
+  for (int t = 0; t < HT; ++t) nh[t] = bhn[t];
+  if (h_zero) return;
+  Parts hp[S::CH];
+#pragma unroll
+  for (int c = 0; c < S::CH; ++c) {
+    float v[8];
+    chunk_vals<HT>(v, h, c);
+    hp[c] = split3(v);
+  }
+#pragma unroll
+  for (int T = 0; T < S::NT; ++T) {
+    f32x4 acc = T < 2 * HT ? rz[T] : nh[T - 2 * HT];
+#pragma unroll
+    for (int c = 0; c < S::CH; ++c) {
+      const bf16x8* wf = whh_b + ((T * S::CH + c) * 3) * 64 + lane;
+#if D2D_GRU_SPLIT8  // ablation: eight terms
+      acc = mfma_split8(Parts{wf[0], wf[64], wf[128]}, hp[c], acc);
+#else
+      acc = mfma_split(Parts{wf[0], wf[64], wf[128]}, hp[c], false, acc);
+#endif
+    }
+    if (T < 2 * HT) rz[T] = acc;
+    else nh[T - 2 * HT] = acc;
+  }
+}
+
 // b_hn of agent k in accumulator layout (unit 16t + 4g + r)
 template <int HT>
 __device__ __forceinline__ void load_bhn(f32x4 (&bhn)[HT], const GruW& w, int k, int H, int g) {

@@ -54,17 +54,25 @@ enum { kGruBernoulli = 0, kGruCategorical = 1, kGruValue = 2 };
 // ------------------------------------------------------------------------------ policy kernel
 // Workgroup = agent k x a strided set of tiles; 8 waves (2 per SIMD), one 16-env tile per wave at a
 // time.  LDS: the agent's input and recurrent images (fp32, swizzled; 72 KB at H = 64, F < 32).
-template <int HT, int IT, int KIND, int MODE>
+// SPLIT: the step on v_mfma_f32_16x16x32_bf16 over exact three-way splits (gru_preact_split; LDS:
+// the split images, 108 KB at H = 64, F < 32), else on v_mfma_f32_16x16x4_f32 (gru_preact).
+template <int HT, int IT, int KIND, int MODE, bool SPLIT>
 __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
   constexpr int HW = 16 * HT, IW = 16 * IT, R3 = 3 * HW;
-  __shared__ float wih_s[R3 * IW];
-  __shared__ float whh_s[R3 * HW];
+  using SP = GruSplit<HT, IT>;
+  constexpr int IMG_BYTES = SPLIT ? 16 * (SP::WIH + SP::WHH) : 4 * (R3 * IW + R3 * HW);
+  __shared__ __attribute__((aligned(16))) unsigned char img_raw[IMG_BYTES];
+  float* wih_s = reinterpret_cast<float*>(img_raw);
+  float* whh_s = wih_s + R3 * IW;
+  bf16x8* wih_b = reinterpret_cast<bf16x8*>(img_raw);
+  bf16x8* whh_b = wih_b + SP::WIH;
   __shared__ float head_s[HeadImg<HT>::SIZE];
   const int k = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H, F = a.F, N = a.N, E = a.E;
-  load_gru_images<HT, IT>(wih_s, whh_s, a.w, k, H, F, tid, blockDim.x);
+  if constexpr (SPLIT) load_gru_split_images<HT, IT>(wih_b, whh_b, a.w, k, H, F, tid, blockDim.x);
+  else load_gru_images<HT, IT>(wih_s, whh_s, a.w, k, H, F, tid, blockDim.x);
   for (int idx = tid; idx < HeadImg<HT>::SIZE; idx += blockDim.x)
     head_s[idx] = head_img_elem<HT>(a.w, k, H, KIND == kGruValue ? 1 : a.A, idx);
   f32x4 bhn[HT];
@@ -99,7 +107,21 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
       load_x<IT>(x, a.ov, ((size_t)row_slot * E + e0) * N + k, xsg, g, i, ok, zero);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
-      gru_preact<HT, IT, true>(wih_s + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
+      if constexpr (SPLIT) {
+        // every input bf16-exact (record bytes, integer fp32 rows): three weight-part products only
+        bool x_exact = a.ov.u8 != 0;
+        if (!x_exact) {
+          uint32_t low = 0;
+#pragma unroll
+          for (int q = 0; q < IT; ++q)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) low |= fbits(x[q][r]) & 0xFFFFu;
+          x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;
+        }
+        gru_preact_split<HT, IT>(wih_b + z, whh_b + z, lane, x, x_exact, h, bhn, rz, ni, nh, j == 0);
+      } else {
+        gru_preact<HT, IT, true>(wih_s + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
+      }
       gru_gates<HT>(rz, ni, nh, h);
     }
     f32x4 pre1[HT], lg;
@@ -696,16 +718,31 @@ __global__ void gru_reduce_kernel(const float* __restrict__ partial, int G, int 
 
 using namespace d2d;
 
-template <int HT, int IT, int KIND>
-static void launch_policy_mode(const GruArgs& a, dim3 grid, hipStream_t s) {
+extern int g_policy_f32_mfma;  // policy_kernels.hip (D2D_OPT_POLICY_F32_MFMA)
+
+template <int HT, int IT, int KIND, bool SPLIT>
+static void launch_policy_split(const GruArgs& a, dim3 grid, hipStream_t s) {
   if (KIND == kGruValue || a.ep.forced == nullptr) {
     if (KIND != kGruValue && a.ep.deterministic)
-      hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeDeterministic>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeDeterministic, SPLIT>), grid, dim3(512), 0, s, a);
     else
-      hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeSample>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeSample, SPLIT>), grid, dim3(512), 0, s, a);
   } else {
-    hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeForced>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeForced, SPLIT>), grid, dim3(512), 0, s, a);
   }
+}
+
+// the split kernel where its images fit LDS (IT <= 2: F < 32); the fp32-MFMA kernel otherwise or
+// when D2D_OPT_POLICY_F32_MFMA asks for it (A/B timing and tests)
+template <int HT, int IT, int KIND>
+static void launch_policy_mode(const GruArgs& a, dim3 grid, hipStream_t s) {
+  if constexpr (IT <= 2) {
+    if (!g_policy_f32_mfma) {
+      launch_policy_split<HT, IT, KIND, true>(a, grid, s);
+      return;
+    }
+  }
+  launch_policy_split<HT, IT, KIND, false>(a, grid, s);
 }
 
 template <int HT, int IT>
