@@ -260,42 +260,67 @@ struct GruSplit {
   static constexpr int WIH = NT * CI * 3 * 64, WHH = NT * CH * 3 * 64;  // bf16x8 words
 };
 
-// Fill agent k's split images (all threads of the workgroup): the input image carries the summed r /
-// z biases and b_in at column F (x_F = 1), as load_gru_images does for the fp32 image.
+// Fragment `rel` of agent k's input (inp) or recurrent split image: rel = (T * NC + c) * 64 + lane,
+// its three parts stored 64 words apart ([T][c][part][lane]).  The input image carries the summed
+// r / z biases and b_in at column F (x_F = 1), as load_gru_images does for the fp32 image.
 template <int HT, int IT>
-__device__ void load_gru_split_images(bf16x8* wih_b, bf16x8* whh_b, const GruW& w, int k, int H, int F, int tid,
-                                      int nthr) {
+__device__ __forceinline__ Parts split_frag(const GruW& w, int k, int H, int F, bool inp, int rel) {
   using S = GruSplit<HT, IT>;
+  const int NC = inp ? S::CI : S::CH;
+  const int T = rel / (NC * 64), c = (rel / 64) % NC, lane = rel & 63, g = lane >> 4, i = lane & 15;
+  const int R = 16 * T + i, G = R / S::HW, u = R - G * S::HW, src = G * H + u;
   const float* Wih = w.w_ih + (size_t)k * 3 * H * F;
   const float* Whh = w.w_hh + (size_t)k * 3 * H * H;
   const float* bih = w.b_ih + (size_t)k * 3 * H;
   const float* bhh = w.b_hh + (size_t)k * 3 * H;
-  for (int idx = tid; idx < S::NT * (S::CI + S::CH) * 64; idx += nthr) {
-    const bool inp = idx < S::NT * S::CI * 64;
-    const int rel = inp ? idx : idx - S::NT * S::CI * 64, NC = inp ? S::CI : S::CH;
-    const int T = rel / (NC * 64), c = (rel / 64) % NC, lane = rel & 63, g = lane >> 4, i = lane & 15;
-    const int R = 16 * T + i, G = R / S::HW, u = R - G * S::HW, src = G * H + u;
-    float v[8];
+  float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int col = chunk_col(c, g, j);
-      v[j] = 0.f;
-      if (u < H) {
-        if (inp) {
-          if (col < F) v[j] = Wih[(size_t)src * F + col];
-          else if (col == F) v[j] = G < 2 ? bih[src] + bhh[src] : bih[src];
-        } else if (col < H) {
-          v[j] = Whh[(size_t)src * H + col];
-        }
+  for (int j = 0; j < 8; ++j) {
+    const int col = chunk_col(c, g, j);
+    v[j] = 0.f;
+    if (u < H) {
+      if (inp) {
+        if (col < F) v[j] = Wih[(size_t)src * F + col];
+        else if (col == F) v[j] = G < 2 ? bih[src] + bhh[src] : bih[src];
+      } else if (col < H) {
+        v[j] = Whh[(size_t)src * H + col];
       }
-      if (2 * c + (j >> 2) >= (inp ? IT : HT)) v[j] = 0.f;
     }
-    const Parts p = split3(v);
-    bf16x8* dst = (inp ? wih_b : whh_b) + ((T * NC + c) * 3) * 64 + lane;
-    dst[0] = p.h;
-    dst[64] = p.m;
-    dst[128] = p.l;
+    if (2 * c + (j >> 2) >= (inp ? IT : HT)) v[j] = 0.f;
   }
+  return split3(v);
+}
+__device__ __forceinline__ void store_parts(bf16x8* dst, const Parts& p) {
+  dst[0] = p.h;
+  dst[64] = p.m;
+  dst[128] = p.l;
+}
+__device__ __forceinline__ int split_word(int rel) { return (rel >> 6) * 3 * 64 + (rel & 63); }
+
+// Fill agent k's split images in LDS (all threads of the workgroup); either may be NULL.
+template <int HT, int IT>
+__device__ void load_gru_split_images(bf16x8* wih_b, bf16x8* whh_b, const GruW& w, int k, int H, int F, int tid,
+                                      int nthr) {
+  using S = GruSplit<HT, IT>;
+  if (wih_b)
+    for (int rel = tid; rel < S::NT * S::CI * 64; rel += nthr)
+      store_parts(wih_b + split_word(rel), split_frag<HT, IT>(w, k, H, F, true, rel));
+  if (whh_b)
+    for (int rel = tid; rel < S::NT * S::CH * 64; rel += nthr)
+      store_parts(whh_b + split_word(rel), split_frag<HT, IT>(w, k, H, F, false, rel));
+}
+
+// Whether every input of a window step is bf16-exact (wave-uniform): always for the compact record,
+// one ballot over the low halves for fp32 rows.
+template <int IT>
+__device__ __forceinline__ bool x_exact_step(const ObsView& ov, const float (&x)[IT][4]) {
+  if (ov.u8) return true;
+  uint32_t low = 0;
+#pragma unroll
+  for (int q = 0; q < IT; ++q)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) low |= fbits(x[q][r]) & 0xFFFFu;
+  return __builtin_amdgcn_ballot_w64(low != 0) == 0;
 }
 
 // chunk c of a lane's two accumulator-layout tiles as 8 k-slot values

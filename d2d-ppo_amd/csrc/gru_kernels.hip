@@ -109,16 +109,7 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
       const int z = opaque_zero();
       if constexpr (SPLIT) {
         // every input bf16-exact (record bytes, integer fp32 rows): three weight-part products only
-        bool x_exact = a.ov.u8 != 0;
-        if (!x_exact) {
-          uint32_t low = 0;
-#pragma unroll
-          for (int q = 0; q < IT; ++q)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) low |= fbits(x[q][r]) & 0xFFFFu;
-          x_exact = __builtin_amdgcn_ballot_w64(low != 0) == 0;
-        }
-        gru_preact_split<HT, IT>(wih_b + z, whh_b + z, lane, x, x_exact, h, bhn, rz, ni, nh, j == 0);
+        gru_preact_split<HT, IT>(wih_b + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), h, bhn, rz, ni, nh, j == 0);
       } else {
         gru_preact<HT, IT, true>(wih_s + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
       }
@@ -250,10 +241,16 @@ struct GruOff {
 // writes its dgi / dgh_n / h_{j-1} rows (sample-on-k layout, through the wave's LDS scratch) to a
 // per-wave global history, and after the window one GEMM per tile with K = L x 16 accumulates them
 // in registers and adds them into the wave's global sums -- deterministic (no atomics anywhere).
-template <int HT, int IT, int KIND>
+// SPLIT (default): the forward and the BPTT recompute on the policy kernel's split step
+// (gru_preact_split: the 74 KB split W_hh image in LDS, the split W_ih image from L2); the scratch is
+// then 2 HW rows per wave (the step's gradient rows leave it in three passes), 155 KB in all.
+template <int HT, int IT, int KIND, bool SPLIT>
 __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
-  constexpr int HW = 16 * HT, R3 = 3 * HW, RT = R3 + 4, SROWS = R3;
-  __shared__ float whh_s[R3 * HW];
+  constexpr int HW = 16 * HT, R3 = 3 * HW, RT = R3 + 4, SROWS = 2 * HW;
+  using SP = GruSplit<HT, IT>;
+  __shared__ __attribute__((aligned(16))) unsigned char whh_raw[SPLIT ? 16 * SP::WHH : 4 * R3 * HW];
+  float* whh_s = reinterpret_cast<float*>(whh_raw);
+  bf16x8* whh_b = reinterpret_cast<bf16x8*>(whh_raw);
   __shared__ __attribute__((aligned(16))) float whhT_s[HW * RT];  // [unit u][gate row R], row stride R3 + 4
   __shared__ __attribute__((aligned(16))) float scr[4][SROWS * 16];
   const int k = blockIdx.x;
@@ -266,9 +263,10 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     for (int idx = tid; idx < R3 * HW; idx += blockDim.x) {
       const int R = idx / HW, c = idx - R * HW, G = R / HW, u = R - G * HW;
       const float v = (u < H && c < H) ? Whh[(size_t)(G * H + u) * H + c] : 0.f;
-      whh_s[swz<HW>(R, c)] = v;
+      if constexpr (!SPLIT) whh_s[swz<HW>(R, c)] = v;
       whhT_s[c * RT + R] = v;
     }
+    if constexpr (SPLIT) load_gru_split_images<HT, IT>(nullptr, whh_b, a.w, k, H, F, tid, blockDim.x);
   }
   f32x4 bhn[HT];
   load_bhn<HT>(bhn, a.w, k, H, g);
@@ -279,6 +277,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   // the input image of gru_common.h (bias column F) written by gru_wih_image_kernel: A fragments
   // straight from L2 every step (registers are the update kernel's scarce resource)
   const float* wimg = a.wimg + (size_t)k * 3 * HW * (16 * IT);
+  const bf16x8* wih_g = reinterpret_cast<const bf16x8*>(a.wimg) + (size_t)k * SP::WIH;  // SPLIT: split image
   const SwzOff<16 * IT> oi(g, i);  // (unused: W_ih comes from the global image)
   const SwzOff<HW> oh(g, i);
   const XSigns<IT> xsg(a.ov, k);
@@ -316,7 +315,10 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       load_x<IT>(x, a.ov, row_of(j), xsg, g, i, ok, j < pad);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
-      gru_preact<HT, IT, false>(wimg + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
+      if constexpr (SPLIT)
+        gru_preact_split<HT, IT>(wih_g + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), h, bhn, rz, ni, nh, j == 0);
+      else
+        gru_preact<HT, IT, false>(wimg + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
       gru_gates<HT>(rz, ni, nh, h);
       if (j + 1 < L) {
         f32x4* dst = reinterpret_cast<f32x4*>(hist + ((size_t)j * 64 + lane) * 4 * HT);
@@ -434,8 +436,10 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       load_x<IT>(x, a.ov, xrow, xsg, g, i, ok, zero);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
-      const float* wh = whh_s + z;
-      gru_preact<HT, IT, false>(wimg + z, wh, oi, oh, x, hp, bhn, rz, ni, nh, g, i, j == 0);
+      if constexpr (SPLIT)
+        gru_preact_split<HT, IT>(wih_g + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), hp, bhn, rz, ni, nh, j == 0);
+      else
+        gru_preact<HT, IT, false>(wimg + z, whh_s + z, oi, oh, x, hp, bhn, rz, ni, nh, g, i, j == 0);
       __builtin_amdgcn_sched_barrier(0);
       float drp[HT][4], dzp[HT][4], dnp[HT][4], dghn[HT][4], gz[HT][4];
 #pragma unroll
@@ -454,35 +458,29 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
           acc.bhn[t][r] += dghn[t][r];
         }
       // this step's rows of the weight-gradient GEMMs, through the wave's scratch (sample-on-k layout)
-      // to the global history: dgi (r, z, n_in rows), then dgh_n (= dn_pre * r) and h_{j-1}
+      // to the global history, two row blocks per pass: dgi (r, z, n_in rows), dgh_n (= dn_pre * r),
+      // h_{j-1} -- rows [0, 5 HW) of the step's history block
       float* hrow = ghist + (size_t)j * 5 * HW * 16;
+      auto stage_rows = [&](const float (&b0)[HT][4], const float (*b1)[4], int row0) {
 #pragma unroll
-      for (int t = 0; t < HT; ++t)
+        for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int u = 16 * t + 4 * g + r, c = pcol(i);
-          sc[u * 16 + c] = drp[t][r];
-          sc[(HW + u) * 16 + c] = dzp[t][r];
-          sc[(2 * HW + u) * 16 + c] = dnp[t][r];
-        }
-      lds_order();
+          for (int r = 0; r < 4; ++r) {
+            const int u = 16 * t + 4 * g + r, c = pcol(i);
+            sc[u * 16 + c] = b0[t][r];
+            if (b1) sc[(HW + u) * 16 + c] = b1[t][r];
+          }
+        lds_order();
+        const int nv = (b1 ? 2 : 1) * HW * 4 / 64;
 #pragma unroll
-      for (int v = 0; v < R3 * 4 / 64; ++v)
-        reinterpret_cast<f32x4*>(hrow)[v * 64 + lane] = reinterpret_cast<const f32x4*>(sc)[v * 64 + lane];
-      lds_order();
-#pragma unroll
-      for (int t = 0; t < HT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int u = 16 * t + 4 * g + r, c = pcol(i);
-          sc[u * 16 + c] = dghn[t][r];
-          sc[(HW + u) * 16 + c] = hp[t][r];
-        }
-      lds_order();
-#pragma unroll
-      for (int v = 0; v < 2 * HW * 4 / 64; ++v)
-        reinterpret_cast<f32x4*>(hrow + R3 * 16)[v * 64 + lane] = reinterpret_cast<const f32x4*>(sc)[v * 64 + lane];
-      lds_order();
+        for (int v = 0; v < 2 * HW * 4 / 64; ++v)
+          if (v < nv)
+            reinterpret_cast<f32x4*>(hrow + row0 * 16)[v * 64 + lane] = reinterpret_cast<const f32x4*>(sc)[v * 64 + lane];
+        lds_order();
+      };
+      stage_rows(drp, dzp, 0);
+      stage_rows(dnp, dghn, 2 * HW);
+      stage_rows(hp, nullptr, 4 * HW);
       __builtin_amdgcn_sched_barrier(0);
       // dh_{j-1} = g z + W_hh^T dgh: A fragments from the transposed image, 4 k-steps per ds_read_b128
       const float* wt = whhT_s + z;
@@ -851,7 +849,8 @@ static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, 
   w.partial = 0;
   w.hist = up(G * N * P);
   w.wimg = w.hist + up(waves * L * 64 * 4 * htp);
-  w.hacc = w.wimg + up(N * 3 * HW * 32);
+  // fp32 input images [N][3 HW][32] or the split ones [N][3 htp][1][3 parts][64] 16-byte words
+  w.hacc = w.wimg + up(N * std::max<int64_t>(3 * HW * 32, 3 * htp * 3 * 64 * 4));
   w.himg = w.hacc + up(waves * 64 * (htp * htp * 4 + htp * 8 + 4));
   w.ghist = w.himg + up(N * (HW * HW + 16 * HW + HW + 16));
   w.gpart = w.ghist + up(waves * L * 5 * HW * 16);
@@ -868,12 +867,37 @@ extern "C" int64_t d2d_gru_grad_workspace(const d2d_gru_desc* d, int32_t T) {
   return gru_ws_layout(G, d->n_agents, o.P, d->history_len, ht, d->obs_dim + 1 <= 16 ? 1 : 2).total;
 }
 
+#ifndef D2D_GRU_GRAD_SPLIT
+#define D2D_GRU_GRAD_SPLIT 1  // 0: the fp32-MFMA step in the update kernel (ablation builds)
+#endif
+constexpr bool kGradSplit = D2D_GRU_GRAD_SPLIT != 0;
+
 template <int HT, int IT>
 static void launch_grad_kind(const GruArgs& a, dim3 grid, hipStream_t s) {
-  if (a.kind == kGruBernoulli) hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruBernoulli>), grid, dim3(256), 0, s, a);
+  if (a.kind == kGruBernoulli)
+    hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruBernoulli, kGradSplit>), grid, dim3(256), 0, s, a);
   else if (a.kind == kGruCategorical)
-    hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruCategorical>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruValue>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruCategorical, kGradSplit>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruValue, kGradSplit>), grid, dim3(256), 0, s, a);
+}
+
+// the split W_ih images of all agents in the update workspace ([N][GruSplit::WIH] 16-byte words)
+template <int HT, int IT>
+__global__ void gru_wih_split_image_kernel(GruW w, int N, int H, int F, bf16x8* img) {
+  using S = GruSplit<HT, IT>;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  constexpr int PER = S::NT * S::CI * 64;
+  if (idx >= (int64_t)N * PER) return;
+  const int k = (int)(idx / PER), rel = (int)(idx - (int64_t)k * PER);
+  store_parts(img + (size_t)k * S::WIH + split_word(rel), split_frag<HT, IT>(w, k, H, F, true, rel));
+}
+template <int HT>
+static void launch_wih_split(const GruArgs& a, int itp, hipStream_t s) {
+  const int64_t n = (int64_t)a.N * 3 * HT * 64;  // CI = 1 for IT <= 2
+  const dim3 grid((unsigned)((n + 255) / 256));
+  bf16x8* img = reinterpret_cast<bf16x8*>(a.wimg);
+  if (itp == 1) hipLaunchKernelGGL((gru_wih_split_image_kernel<HT, 1>), grid, dim3(256), 0, s, a.w, a.N, a.H, a.F, img);
+  else hipLaunchKernelGGL((gru_wih_split_image_kernel<HT, 2>), grid, dim3(256), 0, s, a.w, a.N, a.H, a.F, img);
 }
 
 extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, const void* actions,
@@ -921,9 +945,15 @@ extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, c
   if (a.N == 0) return D2D_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   {
-    const int64_t n = (int64_t)a.N * 3 * 16 * htp * 16 * itp;
-    hipLaunchKernelGGL(gru_wih_image_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.w, a.N, a.H, a.F,
-                       16 * htp, 16 * itp, a.wimg);
+    if (kGradSplit) {
+      if (htp == 1) launch_wih_split<1>(a, itp, s);
+      else if (htp == 2) launch_wih_split<2>(a, itp, s);
+      else launch_wih_split<4>(a, itp, s);
+    } else {
+      const int64_t n = (int64_t)a.N * 3 * 16 * htp * 16 * itp;
+      hipLaunchKernelGGL(gru_wih_image_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.w, a.N, a.H, a.F,
+                         16 * htp, 16 * itp, a.wimg);
+    }
     const int64_t nh = (int64_t)a.N * (16 * htp * 16 * htp + 16 * 16 * htp + 16 * htp + 16);
     const dim3 gh((unsigned)((nh + 255) / 256));
     if (htp == 1) hipLaunchKernelGGL(gru_head_image_kernel<1>, gh, dim3(256), 0, s, a.w, a.N, a.H, a.A, a.himg);
