@@ -22,6 +22,12 @@
 #include "policy_epilogue.h"
 #include "ppo_epilogue.h"
 
+#ifndef D2D_GRU_ABLATE
+// != 0 only in tools/gpu/build_ablate_gru.sh's timing builds (wrong gradients by design):
+// 1 no weight-gradient GEMMs, 2 no dh MFMAs, 3 no history staging, 4 no BPTT gate recompute
+#define D2D_GRU_ABLATE 0
+#endif
+
 namespace d2d {
 
 struct GruArgs {
@@ -436,10 +442,18 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       load_x<IT>(x, a.ov, xrow, xsg, g, i, ok, zero);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
+#if D2D_GRU_ABLATE == 4
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        rz[t] = rz[HT + t] = f32x4{hp[t][0], hp[t][1], hp[t][2], hp[t][3]};
+        ni[t] = nh[t] = f32x4{x[0][0], x[0][1], x[0][2], x[0][3]};
+      }
+#else
       if constexpr (SPLIT)
         gru_preact_split<HT, IT>(wih_g + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), hp, bhn, rz, ni, nh, j == 0);
       else
         gru_preact<HT, IT, false>(wimg + z, whh_s + z, oi, oh, x, hp, bhn, rz, ni, nh, g, i, j == 0);
+#endif
       __builtin_amdgcn_sched_barrier(0);
       float drp[HT][4], dzp[HT][4], dnp[HT][4], dghn[HT][4], gz[HT][4];
 #pragma unroll
@@ -478,15 +492,20 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
             reinterpret_cast<f32x4*>(hrow + row0 * 16)[v * 64 + lane] = reinterpret_cast<const f32x4*>(sc)[v * 64 + lane];
         lds_order();
       };
+#if D2D_GRU_ABLATE != 3
       stage_rows(drp, dzp, 0);
       stage_rows(dnp, dghn, 2 * HW);
       stage_rows(hp, nullptr, 4 * HW);
+#endif
       __builtin_amdgcn_sched_barrier(0);
       // dh_{j-1} = g z + W_hh^T dgh: A fragments from the transposed image, 4 k-steps per ds_read_b128
       const float* wt = whhT_s + z;
 #pragma unroll
       for (int t = 0; t < HT; ++t) {
         f32x4 dh = {gz[t][0], gz[t][1], gz[t][2], gz[t][3]};
+#if D2D_GRU_ABLATE == 2
+        dh += f32x4{drp[t][0], dzp[t][1], dghn[t][2], wt[lane]};
+#else
 #pragma unroll
         for (int T = 0; T < 3 * HT; ++T) {
           const f32x4 wv = *reinterpret_cast<const f32x4*>(wt + (16 * t + i) * RT + 16 * T + 4 * g);
@@ -496,6 +515,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
             dh = mfma4(wv[s4], bv, dh);
           }
         }
+#endif
 #pragma unroll
         for (int r = 0; r < 4; ++r) gcur[t][r] = dh[r];
       }
@@ -504,7 +524,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     // ---- the tile's weight-gradient GEMMs over the history, K = L steps x 16 samples, one hidden
     // tile tb (its r, z, n gate tiles) at a time: dW_hh += dgh h_{j-1}^T, dW_ih += dgi x^T
 #pragma unroll 1
-    for (int tb = 0; tb < HT; ++tb) {
+    for (int tb = 0; tb < (D2D_GRU_ABLATE == 1 ? 0 : HT); ++tb) {
       f32x4 dwh[3][HT], dwi[3][IT];
 #pragma unroll
       for (int g3 = 0; g3 < 3; ++g3) {
