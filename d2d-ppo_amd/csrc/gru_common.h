@@ -137,34 +137,77 @@ struct XSigns {
 // column F = 1, columns past F = 0.  `row0` = row index (slot, e0, agent k) of env e0; consecutive
 // envs are N rows apart; rows of envs >= E read 0 through the range-checked buffer descriptor
 // (zero: the x of a front-padding step, bias column only).
+// A range-checked buffer descriptor from WAVE-UNIFORM values, read through readfirstlane: the
+// compiler cannot always prove a base / extent uniform (they derive from the tile and window step),
+// and a descriptor it takes for divergent costs a waterfall loop (readfirstlane, compare, exec
+// masking, one load per pass) around every buffer load.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint32_t nbytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                           __builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
+}
+
+// descriptor of the rows from row0 on (row0 and zero wave-uniform; zero: none -- reads return 0)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const ObsView& ov, size_t row0, bool zero) {
+  const int64_t rest = (ov.rows - (int64_t)row0) * ov.RB;
+  const uint32_t nbytes = zero || rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
+  return uniform_rsrc(ov.base + row0 * ov.RB, nbytes);
+}
+
+template <int IT>
+struct XRaw {     // the raw words of one x tile (issued ahead of use: decode_x waits for them)
+  uint32_t w[IT][4];  // fp32 rows: inputs 16q + 4g + r; record: w[q][0] = bytes 16q + 4g .. + 3
+  bool zero;
+};
+template <int IT>
+__device__ __forceinline__ void load_x_raw(XRaw<IT>& xr, const ObsView& ov, size_t row0, int g, int i, bool env_ok,
+                                           bool zero) {
+  const __amdgpu_buffer_rsrc_t rsrc = rows_rsrc(ov, row0, zero);
+  const uint32_t vbase = env_ok ? (uint32_t)(i * ov.N * ov.RB) : 0x80000000u;
+  xr.zero = zero;
+#pragma unroll
+  for (int q = 0; q < IT; ++q) {
+    if (ov.u8) {  // wave-uniform
+      xr.w[q][0] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vbase + (uint32_t)(16 * q + 4 * g), 0, 0);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        xr.w[q][r] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vbase + 4u * (uint32_t)(16 * q + 4 * g + r), 0, 0);
+    }
+  }
+}
+template <int IT>
+__device__ __forceinline__ void decode_x(float (&x)[IT][4], const XRaw<IT>& xr, const ObsView& ov,
+                                         const XSigns<IT>& sg, int g) {
+  const int F = ov.F;
+#pragma unroll
+  for (int q = 0; q < IT; ++q) {
+    if (ov.u8) {  // the record row holds the bias input 1 at column F, zeros past it (a padding step
+                  // reads nothing: its bias input is set here)
+      const uint32_t m = sign_bytes(sg.bits4(16 * q + 4 * g));
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[q][r] = (xr.zero && 16 * q + 4 * g + r == F) ? 1.f : rec_byte(xr.w[q][0], r, m);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = 16 * q + 4 * g + r;
+        x[q][r] = col < F ? uf(xr.w[q][r]) : col == F ? 1.f : 0.f;
+      }
+    }
+  }
+}
+// x tile of one window step: lane (g, i) <- x[env i][16q + 4g + r] (q < IT, r < 4), the bias
+// column F = 1, columns past F = 0.  `row0` = row index (slot, e0, agent k) of env e0; consecutive
+// envs are N rows apart; rows of envs >= E read 0 through the range-checked buffer descriptor
+// (zero: the x of a front-padding step, bias column only).
 template <int IT>
 __device__ __forceinline__ void load_x(float (&x)[IT][4], const ObsView& ov, size_t row0, const XSigns<IT>& sg, int g,
                                        int i, bool env_ok, bool zero) {
-  const int64_t rest = (ov.rows - (int64_t)row0) * ov.RB;
-  const uint32_t nbytes = zero || rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
-  const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(ov.base + row0 * ov.RB), 0, nbytes, 0x00020000);
-  const uint32_t vbase = env_ok ? (uint32_t)(i * ov.N * ov.RB) : 0x80000000u;
-  const int F = ov.F;
-  if (ov.u8) {  // wave-uniform; the record row holds the bias input 1 at column F, zeros past it
-    // (a padding step reads nothing: its bias input is set here)
-#pragma unroll
-    for (int q = 0; q < IT; ++q) {
-      const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(rsrc, vbase + (uint32_t)(16 * q + 4 * g), 0, 0);
-      const uint32_t m = sign_bytes(sg.bits4(16 * q + 4 * g));
-#pragma unroll
-      for (int r = 0; r < 4; ++r) x[q][r] = (zero && 16 * q + 4 * g + r == F) ? 1.f : rec_byte(w, r, m);
-    }
-    return;
-  }
-#pragma unroll
-  for (int q = 0; q < IT; ++q)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int col = 16 * q + 4 * g + r;
-      const float v = uf(__builtin_amdgcn_raw_buffer_load_b32(rsrc, vbase + 4u * (uint32_t)col, 0, 0));
-      x[q][r] = col < F ? v : col == F ? 1.f : 0.f;
-    }
+  XRaw<IT> xr;
+  load_x_raw<IT>(xr, ov, row0, g, i, env_ok, zero);
+  decode_x<IT>(x, xr, ov, sg, g);
 }
 
 // One input of the transposed x operand: column col = 16q + i of the row `vb` bytes past rsrc's base

@@ -106,11 +106,18 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
     for (int t = 0; t < HT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[t][r] = 0.f;
+    // the window step's x tile is loaded one step ahead (its latency hides behind a step's MFMAs)
     float x[IT][4];
-    for (int j = 0; j < pad + S; ++j) {
+    XRaw<IT> xn;
+    auto load_step = [&](int j) {
       const bool zero = j < pad;
       const int row_slot = zero ? lo : lo + (j - pad);
-      load_x<IT>(x, a.ov, ((size_t)row_slot * E + e0) * N + k, xsg, g, i, ok, zero);
+      load_x_raw<IT>(xn, a.ov, ((size_t)row_slot * E + e0) * N + k, g, i, ok, zero);
+    };
+    load_step(0);
+    for (int j = 0; j < pad + S; ++j) {
+      decode_x<IT>(x, xn, a.ov, xsg, g);
+      if (j + 1 < pad + S) load_step(j + 1);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
       if constexpr (SPLIT) {
@@ -229,6 +236,17 @@ struct GruHeadAcc {
   static constexpr int W1 = 0, W2 = HT * HT * 4, B1 = W2 + HT * 4, B2 = B1 + HT * 4, NV = B2 + 4;
 };
 
+// base[(v0 + v) * 64 + lane] += d[v] for a block of per-lane sums: every old value is loaded before
+// any is written back (one memory wait for the block)
+template <int NV>
+__device__ __forceinline__ void rmw_block(float* base, int lane, int v0, const float (&d)[NV]) {
+  float old[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) old[v] = base[(v0 + v) * 64 + lane];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) base[(v0 + v) * 64 + lane] = old[v] + d[v];
+}
+
 // Partial layout per (workgroup, agent): the gradient of every torch tensor of the RNN module
 // (StackedNets "rnn": w_ih, w_hh, b_ih, b_hh, layers.0 w/b, layers.2 w/b), then the 2 loss sums.
 struct GruOff {
@@ -316,9 +334,12 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     for (int t = 0; t < HT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[t][r] = 0.f;
+    XRaw<IT> xn;  // the next step's x tile, loaded one step ahead
+    load_x_raw<IT>(xn, a.ov, row_of(0), g, i, ok, 0 < pad);
     for (int j = 0; j < L; ++j) {
       float x[IT][4];
-      load_x<IT>(x, a.ov, row_of(j), xsg, g, i, ok, j < pad);
+      decode_x<IT>(x, xn, a.ov, xsg, g);
+      if (j + 1 < L) load_x_raw<IT>(xn, a.ov, row_of(j + 1), g, i, ok, j + 1 < pad);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
       if constexpr (SPLIT)
@@ -350,11 +371,15 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 
     // ---- head backward.  dW2 += dlg y^T, db2, dy = W2^T dlg, dpre1 = dy [pre1 > 0]; dW1 += dpre1 h_L^T,
     // db1; dh_L = W1^T dpre1.  The head's gradient sums are read-modified-written in the wave's global block.
+    // (the per-tile sums are batched: a block's old values are all loaded before any is written back,
+    // one memory wait per block instead of one per value)
     using HA = GruHeadAcc<HT>;
+    static_assert(HA::B1 == HA::W2 + 4 * HT && HA::B2 == HA::B1 + 4 * HT, "head sums: W2 | b1 | b2 contiguous");
+    float hd[8 * HT + 4];  // this tile's dW2 (4U + r), db1 (4HT + 4t + r), db2 (8HT + r)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       sc[(4 * g + r) * 16 + pcol(i)] = dlg[r];
-      hacc[(HA::B2 + r) * 64 + lane] += dlg[r];
+      hd[8 * HT + r] = dlg[r];
 #pragma unroll
       for (int t = 0; t < HT; ++t) sc[(16 + 16 * t + 4 * g + r) * 16 + pcol(i)] = y[t][r];
     }
@@ -368,7 +393,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) d = mfma4(af[s4], bf[s4], d);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) hacc[(HA::W2 + 4 * U + r) * 64 + lane] += d[r];
+        for (int r = 0; r < 4; ++r) hd[4 * U + r] = d[r];
       }
     }
     float dpre1[HT][4];
@@ -380,9 +405,10 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         dpre1[t][r] = pre1[t][r] > 0.f ? dy[r] : 0.f;
-        hacc[(HA::B1 + 4 * t + r) * 64 + lane] += dpre1[t][r];
+        hd[4 * HT + 4 * t + r] = dpre1[t][r];
       }
     }
+    rmw_block(hacc, lane, HA::W2, hd);
     lds_order();
 #pragma unroll
     for (int t = 0; t < HT; ++t)
@@ -395,6 +421,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
     for (int t = 0; t < HT; ++t) {
       const f32x4 af = sc_frag(sc, 16 * t + i, g);
+      float dw1[4 * HT];
 #pragma unroll
       for (int U = 0; U < HT; ++U) {
         const f32x4 bf = sc_frag(sc, HW + 16 * U + i, g);
@@ -402,8 +429,9 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) d = mfma4(af[s4], bf[s4], d);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) hacc[(HA::W1 + (t * HT + U) * 4 + r) * 64 + lane] += d[r];
+        for (int r = 0; r < 4; ++r) dw1[4 * U + r] = d[r];
       }
+      rmw_block(hacc, lane, HA::W1 + t * HT * 4, dw1);
     }
     float gcur[HT][4];
 #pragma unroll
@@ -419,27 +447,31 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     }
     lds_order();
 
-    // ---- backpropagation through time, j = L-1 .. 0 (gates recomputed from h_{j-1})
-    for (int j = L - 1; j >= 0; --j) {
-      float hp[HT][4];
+    // ---- backpropagation through time, j = L-1 .. 0 (gates recomputed from h_{j-1}); the step's
+    // h_{j-1} and x tile are loaded one step ahead
+    f32x4 hpn[HT];
+    XRaw<IT> xb;
+    auto load_bstep = [&](int j) {
       if (j == 0) {
 #pragma unroll
-        for (int t = 0; t < HT; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) hp[t][r] = 0.f;
+        for (int t = 0; t < HT; ++t) hpn[t] = f32x4{0.f, 0.f, 0.f, 0.f};
       } else {
         const f32x4* src = reinterpret_cast<const f32x4*>(hist + ((size_t)(j - 1) * 64 + lane) * 4 * HT);
 #pragma unroll
-        for (int t = 0; t < HT; ++t) {
-          const f32x4 v = src[t];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) hp[t][r] = v[r];
-        }
+        for (int t = 0; t < HT; ++t) hpn[t] = src[t];
       }
-      const bool zero = j < pad;
-      const size_t xrow = row_of(j);
+      load_x_raw<IT>(xb, a.ov, row_of(j), g, i, ok, j < pad);
+    };
+    load_bstep(L - 1);
+    for (int j = L - 1; j >= 0; --j) {
+      float hp[HT][4];
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hp[t][r] = hpn[t][r];
       float x[IT][4];
-      load_x<IT>(x, a.ov, xrow, xsg, g, i, ok, zero);
+      decode_x<IT>(x, xb, a.ov, xsg, g);
+      if (j > 0) load_bstep(j - 1);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
 #if D2D_GRU_ABLATE == 4
@@ -521,69 +553,94 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       }
     }
 
-    // ---- the tile's weight-gradient GEMMs over the history, K = L steps x 16 samples, one hidden
-    // tile tb (its r, z, n gate tiles) at a time: dW_hh += dgh h_{j-1}^T, dW_ih += dgi x^T
-#pragma unroll 1
-    for (int tb = 0; tb < (D2D_GRU_ABLATE == 1 ? 0 : HT); ++tb) {
-      f32x4 dwh[3][HT], dwi[3][IT];
+    // ---- the tile's weight-gradient GEMMs over the history, K = L steps x 16 samples, TBP hidden
+    // tiles tb (their r, z, n gate tiles) per pass over the history: dW_hh += dgh h_{j-1}^T,
+    // dW_ih += dgi x^T.  A step's fragments are loaded one step ahead (the history is HBM-resident:
+    // 1.3 MB per wave and window), so their latency hides behind the previous step's MFMAs; two
+    // passes instead of one per hidden tile read the h_{j-1} rows twice instead of HT times.  Every
+    // accumulator still sums j = 0 .. L-1, then s4 = 0 .. 3 in order (bitwise the one-tile passes).
+    constexpr int TBP = HT >= 2 ? 2 : 1;
+    struct WFr {
+      f32x4 ai[TBP][3], an[TBP], bh[HT];
+      float xt[IT][4];
+    };
+    auto load_fr = [&](WFr& f, int j, int tb0) {
+      const float* hrow = ghist + (size_t)j * 5 * HW * 16;
 #pragma unroll
-      for (int g3 = 0; g3 < 3; ++g3) {
+      for (int p = 0; p < TBP; ++p) {
 #pragma unroll
-        for (int U = 0; U < HT; ++U) dwh[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int U = 0; U < IT; ++U) dwi[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int g3 = 0; g3 < 3; ++g3) f.ai[p][g3] = sc_frag(hrow, 16 * (g3 * HT + tb0 + p) + i, g);
+        f.an[p] = sc_frag(hrow, R3 + 16 * (tb0 + p) + i, g);
       }
+#pragma unroll
+      for (int U = 0; U < HT; ++U) f.bh[U] = sc_frag(hrow, R3 + HW + 16 * U + i, g);
+      // x^T operand sample-on-k from the rollout buffer (sample 4 s4 + g, input 16U + i)
+      const bool zero = j < pad;
+      const __amdgpu_buffer_rsrc_t rsrc = rows_rsrc(a.ov, row_of(j), zero);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const int ee = 4 * s4 + g;
+        const bool eok = e0 + ee < E;
+        const uint32_t vb = eok ? (uint32_t)(ee * N * a.ov.RB) : 0x80000000u;
+#pragma unroll
+        for (int U = 0; U < IT; ++U) f.xt[U][s4] = load_xt<IT>(rsrc, vb, a.ov, xsg, U, 16 * U + i, zero);
+      }
+    };
+#pragma unroll 1
+    for (int tb0 = 0; tb0 < (D2D_GRU_ABLATE == 1 ? 0 : HT); tb0 += TBP) {
+      f32x4 dwh[TBP][3][HT], dwi[TBP][3][IT];
+#pragma unroll
+      for (int p = 0; p < TBP; ++p)
+#pragma unroll
+        for (int g3 = 0; g3 < 3; ++g3) {
+#pragma unroll
+          for (int U = 0; U < HT; ++U) dwh[p][g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int U = 0; U < IT; ++U) dwi[p][g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      WFr cur, nxt;
+      load_fr(nxt, 0, tb0);
 #pragma unroll 1
       for (int j = 0; j < L; ++j) {
-        const float* hrow = ghist + (size_t)j * 5 * HW * 16;
-        f32x4 ai[3], an;
+        cur = nxt;
+        if (j + 1 < L) load_fr(nxt, j + 1, tb0);
 #pragma unroll
-        for (int g3 = 0; g3 < 3; ++g3) ai[g3] = sc_frag(hrow, 16 * (g3 * HT + tb) + i, g);
-        an = sc_frag(hrow, R3 + 16 * tb + i, g);
+        for (int p = 0; p < TBP; ++p) {
+          if (tb0 + p >= HT) break;  // (odd HT: the last pass has one tile)
 #pragma unroll
-        for (int U = 0; U < HT; ++U) {
-          const f32x4 bh = sc_frag(hrow, R3 + HW + 16 * U + i, g);
+          for (int U = 0; U < HT; ++U)
 #pragma unroll
-          for (int g3 = 0; g3 < 3; ++g3) {
-            const f32x4 af = g3 < 2 ? ai[g3] : an;
+            for (int g3 = 0; g3 < 3; ++g3) {
+              const f32x4 af = g3 < 2 ? cur.ai[p][g3] : cur.an[p];
 #pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) dwh[g3][U] = mfma4(af[s4], bh[s4], dwh[g3][U]);
-          }
+              for (int s4 = 0; s4 < 4; ++s4) dwh[p][g3][U] = mfma4(af[s4], cur.bh[U][s4], dwh[p][g3][U]);
+            }
+#pragma unroll
+          for (int g3 = 0; g3 < 3; ++g3)
+#pragma unroll
+            for (int U = 0; U < IT; ++U)
+#pragma unroll
+              for (int s4 = 0; s4 < 4; ++s4) dwi[p][g3][U] = mfma4(cur.ai[p][g3][s4], cur.xt[U][s4], dwi[p][g3][U]);
         }
-        // x^T operand sample-on-k from the rollout buffer (sample 4 s4 + g, input 16U + i)
-        const bool zero = j < pad;
-        const size_t xrow = row_of(j);
-        float xt[IT][4];
+      }
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          const int ee = 4 * s4 + g;
-          const bool eok = e0 + ee < E;
-          const int64_t rest = (a.ov.rows - (int64_t)xrow) * a.ov.RB;
-          const uint32_t nbytes = zero || rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest;
-          const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-              const_cast<uint8_t*>(a.ov.base + xrow * a.ov.RB), 0, nbytes, 0x00020000);
-          const uint32_t vb = eok ? (uint32_t)(ee * N * a.ov.RB) : 0x80000000u;
+      for (int p = 0; p < TBP; ++p) {
+        if (tb0 + p >= HT) break;
 #pragma unroll
-          for (int U = 0; U < IT; ++U) xt[U][s4] = load_xt<IT>(rsrc, vb, a.ov, xsg, U, 16 * U + i, zero);
-        }
+        for (int g3 = 0; g3 < 3; ++g3) {
+          const int T = g3 * HT + tb0 + p;
+          float dh_[4 * HT], di_[4 * IT];
 #pragma unroll
-        for (int g3 = 0; g3 < 3; ++g3)
+          for (int U = 0; U < HT; ++U)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dh_[4 * U + r] = dwh[p][g3][U][r];
 #pragma unroll
           for (int U = 0; U < IT; ++U)
 #pragma unroll
-            for (int s4 = 0; s4 < 4; ++s4) dwi[g3][U] = mfma4(ai[g3][s4], xt[U][s4], dwi[g3][U]);
-      }
-#pragma unroll
-      for (int g3 = 0; g3 < 3; ++g3) {
-        const int T = g3 * HT + tb;
-#pragma unroll
-        for (int U = 0; U < HT; ++U)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) gpart[((T * HT + U) * 4 + r) * 64 + lane] += dwh[g3][U][r];
-#pragma unroll
-        for (int U = 0; U < IT; ++U)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) gpart[(WA::WI + (T * IT + U) * 4 + r) * 64 + lane] += dwi[g3][U][r];
+            for (int r = 0; r < 4; ++r) di_[4 * U + r] = dwi[p][g3][U][r];
+          rmw_block(gpart, lane, T * HT * 4, dh_);
+          rmw_block(gpart, lane, WA::WI + T * IT * 4, di_);
+        }
       }
     }
   }
