@@ -210,18 +210,6 @@ __device__ __forceinline__ void load_x(float (&x)[IT][4], const ObsView& ov, siz
   decode_x<IT>(x, xr, ov, sg, g);
 }
 
-// One input of the transposed x operand: column col = 16q + i of the row `vb` bytes past rsrc's base
-template <int IT>
-__device__ __forceinline__ float load_xt(const __amdgpu_buffer_rsrc_t& rsrc, uint32_t vb, const ObsView& ov,
-                                         const XSigns<IT>& sg, int q, int col, bool zero) {
-  if (ov.u8) {  // the record's bias byte at column F; a padding step (zero) reads nothing
-    const uint32_t b = __builtin_amdgcn_raw_buffer_load_b8(rsrc, vb + (uint32_t)col, 0, 0);
-    return (zero && col == ov.F) ? 1.f : sg.bit(col) ? (float)(int8_t)b : (float)b;
-  }
-  const float v = uf(__builtin_amdgcn_raw_buffer_load_b32(rsrc, vb + 4u * (uint32_t)col, 0, 0));
-  return col < ov.F ? v : col == ov.F ? 1.f : 0.f;
-}
-
 // Pre-activations of one step: rz[T] (T < 2 HT: input + recurrent + both biases of r / z rows),
 // ni[t] (input part of n incl. b_in), nh[t] (recurrent part of n incl. b_hn).  h_zero: h = 0 (the
 // recurrent products vanish).  W_ih from the swizzled LDS image (WIH_LDS) or from the same image

@@ -562,7 +562,8 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     constexpr int TBP = HT >= 2 ? 2 : 1;
     struct WFr {
       f32x4 ai[TBP][3], an[TBP], bh[HT];
-      float xt[IT][4];
+      uint32_t xr[IT][4];  // raw x^T words (record: one byte each), decoded where they are used
+      bool zero;
     };
     auto load_fr = [&](WFr& f, int j, int tb0) {
       const float* hrow = ghist + (size_t)j * 5 * HW * 16;
@@ -574,16 +575,36 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       }
 #pragma unroll
       for (int U = 0; U < HT; ++U) f.bh[U] = sc_frag(hrow, R3 + HW + 16 * U + i, g);
-      // x^T operand sample-on-k from the rollout buffer (sample 4 s4 + g, input 16U + i)
-      const bool zero = j < pad;
-      const __amdgpu_buffer_rsrc_t rsrc = rows_rsrc(a.ov, row_of(j), zero);
+      // x^T operand sample-on-k from the rollout buffer (sample 4 s4 + g, input 16U + i): raw loads only
+      // (a decode right after its load would make the wave wait for it there)
+      f.zero = j < pad;
+      const __amdgpu_buffer_rsrc_t rsrc = rows_rsrc(a.ov, row_of(j), f.zero);
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         const int ee = 4 * s4 + g;
         const bool eok = e0 + ee < E;
         const uint32_t vb = eok ? (uint32_t)(ee * N * a.ov.RB) : 0x80000000u;
 #pragma unroll
-        for (int U = 0; U < IT; ++U) f.xt[U][s4] = load_xt<IT>(rsrc, vb, a.ov, xsg, U, 16 * U + i, zero);
+        for (int U = 0; U < IT; ++U) {
+          // record: the aligned dword holding byte col (rows are whole dwords); fp32 rows: word col
+          const uint32_t col = 16 * U + i;
+          f.xr[U][s4] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a.ov.u8 ? (vb + col) & ~3u : vb + 4u * col, 0, 0);
+        }
+      }
+    };
+    // this lane's x^T columns 16U + i: record int8 masks (rec_byte) and the fp32-row column class
+    uint32_t xtm[IT];  // (record) the int8 mask of column 16U + i at its byte i & 3 of the loaded dword
+#pragma unroll
+    for (int U = 0; U < IT; ++U) xtm[U] = (xsg.bit(16 * U + i) << 7) << (8 * (i & 3));
+    auto decode_xt = [&](float (&xt)[IT][4], const WFr& f) {
+#pragma unroll
+      for (int U = 0; U < IT; ++U) {
+        const int col = 16 * U + i;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          const float v = a.ov.u8 ? rec_byte(f.xr[U][s4], i & 3, xtm[U]) : (col < F ? uf(f.xr[U][s4]) : 0.f);
+          xt[U][s4] = col == F && (f.zero || !a.ov.u8) ? 1.f : v;  // the bias column
+        }
       }
     };
 #pragma unroll 1
@@ -604,6 +625,8 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       for (int j = 0; j < L; ++j) {
         cur = nxt;
         if (j + 1 < L) load_fr(nxt, j + 1, tb0);
+        float xt[IT][4];
+        decode_xt(xt, cur);
 #pragma unroll
         for (int p = 0; p < TBP; ++p) {
           if (tb0 + p >= HT) break;  // (odd HT: the last pass has one tile)
@@ -620,7 +643,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
             for (int U = 0; U < IT; ++U)
 #pragma unroll
-              for (int s4 = 0; s4 < 4; ++s4) dwi[p][g3][U] = mfma4(cur.ai[p][g3][s4], cur.xt[U][s4], dwi[p][g3][U]);
+              for (int s4 = 0; s4 < 4; ++s4) dwi[p][g3][U] = mfma4(cur.ai[p][g3][s4], xt[U][s4], dwi[p][g3][U]);
         }
       }
 #pragma unroll
