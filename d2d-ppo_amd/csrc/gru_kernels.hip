@@ -28,7 +28,33 @@
 #define D2D_GRU_ABLATE 0
 #endif
 
+#ifndef D2D_GRU_DW_BF16
+// 1: the update kernel's weight-gradient GEMMs dW_hh = sum dgh h^T, dW_ih = sum dgi x^T on
+// v_mfma_f32_16x16x32_bf16 over two-way RNE splits of the history operands (~2^-17 relative per product
+// term, as the MLP update kernels' dW1 / dW2; x is bf16-exact): 60 bf16 MFMAs of 16 cycles per step and
+// pass instead of 144 fp32 MFMAs of 32.  Measured 306 -> 285 ms per 3.3 M agent-samples, but NOT the
+// default: Adam turns the larger error of near-zero gradient elements into weight steps of up to 2 lr,
+// and the D2D categorical GRU reference trace then misses its 1e-4 final-weight bar (1.5e-4 on one of 768
+// elements).  0 (default): v_mfma_f32_16x16x4_f32, exact products (fp32 numerics).
+#define D2D_GRU_DW_BF16 0
+#endif
+
 namespace d2d {
+
+// Two-way RNE bf16 split of 4 fp32 values as one dword per value, (RNE(v), RNE(v - RNE(v))): the A
+// fragment [h0 m0 h1 m1 h2 m2 h3 m3] of k-slots (value q, part p) = 2q + p
+__device__ __forceinline__ u32x4v split_pairs(const f32x4 v) {
+  u32x4v o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+    const bf2 t = {(__bf16)v[q], (__bf16)0.f};  // v_cvt_pk_bf16_f32
+    const float r = v[q] - ffrom(__builtin_bit_cast(uint32_t, t) << 16);
+    const bf2 hm = {(__bf16)v[q], (__bf16)r};
+    o[q] = __builtin_bit_cast(uint32_t, hm);
+  }
+  return o;
+}
 
 struct GruArgs {
   int T, E, N, F, H, A, L, ep_len, kind;
@@ -627,6 +653,50 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
         if (j + 1 < L) load_fr(nxt, j + 1, tb0);
         float xt[IT][4];
         decode_xt(xt, cur);
+#if D2D_GRU_DW_BF16
+        // B operands with the A fragments' k-slots (sample 4 s4 + g, part): h_{j-1} as [h h] and [m 0]
+        // (the two MFMAs give a_h b_h + a_m b_h and a_h b_m), x (bf16-exact) as [x x]
+        bf16x8 bh1[HT], bh2[HT], bx[IT];
+#pragma unroll
+        for (int U = 0; U < HT; ++U) {
+          const u32x4v w = split_pairs(cur.bh[U]);
+          u32x4v d1, d2;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            d1[q] = __builtin_amdgcn_perm(w[q], w[q], 0x01000100u);
+            d2[q] = w[q] >> 16;
+          }
+          bh1[U] = __builtin_bit_cast(bf16x8, d1);
+          bh2[U] = __builtin_bit_cast(bf16x8, d2);
+        }
+#pragma unroll
+        for (int U = 0; U < IT; ++U) {
+          u32x4v d;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) d[q] = __builtin_amdgcn_perm(fbits(xt[U][q]), fbits(xt[U][q]), 0x03020302u);
+          bx[U] = __builtin_bit_cast(bf16x8, d);
+        }
+#pragma unroll
+        for (int p = 0; p < TBP; ++p) {
+          if (tb0 + p >= HT) break;
+          bf16x8 ag[3], an2;
+#pragma unroll
+          for (int g3 = 0; g3 < 3; ++g3) ag[g3] = __builtin_bit_cast(bf16x8, split_pairs(cur.ai[p][g3]));
+          an2 = __builtin_bit_cast(bf16x8, split_pairs(cur.an[p]));
+#pragma unroll
+          for (int U = 0; U < HT; ++U)
+#pragma unroll
+            for (int g3 = 0; g3 < 3; ++g3) {
+              const bf16x8 af = g3 < 2 ? ag[g3] : an2;
+              dwh[p][g3][U] = mfma_bf16(af, bh1[U], dwh[p][g3][U]);
+              dwh[p][g3][U] = mfma_bf16(af, bh2[U], dwh[p][g3][U]);
+            }
+#pragma unroll
+          for (int g3 = 0; g3 < 3; ++g3)
+#pragma unroll
+            for (int U = 0; U < IT; ++U) dwi[p][g3][U] = mfma_bf16(ag[g3], bx[U], dwi[p][g3][U]);
+        }
+#else
 #pragma unroll
         for (int p = 0; p < TBP; ++p) {
           if (tb0 + p >= HT) break;  // (odd HT: the last pass has one tile)
@@ -645,6 +715,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
               for (int s4 = 0; s4 < 4; ++s4) dwi[p][g3][U] = mfma4(cur.ai[p][g3][s4], xt[U][s4], dwi[p][g3][U]);
         }
+#endif
       }
 #pragma unroll
       for (int p = 0; p < TBP; ++p) {
