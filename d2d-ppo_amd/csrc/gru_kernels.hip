@@ -13,8 +13,10 @@
 //    (ippo.py:194-217, d2d_ppo.py:198-216) for GRU policies and the iPPO GRU critic: per 16-sample
 //    tile the padded window's forward (hidden states kept in a per-wave global scratch), the head
 //    and the loss gradient, then backpropagation through time over the window.  Weight gradients:
-//    W_hh in LDS (accumulated by the four waves with ds_add_f32), W_ih / head / biases in
-//    registers; one partial per (workgroup, agent), summed in fixed order by gru_reduce_kernel.
+//    each BPTT step's gradient / h_{j-1} rows go to a per-wave global history, and per tile two
+//    GEMM passes over it (K = window steps x 16 samples) add dW_hh / dW_ih into per-wave sums; the
+//    head's gradients are per-wave sums too; one partial per (workgroup, agent), summed in fixed
+//    order by gru_reduce_kernel (no atomics).
 #include <algorithm>
 #include <cmath>
 
