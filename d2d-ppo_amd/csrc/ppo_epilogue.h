@@ -22,10 +22,12 @@ constexpr float kEps = 1.1920928955078125e-07f;  // torch.finfo(float32).eps (pr
 // SIGMOID (KIND 0 only): the GRU policy's head, p_c = sigmoid(z_c) independently per channel
 // (ippo.py:49-50); dL/dz_c = p_c (1 - p_c) dL/dp_c.
 // Args: any struct with A, inv_A, clip_lo, clip_hi, beta, scale (UpdArgs, GruArgs).
-template <int KIND, bool HALF, bool SIGMOID = false, class Args>
+// AFIX > 0: the action count is known at compile time (the headline A = 8: every lane's four actions
+// are real, so the per-action validity selects fold away).
+template <int KIND, bool HALF, bool SIGMOID = false, int AFIX = 0, class Args>
 __device__ __forceinline__ f32x4 ppo_dz(const Args& a, f32x4 z, uint32_t act, float lo, float W, bool ok, int ga,
                                         float& surr_acc, float& ent_acc) {
-  const int A = a.A;
+  const int A = AFIX > 0 ? AFIX : a.A;
   bool valid[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) valid[r] = 4 * ga + r < A;
@@ -58,15 +60,14 @@ __device__ __forceinline__ f32x4 ppo_dz(const Args& a, f32x4 z, uint32_t act, fl
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float pc = fminf(fmaxf(p[r], kEps), 1.f - kEps);
-      const bool inside = p[r] >= kEps && p[r] <= 1.f - kEps;
+      const bool inside = pc == p[r];  // == (p >= eps && p <= 1 - eps): the clamp passes p through
       const float l1 = __logf(pc), l0 = __logf(1.f - pc);
       const bool bit = (bits >> r) & 1u;
       lsum += valid[r] ? (bit ? l1 : l0) : 0.f;
       esum += valid[r] ? -(p[r] * l1 + (1.f - p[r]) * l0) : 0.f;
       logit[r] = l1 - l0;
-      // d log_prob / dp: 1/pc or -1/(1-pc) -- one reciprocal of the selected denominator
-      const float rden = __builtin_amdgcn_rcpf(bit ? pc : 1.f - pc);
-      dsur[r] = (valid[r] && inside) ? (bit ? rden : -rden) : 0.f;
+      // d log_prob / dp: 1/pc or -1/(1-pc) -- one reciprocal of the selected (signed) denominator
+      dsur[r] = (valid[r] && inside) ? __builtin_amdgcn_rcpf(bit ? pc : -(1.f - pc)) : 0.f;
     }
     logp = group_sum<HALF>(lsum) * a.inv_A;
     ent = group_sum<HALF>(esum) * a.inv_A;
@@ -105,7 +106,7 @@ __device__ __forceinline__ f32x4 ppo_dz(const Args& a, f32x4 z, uint32_t act, fl
     for (int r = 0; r < 4; ++r) {
       q[r] = p[r] * ipsum;
       const float qc = fminf(fmaxf(q[r], kEps), 1.f - kEps);
-      const bool inside = q[r] >= kEps && q[r] <= 1.f - kEps;
+      const bool inside = qc == q[r];  // the clamp passes q through
       const float lq = __logf(qc);
       const bool chosen = valid[r] && 4 * ga + r == aid;
       lsel += chosen ? lq : 0.f;

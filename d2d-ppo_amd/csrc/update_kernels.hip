@@ -282,7 +282,7 @@ __device__ __forceinline__ void lds_row(float (&v)[8], const float (*xw)[XS], in
 // made once; x is bf16-exact on env observations, so 3 MFMAs per 16x16x32); the logits on
 // v_mfma_f32_16x16x4_f32 (an exact fmaf chain) straight from the accumulator registers; the
 // weight gradients dW1, dW2 on two-way RNE splits of their per-tile operands.
-template <int KC, int HT, int KIND, bool PAIR, bool U8>
+template <int KC, int HT, int KIND, bool PAIR, bool U8, int AFIX = 0>
 __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(UpdArgs a) {
   constexpr int QT = 2 * KC;  // input tiles of 16 in dW1
   const int lane = threadIdx.x & 63;
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   int k, by;
   xcd_block(k, by);  // k = agent, by = sample-chunk group
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int H = a.H, A = a.A, F = a.F;
+  const int H = a.H, A = AFIX > 0 ? AFIX : a.A, F = a.F;
   // the transposed-relu(HT) path (D2D_ACTOR_TR): record inputs only (always bf16-exact, so the
   // fractional-input body never runs) and the bf16 logits, whose split parts it transposes
   constexpr bool TR = U8 && D2D_LOGITS_BF16 && D2D_ACTOR_TR;
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
 #if D2D_UPD_ABLATE == 1  // timing ablation: no epilogue (dz = z)
         const f32x4 dzc = zc;
 #else
-        const f32x4 dzc = ppo_dz<KIND, true>(a, zc, cur.act[0], cur.lo[0], cur.w[0], e < a.E, g & 1, surr_acc, ent_acc);
+        const f32x4 dzc = ppo_dz<KIND, true, false, AFIX>(a, zc, cur.act[0], cur.lo[0], cur.w[0], e < a.E, g & 1, surr_acc, ent_acc);
 #endif
         db2 += dzc;
         *reinterpret_cast<f32x4*>(&zb[g >> 1][i][4 * (g & 1)]) = dzc;
@@ -1141,7 +1141,10 @@ template <int KC, int HT, bool U8>
 static void launch_actor_fmt(const UpdArgs& a, hipStream_t s) {
   dim3 grid(a.N, a.G);
   const bool pair = a.A <= 8;
-  if (a.kind == 0 && pair) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, true, U8>), grid, dim3(256), 0, s, a);
+  // the headline action count (8 channels / 8 ids) on the record: A at compile time
+  if (U8 && a.kind == 0 && a.A == 8) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, true, U8, 8>), grid, dim3(256), 0, s, a);
+  else if (U8 && a.kind == 1 && a.A == 8) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, true, U8, 8>), grid, dim3(256), 0, s, a);
+  else if (a.kind == 0 && pair) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, true, U8>), grid, dim3(256), 0, s, a);
   else if (a.kind == 0) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, false, U8>), grid, dim3(256), 0, s, a);
   else if (pair) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, true, U8>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, false, U8>), grid, dim3(256), 0, s, a);

@@ -2,7 +2,8 @@
 ablated kernels compute wrong gradients).  Build on the CPU host first:
     bash tools/gpu/build_ablate.sh
 then on the GPU box:  python3 tools/gpu/ablate_update.py
-Prints ms per actor-gradient launch at 2,048 envs x 200 slots x 64 agents (F 30, H 64, A 8)."""
+Prints ms per actor / critic gradient launch at 2,048 envs x 200 slots x 64 agents (F 30, H 64, A 8), on
+fp32 obs rows and on the compact record (the learners' rollout format)."""
 import json
 import os
 import subprocess
@@ -28,9 +29,19 @@ from d2dhip.update import critic_grads
 vnet = {{"w1": net["w1"].clone(), "b1": net["b1"].clone(), "w2": torch.randn(N, 1, H, device="cuda", generator=g) * 0.1,
         "b2": torch.zeros(N, 1, device="cuda")}}
 R = torch.randn(T, N, E, device="cuda", generator=g).permute(0, 2, 1)
+# the same inputs as the compact record the learners roll out (bias byte 1 at column F, no int8 columns)
+from d2dhip.record import ObsRecord
+from d2dhip import _lib
+RB = _lib.record_bytes(F)
+rdata = torch.zeros((T, E, N, RB), dtype=torch.uint8, device="cuda")
+rdata[..., :F] = obs.to(torch.uint8)
+rdata[..., F] = 1
+rec = ObsRecord(rdata, F, torch.zeros((N, RB // 32), dtype=torch.int32, device="cuda"))
 res = {{}}
 for name, fn in (("actor", lambda: actor_grads(net, obs, acts, lo, W, "comb")),
-                 ("critic", lambda: critic_grads(vnet, obs, R))):
+                 ("critic", lambda: critic_grads(vnet, obs, R)),
+                 ("actor_rec", lambda: actor_grads(net, rec, acts, lo, W, "comb")),
+                 ("critic_rec", lambda: critic_grads(vnet, rec, R))):
     for _ in range(2):
         fn()
     torch.cuda.synchronize()
