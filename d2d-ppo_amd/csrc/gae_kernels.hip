@@ -287,3 +287,46 @@ extern "C" int d2d_normalize_columns_tce(int32_t T, int32_t cols, int32_t E, flo
   }
   return normalize((int64_t)T * cols * E, cols, E, x, mean, scale, gate, stream);
 }
+
+// ---------------------------------------------------------------------------------------------
+// fp32 -> bf16 with an exactness check, one pass (the D2D central critic's bf16 GEMM operand,
+// algorithms/d2d_ppo.py _critic_split_forward): out = the high 16 bits of every x; *inexact = 1 if
+// any x has nonzero low bits (then the caller keeps the fp32 path).  One read of x and one write of
+// out instead of torch's conversion + a chunked compare / all() over a second fp32 copy.  The flag
+// is a plain (benign-race) store of 1 by the lanes that found one: no atomics.
+__global__ __launch_bounds__(256) void bf16_exact_kernel(int64_t n, const float* __restrict__ x,
+                                                         uint16_t* __restrict__ out, int32_t* __restrict__ inexact) {
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  uint32_t low = 0;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
+    const uint4 v = reinterpret_cast<const uint4*>(x)[q];
+    low |= (v.x | v.y | v.z | v.w) & 0xFFFFu;
+    reinterpret_cast<uint2*>(out)[q] = make_uint2((v.x >> 16) | (v.y & 0xFFFF0000u), (v.z >> 16) | (v.w & 0xFFFF0000u));
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {  // tail
+    const uint32_t v = __float_as_uint(x[(n4 << 2) + threadIdx.x]);
+    low |= v & 0xFFFFu;
+    out[(n4 << 2) + threadIdx.x] = (uint16_t)(v >> 16);
+  }
+  if (low) inexact[0] = 1;
+}
+
+extern "C" int d2d_f32_to_bf16_exact(int64_t n, const float* x, uint16_t* out, int32_t* inexact, void* stream) {
+  if (n < 0 || (n > 0 && (!x || !out)) || !inexact) {
+    d2d_set_error("d2d_f32_to_bf16_exact: bad arguments");
+    return D2D_EINVAL;
+  }
+  if ((reinterpret_cast<uintptr_t>(x) & 15) || (reinterpret_cast<uintptr_t>(out) & 7)) {
+    d2d_set_error("d2d_f32_to_bf16_exact: x must be 16-byte and out 8-byte aligned");
+    return D2D_EINVAL;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  D2D_CHECK_HIP(hipMemsetAsync(inexact, 0, sizeof(int32_t), s));
+  if (n == 0) return D2D_OK;
+  int64_t grid = ((n >> 2) + 255) / 256;
+  grid = grid < 1 ? 1 : grid > 16384 ? 16384 : grid;
+  hipLaunchKernelGGL(bf16_exact_kernel, dim3((unsigned)grid), dim3(256), 0, s, n, x, out, inexact);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}

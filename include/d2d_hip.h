@@ -43,8 +43,8 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 6  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
-                              6: d2d_env_desc.poisson_cdf */
+#define D2D_ABI_VERSION 7  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
+                              6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -212,6 +212,12 @@ int d2d_normalize_columns(int64_t rows, int32_t cols, float* x, const double* me
 /* the same on x [T][cols][E] */
 int d2d_normalize_columns_tce(int32_t T, int32_t cols, int32_t E, float* x, const double* mean, const double* scale,
                               const int32_t* gate, void* stream);
+
+/* fp32 -> bf16 (the high 16 bits) of n floats in one pass, *inexact = 1 iff some x is not
+ * bf16-exact (nonzero low 16 bits), else 0.  x 16-byte, out 8-byte aligned.  Replaces the
+ * conversion + exactness check of the D2D central critic's bf16 GEMM operand (the states,
+ * algorithms/d2d_ppo.py:95-98 Value.forward on the whole state batch; ABI v7). */
+int d2d_f32_to_bf16_exact(int64_t n, const float* x, uint16_t* out, int32_t* inexact, void* stream);
 
 /* D2D-PPO's sequential agent update chain (algorithms/d2d_ppo.py:405-433): for the agent
  * permutation perm[0..N), M[perm[j]][b] = adv[b] * prod_{l<j} exp(logp_new[perm[l]][b] -
