@@ -337,16 +337,37 @@ class D2DPPO(BatchedLearnerBase):
             d = v - ro.ret_mean
             value_loss = (d * d).mean()
             dv = d * (2.0 / d.numel())                                                  # [B]
-            g_w2 = torch.mv(hid, dv)                                                    # [H]
             g_b2 = dv.sum().reshape(1)
-            dpre = torch.where(pre > 0, l2.weight.t() * dv[None, :], torch.zeros_like(pre))  # [H][B]
-            dh = dpre.to(torch.bfloat16)
-            dm = (dpre - dh.float()).to(torch.bfloat16)
-            g = torch.mm(torch.cat([dh, dm], 0), ro.state_bf16, out_dtype=torch.float32)  # [2H][S]
-            grads = {l1.weight: g[:H] + g[H:], l1.bias: dpre.sum(1), l2.weight: g_w2, l2.bias: g_b2}
+            # dpre = [pre > 0] w2^T dv as its two-way RNE bf16 split [2H][B], db1 = sum_b dpre and
+            # dW2 = sum_b relu(pre) dv, in one HIP pass over pre (d2d_critic_dpre_split)
+            from d2dhip import _lib
+            lib = _lib.require_gpu()
+            B = pre.shape[1]
+            G = int(lib.d2d_critic_dpre_blocks(B))
+            pre_c, w2v, dv_c = pre.contiguous(), l2.weight.detach().reshape(-1).contiguous(), dv.contiguous()
+            dhm = torch.empty((2 * H, B), dtype=torch.bfloat16, device=pre.device)
+            part = torch.empty((G, 2 * H), dtype=torch.float32, device=pre.device)
+            _lib.check(lib.d2d_critic_dpre_split(H, B, pre_c.data_ptr(), w2v.data_ptr(), dv_c.data_ptr(), dhm.data_ptr(),
+                                                 part.data_ptr(), G, _lib.stream_ptr()), "d2d_critic_dpre_split")
+            sums = part.sum(0)                                                              # [2H]: db1 | dW2
+            g = self._dw1_gemm(dhm, ro.state_bf16)                                          # [2H][S]
+            grads = {l1.weight: g[:H] + g[H:], l1.bias: sums[:H], l2.weight: sums[H:], l2.bias: g_b2}
             for prm, gr in grads.items():
                 prm.grad = gr.reshape(prm.shape).contiguous()
         return value_loss
+
+    @staticmethod
+    def _dw1_gemm(dhm, xb):
+        """[2H][B] x [B][S] -> fp32 [2H][S] with K = B (the whole sample batch): as one GEMM its output is
+        a single row of tiles, so for large B the K range is split into nc chunks of a batched GEMM
+        (hipBLASLt strided batches, [nc][2H][S] partials) summed afterwards."""
+        B = dhm.shape[1]
+        nc = next((c for c in (64, 50, 40, 32, 25, 20, 16, 10, 8, 5, 4, 2) if B % c == 0 and B // c >= 4096), 1)
+        if nc == 1:
+            return torch.mm(dhm, xb, out_dtype=torch.float32)
+        Bc = B // nc
+        a = dhm.view(dhm.shape[0], nc, Bc).permute(1, 0, 2)                          # [nc][2H][Bc], strided
+        return torch.bmm(a, xb.view(nc, Bc, xb.shape[1]), out_dtype=torch.float32).sum(0)
 
     def _chain_dev(self, A, logp_new, logp_old_tne, cycle, T, E):
         """happo_chain on the GPU (d2d_happo_chain): ratios and the sequential fp32 products in one

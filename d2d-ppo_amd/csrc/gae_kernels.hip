@@ -330,3 +330,69 @@ extern "C" int d2d_f32_to_bf16_exact(int64_t n, const float* x, uint16_t* out, i
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// D2D central critic, backward glue (algorithms/d2d_ppo.py _critic_split_backward; the reference's
+// value_loss.backward() through Value = linear2(relu(linear1(state))), d2d_ppo.py:95-98, 208-216):
+//   dpre[h][b] = pre[h][b] > 0 ? w2[h] * dv[b] : 0                 (torch.where(pre > 0, w2^T dv, 0))
+//   dhm[h][b] = RNE_bf16(dpre), dhm[H + h][b] = RNE_bf16(dpre - dhm[h][b])   (the dW1 GEMM's A operand)
+//   partial[g][h] = sum_b dpre (db1),  partial[g][H + h] = sum_b relu(pre) dv (dW2)   over block g's samples
+// One pass over pre instead of ~8 torch elementwise kernels over [H][B].  Block g owns samples
+// [g chunk, (g + 1) chunk); its sums are reduced in a fixed order (wave shuffles, then the 4 waves
+// in order): deterministic, no atomics.
+__global__ __launch_bounds__(256) void critic_dpre_kernel(int H, int64_t B, int64_t chunk, const float* __restrict__ pre,
+                                                          const float* __restrict__ w2, const float* __restrict__ dv,
+                                                          uint16_t* __restrict__ dhm, float* __restrict__ partial) {
+  __shared__ float red[2][4];
+  const int64_t b0 = (int64_t)blockIdx.x * chunk;
+  const int64_t b1 = b0 + chunk < B ? b0 + chunk : B;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int h = 0; h < H; ++h) {
+    const float m = w2[h];
+    float s_db = 0.f, s_gw = 0.f;
+    for (int64_t b = b0 + threadIdx.x; b < b1; b += 256) {
+      const float p = pre[(int64_t)h * B + b], d = dv[b];
+      const float dp = p > 0.f ? m * d : 0.f;
+      const __bf16 hb = (__bf16)dp;  // v_cvt_pk_bf16_f32: round to nearest even, like torch's .to(bfloat16)
+      const __bf16 mb = (__bf16)(dp - (float)hb);
+      dhm[(int64_t)h * B + b] = __builtin_bit_cast(uint16_t, hb);
+      dhm[(int64_t)(H + h) * B + b] = __builtin_bit_cast(uint16_t, mb);
+      s_db += dp;
+      s_gw += fmaxf(p, 0.f) * d;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      s_db += __shfl_xor(s_db, o);
+      s_gw += __shfl_xor(s_gw, o);
+    }
+    if (lane == 0) {
+      red[0][wave] = s_db;
+      red[1][wave] = s_gw;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float* out = partial + (int64_t)blockIdx.x * 2 * H;
+      out[h] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+      out[H + h] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    }
+    __syncthreads();
+  }
+}
+
+extern "C" int32_t d2d_critic_dpre_blocks(int64_t B) {
+  const int64_t g = (B + 2047) / 2048;
+  return (int32_t)(g < 1 ? 1 : g > 1024 ? 1024 : g);
+}
+
+extern "C" int d2d_critic_dpre_split(int32_t H, int64_t B, const float* pre, const float* w2, const float* dv,
+                                     uint16_t* dhm, float* partial, int32_t G, void* stream) {
+  if (H < 1 || B < 0 || G != d2d_critic_dpre_blocks(B) || !pre || !w2 || !dv || !dhm || !partial) {
+    d2d_set_error("d2d_critic_dpre_split: bad arguments (G must be d2d_critic_dpre_blocks(B))");
+    return D2D_EINVAL;
+  }
+  const int64_t chunk = (B + G - 1) / G;
+  hipLaunchKernelGGL(critic_dpre_kernel, dim3((unsigned)G), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), H, B,
+                     chunk, pre, w2, dv, dhm, partial);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}

@@ -44,7 +44,7 @@ extern "C" {
 #endif
 
 #define D2D_ABI_VERSION 7  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
-                              6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact */
+                              6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_critic_dpre_split */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -218,6 +218,16 @@ int d2d_normalize_columns_tce(int32_t T, int32_t cols, int32_t E, float* x, cons
  * conversion + exactness check of the D2D central critic's bf16 GEMM operand (the states,
  * algorithms/d2d_ppo.py:95-98 Value.forward on the whole state batch; ABI v7). */
 int d2d_f32_to_bf16_exact(int64_t n, const float* x, uint16_t* out, int32_t* inexact, void* stream);
+
+/* D2D central critic backward glue (algorithms/d2d_ppo.py:208-216 value_loss.backward() through
+ * Value = linear2(relu(linear1(state)))), pre [H][B] (the first layer's pre-activations), w2 [H]
+ * (linear2.weight), dv [B] (dL/dV): dpre = pre > 0 ? w2[h] dv[b] : 0 written as the two-way RNE bf16
+ * split dhm [2H][B] (rows h: RNE(dpre), rows H + h: RNE(dpre - RNE(dpre))), and per-block sums
+ * partial [G][2H]: [g][h] = sum dpre (db1), [g][H + h] = sum relu(pre) dv (dW2) over block g's samples;
+ * G = d2d_critic_dpre_blocks(B).  Deterministic (fixed-order sums, no atomics).  ABI v7. */
+int32_t d2d_critic_dpre_blocks(int64_t B);
+int d2d_critic_dpre_split(int32_t H, int64_t B, const float* pre, const float* w2, const float* dv, uint16_t* dhm,
+                          float* partial, int32_t G, void* stream);
 
 /* D2D-PPO's sequential agent update chain (algorithms/d2d_ppo.py:405-433): for the agent
  * permutation perm[0..N), M[perm[j]][b] = adv[b] * prod_{l<j} exp(logp_new[perm[l]][b] -
