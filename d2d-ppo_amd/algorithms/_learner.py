@@ -43,6 +43,13 @@ class Rollout:
         self.__dict__.update(kw)
 
     def __getattr__(self, name):
+        if name == "state_seq" and "state_dim" in self.__dict__:
+            # env-major fp32 states [E*T][S] (d2d_ppo.py's rollout states), copied from the slot-major
+            # buffer only when a consumer asks (the bf16 central critic reads the buffer directly)
+            st = self.__dict__["states"]
+            v = st[:, :, : self.__dict__["state_dim"]].transpose(0, 1).reshape(st.shape[0] * st.shape[1], -1)
+            self.__dict__[name] = v
+            return v
         if name == "obs_f32":
             o = self.__dict__["obs"]
             v = o.decode() if isinstance(o, ObsRecord) else o

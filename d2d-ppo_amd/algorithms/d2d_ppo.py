@@ -149,7 +149,7 @@ class D2DPPO(BatchedLearnerBase):
         # load_state_dict on an agent's module, a broadcast) before taking the ratio = 1 shortcut
         ro.policy_snapshot = [p.detach().clone() for p in self.policy.parameters()]
         S = self.env.state_space.shape[0]
-        ro.state_seq = ro.states[:, :, :S].transpose(0, 1).reshape(ro.E * ro.T, S)     # [E*T][S]
+        ro.state_dim = S  # ro.state_seq: the env-major [E*T][S] fp32 states, materialised on first use
         # returns = discount_rewards(rewards (T,N)).mean(1) (d2d_ppo.py:333,339): every agent has the
         # same reward, so all N normalised columns are identical and their mean is that column
         zero_v = torch.zeros((ro.T, ro.E, 1), dtype=torch.float32, device=self.device)
@@ -287,7 +287,7 @@ class D2DPPO(BatchedLearnerBase):
         channel bits, ACKs) and so exact in bf16, and W1 is split three ways (h + m + l, exact), so
         the product is fp32-accurate at the bf16 matrix rate.  Returns (values [B], pre-activation [H][B],
         hidden [H][B]) or None when the fp32 torch path applies (small states or non-integer states)."""
-        S = ro.state_seq.shape[1]
+        S = ro.state_dim if "state_dim" in ro.__dict__ else ro.state_seq.shape[1]
         if not self.critic_split or S < self.CRITIC_SPLIT_MIN_DIM:
             return None
         xb = getattr(ro, "state_bf16", None)
@@ -299,12 +299,21 @@ class D2DPPO(BatchedLearnerBase):
             # one HIP pass converts and checks (d2d_f32_to_bf16_exact; was torch's conversion plus a
             # chunked compare / all() over a second fp32 copy: ~200 small launches per rollout at 256 agents)
             from d2dhip import _lib
-            st = ro.state_seq.contiguous()
-            xb = torch.empty(st.shape, dtype=torch.bfloat16, device=st.device)
-            flag = torch.empty(1, dtype=torch.int32, device=st.device)
-            _lib.check(_lib.require_gpu().d2d_f32_to_bf16_exact(st.numel(), st.data_ptr(), xb.data_ptr(),
-                                                                 flag.data_ptr(), _lib.stream_ptr()),
-                       "d2d_f32_to_bf16_exact")
+            lib = _lib.require_gpu()
+            st = ro.__dict__.get("states")
+            if "state_seq" not in ro.__dict__ and st is not None and st.is_contiguous() and st.dim() == 3:
+                # straight from the slot-major rollout buffer [T][E][stride] (no env-major fp32 copy)
+                T_, E_ = st.shape[0], st.shape[1]
+                xb = torch.empty((E_ * T_, S), dtype=torch.bfloat16, device=st.device)
+                flag = torch.empty(1, dtype=torch.int32, device=st.device)
+                _lib.check(lib.d2d_states_to_bf16_exact(T_, E_, S, st.shape[2], st.data_ptr(), xb.data_ptr(),
+                                                        flag.data_ptr(), _lib.stream_ptr()), "d2d_states_to_bf16_exact")
+            else:
+                sq = ro.state_seq.contiguous()
+                xb = torch.empty(sq.shape, dtype=torch.bfloat16, device=sq.device)
+                flag = torch.empty(1, dtype=torch.int32, device=sq.device)
+                _lib.check(lib.d2d_f32_to_bf16_exact(sq.numel(), sq.data_ptr(), xb.data_ptr(), flag.data_ptr(),
+                                                     _lib.stream_ptr()), "d2d_f32_to_bf16_exact")
             if int(flag.item()) != 0:
                 self.critic_split = False  # fractional / large states: keep torch fp32
                 return None

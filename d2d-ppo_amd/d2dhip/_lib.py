@@ -112,6 +112,8 @@ _SIGS = {
     "d2d_set_option": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),
     "d2d_happo_chain": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p, _p, _p, _p]),
     "d2d_f32_to_bf16_exact": (ctypes.c_int, [ctypes.c_int64, _p, _p, _p, _p]),
+    "d2d_states_to_bf16_exact": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, _p, _p,
+                                                _p, _p]),
     "d2d_critic_dpre_blocks": (ctypes.c_int32, [ctypes.c_int64]),
     "d2d_critic_dpre_split": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, _p, _p, _p, _p, _p, ctypes.c_int32, _p]),
     "d2d_policy_mlp_step": (ctypes.c_int, [ctypes.POINTER(MlpDesc), _p, _p, ctypes.c_uint32, ctypes.c_int32, _p, _p,

@@ -44,7 +44,8 @@ extern "C" {
 #endif
 
 #define D2D_ABI_VERSION 7  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
-                              6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_critic_dpre_split */
+                              6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_states_to_bf16_exact,
+                              d2d_critic_dpre_split */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -218,6 +219,10 @@ int d2d_normalize_columns_tce(int32_t T, int32_t cols, int32_t E, float* x, cons
  * conversion + exactness check of the D2D central critic's bf16 GEMM operand (the states,
  * algorithms/d2d_ppo.py:95-98 Value.forward on the whole state batch; ABI v7). */
 int d2d_f32_to_bf16_exact(int64_t n, const float* x, uint16_t* out, int32_t* inexact, void* stream);
+/* The same from the rollout's slot-major state buffer x [T][E][ld] (its first S floats per row) into
+ * the env-major bf16 operand out [E*T][S] (row e*T + t), no fp32 env-major copy first (ABI v7). */
+int d2d_states_to_bf16_exact(int32_t T, int32_t E, int32_t S, int64_t ld, const float* x, uint16_t* out,
+                             int32_t* inexact, void* stream);
 
 /* D2D central critic backward glue (algorithms/d2d_ppo.py:208-216 value_loss.backward() through
  * Value = linear2(relu(linear1(state)))), pre [H][B] (the first layer's pre-activations), w2 [H]

@@ -56,3 +56,24 @@ def test_rejects_misaligned_input():
     rc = _lib.require_gpu().d2d_f32_to_bf16_exact(64, x.data_ptr() + 4, out.data_ptr(), flag.data_ptr(),
                                                    _lib.stream_ptr())
     assert rc != 0
+
+
+@pytest.mark.parametrize("T,E,S,ld", [(200, 64, 3848, 3848), (7, 5, 23, 24), (3, 2, 3848, 3852), (200, 33, 21, 21)])
+def test_states_from_the_slot_major_buffer(T, E, S, ld):
+    """d2d_states_to_bf16_exact: the env-major operand [E*T][S] straight from the rollout buffer [T][E][ld]."""
+    g = torch.Generator(device="cuda").manual_seed(T + E + S)
+    x = torch.randint(-1, 20, (T, E, ld), device="cuda", generator=g).float()
+    ref = x[:, :, :S].transpose(0, 1).reshape(E * T, S)
+    out = torch.empty((E * T, S), dtype=torch.bfloat16, device="cuda")
+    flag = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+    lib = _lib.require_gpu()
+    _lib.check(lib.d2d_states_to_bf16_exact(T, E, S, ld, x.data_ptr(), out.data_ptr(), flag.data_ptr(),
+                                            _lib.stream_ptr()), "d2d_states_to_bf16_exact")
+    torch.cuda.synchronize()
+    assert int(flag.item()) == 0 and torch.equal(out, ref.to(torch.bfloat16))
+    x[T - 1, E - 1, S - 1] = 0.3  # one inexact state value (padding columns past S are not read)
+    x[0, 0, ld - 1] = 0.3 if ld > S else x[0, 0, ld - 1]
+    _lib.check(lib.d2d_states_to_bf16_exact(T, E, S, ld, x.data_ptr(), out.data_ptr(), flag.data_ptr(),
+                                            _lib.stream_ptr()), "d2d_states_to_bf16_exact")
+    torch.cuda.synchronize()
+    assert int(flag.item()) == 1
