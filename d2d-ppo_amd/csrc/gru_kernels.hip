@@ -334,7 +334,9 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   const SwzOff<HW> oh(g, i);
   const XSigns<IT> xsg(a.ov, k);
   const size_t wave_id = (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave;
-  float* hist = a.hist + wave_id * (size_t)L * 64 * 4 * HT;
+  // per wave: [0, L) the tile's h_j, [L, 2L) the front-padding table: h after j + 1 all-padding steps
+  float* hist = a.hist + wave_id * (size_t)2 * L * 64 * 4 * HT;
+  float* ptab = hist + (size_t)L * 64 * 4 * HT;
   float* hacc = a.hacc + wave_id * (size_t)GruHeadAcc<HT>::NV * 64;
   for (int v = 0; v < GruHeadAcc<HT>::NV; ++v) hacc[v * 64 + lane] = 0.f;
   using WA = GruWAcc<HT, IT>;
@@ -342,6 +344,41 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   float* gpart = a.gpart + wave_id * (size_t)WA::NV * 64;
   for (int v = 0; v < WA::NV; ++v) gpart[v * 64 + lane] = 0.f;
   __syncthreads();
+
+  // The front-padding steps of a training window (x = the bias input only, h0 = 0) give the same h_j
+  // for every sample: the wave runs them once here -- the very instructions and data of any tile's
+  // padding steps, so bitwise the same h -- and its tiles start their forward at step pad.
+  for (int j = 0; j + 1 < L; ++j) {
+    float h[HT][4];
+    if (j == 0) {
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[t][r] = 0.f;
+    } else {
+      const f32x4* src = reinterpret_cast<const f32x4*>(ptab + ((size_t)(j - 1) * 64 + lane) * 4 * HT);
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        const f32x4 v = src[t];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[t][r] = v[r];
+      }
+    }
+    XRaw<IT> xr;
+    load_x_raw<IT>(xr, a.ov, 0, g, i, false, true);  // a padding step: nothing is read
+    float x[IT][4];
+    decode_x<IT>(x, xr, a.ov, xsg, g);
+    f32x4 rz[2 * HT], ni[HT], nh[HT];
+    const int z = opaque_zero();
+    if constexpr (SPLIT)
+      gru_preact_split<HT, IT>(wih_g + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), h, bhn, rz, ni, nh, j == 0);
+    else
+      gru_preact<HT, IT, false>(wimg + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
+    gru_gates<HT>(rz, ni, nh, h);
+    f32x4* dst = reinterpret_cast<f32x4*>(ptab + ((size_t)j * 64 + lane) * 4 * HT);
+#pragma unroll
+    for (int t = 0; t < HT; ++t) dst[t] = f32x4{h[t][0], h[t][1], h[t][2], h[t][3]};
+  }
 
   const int n_tiles = a.T * a.env_tiles;
   for (int tile = blockIdx.y * 4 + wave; tile < n_tiles; tile += gridDim.y * 4) {  // wave-uniform
@@ -357,14 +394,25 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     auto row_of = [&](int j) { return ((size_t)(j < pad ? lo : lo + j - pad) * E + e0) * N + k; };
 
     // ---- forward over the window; h_j (j < L - 1) to the wave's scratch
+    // (steps j < pad: the padding table)
     float h[HT][4];
+    if (pad == 0) {
 #pragma unroll
-    for (int t = 0; t < HT; ++t)
+      for (int t = 0; t < HT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h[t][r] = 0.f;
+        for (int r = 0; r < 4; ++r) h[t][r] = 0.f;
+    } else {
+      const f32x4* src = reinterpret_cast<const f32x4*>(ptab + ((size_t)(pad - 1) * 64 + lane) * 4 * HT);
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        const f32x4 v = src[t];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[t][r] = v[r];
+      }
+    }
     XRaw<IT> xn;  // the next step's x tile, loaded one step ahead
-    load_x_raw<IT>(xn, a.ov, row_of(0), g, i, ok, 0 < pad);
-    for (int j = 0; j < L; ++j) {
+    load_x_raw<IT>(xn, a.ov, row_of(pad), g, i, ok, false);
+    for (int j = pad; j < L; ++j) {
       float x[IT][4];
       decode_x<IT>(x, xn, a.ov, xsg, g);
       if (j + 1 < L) load_x_raw<IT>(xn, a.ov, row_of(j + 1), g, i, ok, j + 1 < pad);
@@ -484,7 +532,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
         for (int t = 0; t < HT; ++t) hpn[t] = f32x4{0.f, 0.f, 0.f, 0.f};
       } else {
-        const f32x4* src = reinterpret_cast<const f32x4*>(hist + ((size_t)(j - 1) * 64 + lane) * 4 * HT);
+        const f32x4* src = reinterpret_cast<const f32x4*>((j - 1 < pad ? ptab : hist) + ((size_t)(j - 1) * 64 + lane) * 4 * HT);
 #pragma unroll
         for (int t = 0; t < HT; ++t) hpn[t] = src[t];
       }
@@ -1021,7 +1069,7 @@ static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, 
   GruWs w;
   w.partial = 0;
   w.hist = up(G * N * P);
-  w.wimg = w.hist + up(waves * L * 64 * 4 * htp);
+  w.wimg = w.hist + up(waves * 2 * L * 64 * 4 * htp);  // per wave: the tile's h history + the padding table
   // fp32 input images [N][3 HW][32] or the split ones [N][3 htp][1][3 parts][64] 16-byte words
   w.hacc = w.wimg + up(N * std::max<int64_t>(3 * HW * 32, 3 * htp * 3 * 64 * 4));
   w.himg = w.hacc + up(waves * 64 * (htp * htp * 4 + htp * 8 + 4));
