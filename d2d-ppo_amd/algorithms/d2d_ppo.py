@@ -336,10 +336,11 @@ class D2DPPO(BatchedLearnerBase):
         return v, pre, hid
 
     def _critic_split_backward(self, ro, crit):
-        """Gradients of mse(V, returns) into the critic's .grad (what value_loss.backward() leaves):
-        dW1 = dPreᵀ X on a two-way RNE bf16 split of dPre (≤ 2^-17 relative per product term, as in
-        the fused update kernels) against the exact bf16 states."""
-        v, pre, hid = crit
+        """Gradients of mse(V, returns) into the critic's .grad (what value_loss.backward() leaves,
+        d2d_ppo.py:208-216): dW1 = dPreᵀ X on a two-way RNE bf16 split of dPre (≤ 2^-17 relative per
+        product term, as in the fused update kernels) against the exact bf16 states; dPre's split and the
+        db1 / dW2 sums come from one HIP pass (d2d_critic_dpre_split), dW1 from a split-K batched GEMM."""
+        v, pre, _ = crit
         l1, l2 = self.value_network.linear1, self.value_network.linear2
         H = l1.weight.shape[0]
         with torch.no_grad():
