@@ -84,6 +84,7 @@ struct GruArgs {
 };
 
 enum { kGruBernoulli = 0, kGruCategorical = 1, kGruValue = 2 };
+constexpr int kGruPadTab = 63;  // padding-table steps of the policy kernel (history_len <= 64)
 
 // ------------------------------------------------------------------------------ policy kernel
 // Workgroup = agent k x a strided set of tiles; 8 waves (2 per SIMD), one 16-env tile per wave at a
@@ -115,6 +116,37 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
   const SwzOff<IW> oi(g, i);
   const SwzOff<HW> oh(g, i);
   const XSigns<IT> xsg(a.ov, k);
+  // Padded (training) windows: the front-padding steps (x = the bias input only, h0 = 0) give the same
+  // h_j for every sample, so wave 0 runs them once into an LDS table -- the very instructions and data
+  // of any tile's padding steps, so bitwise the same h -- and tiles start their window at step pad.
+  __shared__ float ptab_s[kGruPadTab * HW];  // [step j][unit]: h after j + 1 padding steps
+  const bool use_tab = a.padded && a.L - 1 <= kGruPadTab;
+  if (use_tab && wave == 0) {
+    float h[HT][4];
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[t][r] = 0.f;
+    for (int j = 0; j + 1 < a.L; ++j) {
+      XRaw<IT> xr;
+      load_x_raw<IT>(xr, a.ov, 0, g, i, false, true);  // a padding step: nothing is read
+      float x[IT][4];
+      decode_x<IT>(x, xr, a.ov, xsg, g);
+      f32x4 rz[2 * HT], ni[HT], nh[HT];
+      const int z = opaque_zero();
+      if constexpr (SPLIT)
+        gru_preact_split<HT, IT>(wih_b + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), h, bhn, rz, ni, nh, j == 0);
+      else
+        gru_preact<HT, IT, true>(wih_s + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
+      gru_gates<HT>(rz, ni, nh, h);
+      if (i == 0) {  // every sample lane holds the same h: lanes (g, 0) write units 16t + 4g + r
+#pragma unroll
+        for (int t = 0; t < HT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ptab_s[j * HW + 16 * t + 4 * g + r] = h[t][r];
+      }
+    }
+  }
   __syncthreads();
 
   const int n_tiles = a.n_slots * a.env_tiles;
@@ -129,11 +161,12 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
     const int S = min(pos + 1, a.L);
     const int lo = slot - S + 1;
     const int pad = a.padded ? a.L - S : 0;
+    const int j0 = use_tab ? pad : 0;  // the first step computed here (steps j < j0: the padding table)
     float h[HT][4];
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h[t][r] = 0.f;
+      for (int r = 0; r < 4; ++r) h[t][r] = j0 > 0 ? ptab_s[(j0 - 1) * HW + 16 * t + 4 * g + r] : 0.f;
     // the window step's x tile is loaded one step ahead (its latency hides behind a step's MFMAs)
     float x[IT][4];
     XRaw<IT> xn;
@@ -142,8 +175,8 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
       const int row_slot = zero ? lo : lo + (j - pad);
       load_x_raw<IT>(xn, a.ov, ((size_t)row_slot * E + e0) * N + k, g, i, ok, zero);
     };
-    load_step(0);
-    for (int j = 0; j < pad + S; ++j) {
+    load_step(j0);
+    for (int j = j0; j < pad + S; ++j) {
       decode_x<IT>(x, xn, a.ov, xsg, g);
       if (j + 1 < pad + S) load_step(j + 1);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
