@@ -90,7 +90,8 @@ constexpr int kGruPadTab = 63;  // padding-table steps of the policy kernel (his
 // Workgroup = agent k x a strided set of tiles; 8 waves (2 per SIMD), one 16-env tile per wave at a
 // time.  LDS: the agent's input and recurrent images (fp32, swizzled; 72 KB at H = 64, F < 32).
 // SPLIT: the step on v_mfma_f32_16x16x32_bf16 over exact three-way splits (gru_preact_split; LDS:
-// the split images, 108 KB at H = 64, F < 32), else on v_mfma_f32_16x16x4_f32 (gru_preact).
+// the split images, 108 KB at H = 64, F < 32), else on v_mfma_f32_16x16x4_f32 (gru_preact).  Plus the
+// head image and the 16 KB padding table of padded windows: 147.5 KB at H = 64.
 template <int HT, int IT, int KIND, int MODE, bool SPLIT>
 __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
   constexpr int HW = 16 * HT, IW = 16 * IT, R3 = 3 * HW;
@@ -319,8 +320,8 @@ struct GruOff {
 };
 
 // Workgroup = agent k x a strided set of 16-sample tiles; 4 waves (one per SIMD).
-// LDS (H = 64): W_hh image 48 KB (forward A fragments) + its transpose 49 KB (the A fragments of
-// dh = W_hh^T dg, one ds_read_b128 per 4 MFMAs) + 4 x 12 KB wave scratch = 145 KB.
+// LDS (H = 64, !SPLIT): W_hh image 48 KB (forward A fragments) + its transpose 49 KB (the A fragments
+// of dh = W_hh^T dg, one ds_read_b128 per 4 MFMAs) + 4 x 12 KB wave scratch = 145 KB (SPLIT: below).
 // The weight gradients dW_hh = sum_j dgh_j h_{j-1}^T and dW_ih = sum_j dgi_j x_j^T are not summed
 // step by step (that took one LDS atomic per element per step, ~40 % of the LDS issue): every step
 // writes its dgi / dgh_n / h_{j-1} rows (sample-on-k layout, through the wave's LDS scratch) to a
