@@ -31,11 +31,20 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(int T, int E, int cols, i
   const int e = tce ? (int)(i % E) : (int)(i / cols);
   const bool global_last = last_shard && (e == E - 1);
   double gae = 0.0, R = 0.0, v_next = 0.0;
+  // step t's inputs are loaded one step ahead (t + 1's recursion hides their latency)
+  auto r_at = [&](int t) { return rew[rcols == 1 ? (int64_t)t * E + e : (int64_t)t * width + i]; };
+  float rn = T > 0 ? r_at(T - 1) : 0.f, vn = T > 0 ? val[(int64_t)(T - 1) * width + i] : 0.f;
+  uint8_t dn = T > 0 ? done[T - 1] : 0;
   for (int t = T - 1; t >= 0; --t) {
     const int64_t o = (int64_t)t * width + i;
-    const double r = (double)rew[rcols == 1 ? (int64_t)t * E + e : o];
-    const double v = (double)val[o];
-    const double nd = done[t] ? 0.0 : 1.0;
+    const double r = (double)rn;
+    const double v = (double)vn;
+    const double nd = dn ? 0.0 : 1.0;
+    if (t > 0) {
+      rn = r_at(t - 1);
+      vn = val[o - width];
+      dn = done[t - 1];
+    }
     // discount_rewards: R = r + R * gamma * (1 - done)   (ippo.py:107-109)
     R = r + R * gamma * nd;
     double a;
