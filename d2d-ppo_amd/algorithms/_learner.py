@@ -294,23 +294,33 @@ class BatchedLearnerBase(DataParallelMixin):
         env = self.env
         E, L = b.E, env.episode_length
         waves = max(1, math.ceil(num_episodes / E))
-        if teacher is None and self._graph_ok(train, b, waves * L):
-            return self._collect_graph(b, waves, want_values, want_state)
-        bufs = self._rollout_buffers(b, waves, want_values, want_state)
-        tf = self._teacher_tensors(teacher, b, waves) if teacher is not None else None
-        self._waves(bufs, b, waves, train, tf)
-        return self._rollout_result(bufs, b, waves, train)
+        if teacher is None and self._graph_ok(train, b, waves * L, want_values, want_state):
+            ro = self._collect_graph(b, waves, want_values, want_state)
+        else:
+            bufs = self._rollout_buffers(b, waves, want_values, want_state)
+            tf = self._teacher_tensors(teacher, b, waves) if teacher is not None else None
+            self._waves(bufs, b, waves, train, tf)
+            ro = self._rollout_result(bufs, b, waves, train)
+        self._sync_episode_rng(b)
+        return ro
 
     # ---------------------------------------------- episode-parallel rollouts (n_envs == 1)
     episode_parallel = os.environ.get("D2D_EPISODE_PARALLEL", "1") != "0"
+
+    EPISODE_ENV_BASE = 1 << 31  # Philox env indices of the episode batches (the counter word is 32 bits)
 
     def _episode_batch(self, n):
         """The reference drivers build their envs with the default n_envs = 1 and roll out
         num_episodes episodes one after another (create_rollouts ippo.py:283, test ippo.py:353).  The
         episodes are independent, so here they run side by side: a private device batch of n envs with
-        the env's parameters and its own Philox counter range (env indices from 2^40, disjoint from the
-        env's own batch) replaces the n sequential waves.  Single process only (data-parallel ranks
-        shard their envs explicitly); D2D_EPISODE_PARALLEL=0 keeps the sequential waves."""
+        the env's parameters replaces the n sequential waves.  Single process only (data-parallel ranks
+        shard their envs explicitly); D2D_EPISODE_PARALLEL=0 keeps the sequential waves.
+
+        Fresh draws for every episode, as the reference's one global RNG stream gives: the batches'
+        Philox env indices start at 2^31 (disjoint from the env's own batch, whose indices start at its
+        env_base < 2^31), and every episode batch — the training and the test sizes, and a batch
+        rebuilt after eviction — continues ONE learner-level rng_step counter (`_sync_episode_rng`), so
+        no two rollouts of the learner draw the same (env index, rng_step) Philox counters."""
         main = self.env.batch()
         if not self.episode_parallel or getattr(self, "world_size", 1) > 1:
             return main
@@ -319,10 +329,25 @@ class BatchedLearnerBase(DataParallelMixin):
         if b is None:
             from d2dhip.envbatch import EnvBatch
             if len(cache) >= 2:  # the training and the test batch sizes of a driver
-                cache.pop(next(iter(cache)))
-            b = EnvBatch(main.spec, n, main.device, seed=main.desc.seed, env_base=(1 << 40) + main.desc.env_base)
+                old = cache.pop(next(iter(cache)))
+                self._drop_graphs_of(old)
+            if main.desc.env_base + main.E > self.EPISODE_ENV_BASE:
+                raise ValueError("the env's own Philox env range overlaps the episode batches' (2^31)")
+            b = EnvBatch(main.spec, n, main.device, seed=main.desc.seed, env_base=self.EPISODE_ENV_BASE)
             cache[n] = b
+        b.rng_step = self.__dict__.get("_episode_rng_step", 0)
         return b
+
+    def _sync_episode_rng(self, b):
+        """After a rollout on an episode batch: the learner-level counter moves past its draws."""
+        if b in self.__dict__.get("_episode_batches", {}).values():
+            self._episode_rng_step = b.rng_step
+
+    def _drop_graphs_of(self, b):
+        """Captured rollout graphs bake in a batch's buffers: drop those of an evicted batch."""
+        graphs = self.__dict__.get("_rollout_graphs", {})
+        for k in [k for k, G in graphs.items() if G["batch"] is b]:
+            del graphs[k]
 
     # ------------------------------------------------- rollout body (eager or captured)
     def _rollout_buffers(self, b, waves, want_values, want_state):
@@ -391,20 +416,26 @@ class BatchedLearnerBase(DataParallelMixin):
 
     # ------------------------------------------------------- HIP-graph rollout
     graph_rollout = os.environ.get("D2D_GRAPH_ROLLOUT", "1") != "0"
-    GRAPH_ROLLOUT_MAX_BYTES = 32 << 30
+    GRAPH_ROLLOUT_MAX_BYTES = 40 << 30
 
-    def _graph_ok(self, train, b, T):
+    def _graph_ok(self, train, b, T, want_values=False, want_state=False):
         """Training rollouts of the fused MLP policy replay one captured HIP graph (reset + L x
         (policy kernel, env kernel) per wave + the statistics): at small batches the slot loop is
-        bound by per-launch host work, not the GPU.  The graph keeps its rollout buffers (reused by every
-        replay); rollouts whose obs buffer exceeds 32 GiB (of the 288 GB HBM) stay eager.  The compact
-        record puts the headline rollout (65,536 envs x 200 slots x 64 agents x 32 B = 27 GB) inside."""
+        bound by per-launch host work, not the GPU.  The graph keeps its rollout buffers alive for the
+        learner's lifetime (reused by every replay), so all of them — obs (record or fp32 rows), actions,
+        log-probs, values, rewards and D2D-PPO's [T][E][state_stride] fp32 states — count against a
+        40 GiB budget (of the 288 GB HBM); larger rollouts stay eager.  The compact record puts the
+        headline iPPO rollout inside: 65,536 envs x 200 slots x 64 agents x (32 B record + 1 B actions
+        + 4 B log-prob + 4 B value) = 34.4 GB."""
         if not (self.graph_rollout and train and (self._gru_ok() or (not self.useRNN and self._fused_ok()))
                 and (self.kind == "comb") == bool(self.combinatorial)):
             return False
         s = b.spec
         row = _lib_record_bytes(s.F) if self._record_ok() else 4 * s.F
-        return T * b.E * s.N * row <= self.GRAPH_ROLLOUT_MAX_BYTES
+        act = b.action_buffer().element_size()
+        per_slot_agent = row + act + 4 + (4 if want_values else 0)
+        per_slot_env = s.N * per_slot_agent + 4 + (4 * s.state_stride if want_state else 0)
+        return T * b.E * per_slot_env <= self.GRAPH_ROLLOUT_MAX_BYTES
 
     def _collect_graph(self, b, waves, want_values, want_state):
         """Capture once per rollout shape, replay afterwards.  The kernels add the device word
@@ -413,12 +444,16 @@ class BatchedLearnerBase(DataParallelMixin):
         training rollout of the same shape."""
         env = self.env
         L = env.episode_length
-        # the graph bakes in the env batch's state buffers and the stacked parameters' addresses
+        # the graph bakes in the env batch's state buffers and the stacked parameters' addresses; the
+        # entry holds the batch itself (so its buffers outlive the graph) and must be THIS batch — a
+        # new batch could reuse a freed one's id()
         key = (id(b), b.E, L, waves, bool(want_values), bool(want_state),
                tuple(t.data_ptr() for t in self.policy.params.values()),
                tuple(t.data_ptr() for t in getattr(self.value, "params", {}).values()) if hasattr(self, "value") else ())
         cache = self.__dict__.setdefault("_rollout_graphs", {})
         G = cache.get(key)
+        if G is not None and G["batch"] is not b:
+            G = None
         if G is None:
             cache.clear()  # one live graph (and its buffers) per learner
             bufs = self._rollout_buffers(b, waves, want_values, want_state)
@@ -441,7 +476,7 @@ class BatchedLearnerBase(DataParallelMixin):
                 self.graph_rollout = False
                 print(f"[d2d] rollout graph capture failed ({err}); eager rollouts from now on")
                 return result
-            G = dict(graph=g, bufs=bufs, base=base, delta=b.rng_step - base)
+            G = dict(graph=g, bufs=bufs, base=base, delta=b.rng_step - base, batch=b)
             b.rng_step = base  # capturing ran nothing
             cache[key] = G
             return result

@@ -63,6 +63,234 @@ __global__ __launch_bounds__(256) void gae_scan_kernel(int T, int E, int cols, i
   }
 }
 
+// ---------------------------------------------------------------- scan + normalisation moments
+// The scan of gae_scan_kernel with the column statistics of both outputs fused into it: every
+// thread owns one (env, column) sequence of T elements, so while it writes adv / ret it also
+// accumulates their (shifted) sums in double; the block combines its threads' moments per column
+// with Chan's pairwise formula in a fixed tree order and writes one partial per (column, block);
+// gae_moments_reduce_kernel combines the partials of a column in a fixed order.  Result per column:
+// n, sum and M2 = sum of squared deviations from the column mean -- what two_pass_column_stats
+// (d2dhip/gae.py) needs, without a second or third pass over adv / ret.
+//
+// Block = EPB envs x CT column lanes (EPB * CT = 256), lane tid = el * CT + cl:
+//   layout 1 ([T][cols][E]): CT = 1, block (bx, by) = envs [256 bx, 256 bx + 256) of column by;
+//   layout 0 ([T][E][cols]): CT = min(pow2(cols), 256), block (bx, by) = envs [EPB bx, ...) x columns
+//   [CT by, CT by + CT).  Consecutive lanes read consecutive addresses in both layouts.
+struct Mom {
+  double n, mean, m2;
+};
+
+__device__ __forceinline__ Mom mom_combine(Mom a, Mom b) {  // Chan et al., pairwise update
+  if (b.n == 0.0) return a;
+  if (a.n == 0.0) return b;
+  const double n = a.n + b.n;
+  const double d = b.mean - a.mean;
+  Mom r;
+  r.n = n;
+  r.mean = a.mean + d * (b.n / n);
+  r.m2 = a.m2 + b.m2 + d * d * (a.n * b.n / n);
+  return r;
+}
+
+// per-thread moments of one sequence: sums shifted by its first element (exact 0 for a constant column)
+struct SeqMom {
+  double k, s1, s2;
+  __device__ __forceinline__ void add(double x, bool first) {
+    if (first) k = x;
+    const double d = x - k;
+    s1 += d;
+    s2 += d * d;
+  }
+  __device__ __forceinline__ Mom get(int n) const {
+    Mom m;
+    m.n = (double)n;
+    m.mean = n ? k + s1 / (double)n : 0.0;
+    m.m2 = n ? s2 - s1 * (s1 / (double)n) : 0.0;
+    if (m.m2 < 0.0) m.m2 = 0.0;
+    return m;
+  }
+};
+
+template <int TCE>
+__global__ __launch_bounds__(256) void gae_scan_moments_kernel(int T, int E, int cols, int rcols, int ct,
+                                                               const float* __restrict__ rew,
+                                                               const float* __restrict__ val,
+                                                               const uint8_t* __restrict__ done, double gamma,
+                                                               double lam, int last_shard, float* __restrict__ adv,
+                                                               float* __restrict__ ret, double* __restrict__ partial) {
+  __shared__ Mom red[2][256];
+  const int tid = threadIdx.x;
+  const int epb = 256 / ct;
+  const int el = tid / ct, cl = tid - (tid / ct) * ct;
+  const int e = (int)blockIdx.x * epb + el;
+  const int c = TCE ? (int)blockIdx.y : (int)blockIdx.y * ct + cl;
+  const bool active = e < E && c < cols;
+  const int64_t width = (int64_t)E * cols;
+  const int64_t i = TCE ? (int64_t)c * E + e : (int64_t)e * cols + c;
+  SeqMom ma{0.0, 0.0, 0.0}, mr{0.0, 0.0, 0.0};
+  if (active) {
+    const bool global_last = last_shard && (e == E - 1);
+    // per-column rewards share the values' layout; broadcast rewards are [T][E]
+    const int64_t r_off = rcols == 1 ? (int64_t)e : i;
+    const int64_t r_stride = rcols == 1 ? (int64_t)E : width;
+    // inputs of the next U steps are loaded while the current U are computed (U loads in flight)
+    constexpr int U = 4;
+    float rb[U], vb[U];
+    uint8_t db[U];
+    auto load = [&](int t0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int t = t0 - u;
+        if (t >= 0) {
+          rb[u] = rew[(int64_t)t * r_stride + r_off];
+          vb[u] = val[(int64_t)t * width + i];
+          db[u] = done[t];
+        }
+      }
+    };
+    double gae = 0.0, R = 0.0, v_next = 0.0;
+    load(T - 1);
+    for (int t0 = T - 1; t0 >= 0; t0 -= U) {
+      float rc[U], vc[U];
+      uint8_t dc[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        rc[u] = rb[u];
+        vc[u] = vb[u];
+        dc[u] = db[u];
+      }
+      if (t0 - U >= 0) load(t0 - U);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int t = t0 - u;
+        if (t < 0) break;
+        const double r = (double)rc[u], v = (double)vc[u];
+        const double nd = dc[u] ? 0.0 : 1.0;
+        R = r + R * gamma * nd;  // discount_rewards (ippo.py:107-109)
+        double a;
+        if (t == T - 1 && global_last) {
+          a = r - v;  // adv = [rewards[-1] - values[-1]]  (ippo.py:94)
+          gae = 0.0;
+        } else {
+          const double delta = r + gamma * v_next * nd - v;  // (ippo.py:96-98)
+          gae = delta + gamma * lam * nd * gae;
+          a = gae + v;
+        }
+        v_next = v;
+        const float af = (float)a, rf = (float)R;
+        const int64_t o = (int64_t)t * width + i;
+        adv[o] = af;
+        ret[o] = rf;
+        // the statistics are those of the stored fp32 values, as a separate pass over adv / ret sees them
+        ma.add((double)af, t == T - 1);
+        mr.add((double)rf, t == T - 1);
+      }
+    }
+  }
+  red[0][tid] = ma.get(active ? T : 0);
+  red[1][tid] = mr.get(active ? T : 0);
+  __syncthreads();
+  for (int s = epb >> 1; s >= 1; s >>= 1) {  // fixed-order tree over the block's envs, per column lane
+    if (el < s) {
+      red[0][tid] = mom_combine(red[0][tid], red[0][tid + s * ct]);
+      red[1][tid] = mom_combine(red[1][tid], red[1][tid + s * ct]);
+    }
+    __syncthreads();
+  }
+  if (el == 0 && c < cols) {
+    // partial [cols][nbx][2][3]
+    double* p = partial + ((int64_t)c * gridDim.x + blockIdx.x) * 6;
+    p[0] = red[0][tid].n;
+    p[1] = red[0][tid].mean;
+    p[2] = red[0][tid].m2;
+    p[3] = red[1][tid].n;
+    p[4] = red[1][tid].mean;
+    p[5] = red[1][tid].m2;
+  }
+}
+
+// one block per column: combine its nb partials in a fixed order -> moments [2][3][cols] (n, sum, M2)
+__global__ __launch_bounds__(256) void gae_moments_reduce_kernel(int nb, int cols, const double* __restrict__ partial,
+                                                                 double* __restrict__ moments) {
+  __shared__ Mom red[2][256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  Mom a{0.0, 0.0, 0.0}, r{0.0, 0.0, 0.0};
+  for (int b = tid; b < nb; b += 256) {
+    const double* p = partial + ((int64_t)c * nb + b) * 6;
+    a = mom_combine(a, Mom{p[0], p[1], p[2]});
+    r = mom_combine(r, Mom{p[3], p[4], p[5]});
+  }
+  red[0][tid] = a;
+  red[1][tid] = r;
+  __syncthreads();
+  for (int s = 128; s >= 1; s >>= 1) {
+    if (tid < s) {
+      red[0][tid] = mom_combine(red[0][tid], red[0][tid + s]);
+      red[1][tid] = mom_combine(red[1][tid], red[1][tid + s]);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const Mom m = red[k][0];
+      moments[(3 * k + 0) * cols + c] = m.n;
+      moments[(3 * k + 1) * cols + c] = m.n * m.mean;
+      moments[(3 * k + 2) * cols + c] = m.m2;
+    }
+  }
+}
+
+// x_k = gate_k ? (x_k - mean_k) * scale_k : x_k for both outputs in one pass (x1 may be null)
+__global__ __launch_bounds__(256) void normalize_pair_kernel(int64_t n4, int64_t n, int cols, int inner,
+                                                             float* __restrict__ x0, const double* __restrict__ mean0,
+                                                             const double* __restrict__ scale0,
+                                                             const int32_t* __restrict__ gate0, float* __restrict__ x1,
+                                                             const double* __restrict__ mean1,
+                                                             const double* __restrict__ scale1,
+                                                             const int32_t* __restrict__ gate1) {
+  const bool g0 = x0 && *gate0, g1 = x1 && *gate1;
+  if (!g0 && !g1) return;
+  auto col = [&](int64_t j) { return inner > 0 ? (int)((j / inner) % cols) : (int)(j % cols); };
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
+    const int64_t j = q << 2;
+    int cc[4];
+    if (inner > 0 && (inner & 3) == 0) {  // [T][cols][E], E % 4 == 0: one column per float4
+      cc[0] = cc[1] = cc[2] = cc[3] = col(j);
+    } else if (inner > 0) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) cc[u] = col(j + u);
+    } else {  // [T][E][cols]: consecutive columns, wrapping
+      const int c0 = col(j);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) cc[u] = (c0 + u) % cols;
+    }
+    if (g0) {
+      float4 v = reinterpret_cast<float4*>(x0)[q];
+      v.x = (float)(((double)v.x - mean0[cc[0]]) * scale0[cc[0]]);
+      v.y = (float)(((double)v.y - mean0[cc[1]]) * scale0[cc[1]]);
+      v.z = (float)(((double)v.z - mean0[cc[2]]) * scale0[cc[2]]);
+      v.w = (float)(((double)v.w - mean0[cc[3]]) * scale0[cc[3]]);
+      reinterpret_cast<float4*>(x0)[q] = v;
+    }
+    if (g1) {
+      float4 v = reinterpret_cast<float4*>(x1)[q];
+      v.x = (float)(((double)v.x - mean1[cc[0]]) * scale1[cc[0]]);
+      v.y = (float)(((double)v.y - mean1[cc[1]]) * scale1[cc[1]]);
+      v.z = (float)(((double)v.z - mean1[cc[2]]) * scale1[cc[2]]);
+      v.w = (float)(((double)v.w - mean1[cc[3]]) * scale1[cc[3]]);
+      reinterpret_cast<float4*>(x1)[q] = v;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {  // tail
+    const int64_t j = (n4 << 2) + threadIdx.x;
+    const int c = col(j);
+    if (g0) x0[j] = (float)(((double)x0[j] - mean0[c]) * scale0[c]);
+    if (g1) x1[j] = (float)(((double)x1[j] - mean1[c]) * scale1[c]);
+  }
+}
+
 constexpr int kStatRowBlocks = 1024;
 
 // partial[y][c] = sum over this block's rows of (x - center)^p
@@ -214,6 +442,74 @@ extern "C" int d2d_gae_scan_tce(int32_t T, int32_t E, int32_t cols, int32_t rewa
                                 const float* values, const uint8_t* dones, double gamma, double lam, int32_t last_shard,
                                 float* adv, float* ret, void* stream) {
   return gae_scan(T, E, cols, reward_cols, rewards, values, dones, gamma, lam, last_shard, adv, ret, stream, 1);
+}
+
+static void moments_grid(int32_t E, int32_t cols, int32_t layout, int* ct, dim3* grid) {
+  int c = 1;
+  if (!layout)
+    while (c < cols && c < 256) c <<= 1;
+  const int epb = 256 / c;
+  *ct = c;
+  *grid = dim3((unsigned)((E + epb - 1) / epb), (unsigned)(layout ? cols : (cols + c - 1) / c));
+}
+
+extern "C" int64_t d2d_gae_moments_workspace(int32_t E, int32_t cols, int32_t layout) {
+  if (E < 1 || cols < 1) return 6;
+  int ct;
+  dim3 g;
+  moments_grid(E, cols, layout, &ct, &g);
+  return (int64_t)cols * g.x * 6;
+}
+
+extern "C" int d2d_gae_scan_moments(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards,
+                                    const float* values, const uint8_t* dones, double gamma, double lam,
+                                    int32_t last_shard, int32_t layout, float* adv, float* ret, double* moments,
+                                    double* workspace, int64_t workspace_len, void* stream) {
+  if (T < 0 || E < 0 || cols < 1 || (reward_cols != 1 && reward_cols != cols) || (layout != 0 && layout != 1) ||
+      !rewards || !values || !dones || !adv || !ret || !moments || !workspace ||
+      workspace_len < d2d_gae_moments_workspace(E, cols, layout)) {
+    d2d_set_error("d2d_gae_scan_moments: bad arguments");
+    return D2D_EINVAL;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (T == 0 || E == 0) {
+    D2D_CHECK_HIP(hipMemsetAsync(moments, 0, sizeof(double) * 6 * cols, s));
+    return D2D_OK;
+  }
+  int ct;
+  dim3 grid;
+  moments_grid(E, cols, layout, &ct, &grid);
+  if (layout)
+    hipLaunchKernelGGL(gae_scan_moments_kernel<1>, grid, dim3(256), 0, s, T, E, cols, reward_cols, ct, rewards, values,
+                       dones, gamma, lam, last_shard, adv, ret, workspace);
+  else
+    hipLaunchKernelGGL(gae_scan_moments_kernel<0>, grid, dim3(256), 0, s, T, E, cols, reward_cols, ct, rewards, values,
+                       dones, gamma, lam, last_shard, adv, ret, workspace);
+  D2D_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(gae_moments_reduce_kernel, dim3((unsigned)cols), dim3(256), 0, s, (int)grid.x, cols, workspace,
+                     moments);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
+extern "C" int d2d_normalize_pair(int32_t T, int32_t E, int32_t cols, int32_t layout, float* x0, const double* mean0,
+                                  const double* scale0, const int32_t* gate0, float* x1, const double* mean1,
+                                  const double* scale1, const int32_t* gate1, void* stream) {
+  if (T < 0 || E < 0 || cols < 1 || (layout != 0 && layout != 1) || (!x0 && !x1) ||
+      (x0 && (!mean0 || !scale0 || !gate0)) || (x1 && (!mean1 || !scale1 || !gate1)) ||
+      (reinterpret_cast<uintptr_t>(x0) & 15) || (reinterpret_cast<uintptr_t>(x1) & 15)) {
+    d2d_set_error("d2d_normalize_pair: bad arguments (x0 / x1 16-byte aligned)");
+    return D2D_EINVAL;
+  }
+  const int64_t n = (int64_t)T * E * cols;
+  if (n == 0) return D2D_OK;
+  const int64_t n4 = n >> 2;
+  int64_t grid = (n4 + 255) / 256;
+  grid = grid < 1 ? 1 : grid > 16384 ? 16384 : grid;
+  hipLaunchKernelGGL(normalize_pair_kernel, dim3((unsigned)grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     n4, n, cols, layout ? E : 0, x0, mean0, scale0, gate0, x1, mean1, scale1, gate1);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
 }
 
 extern "C" int64_t d2d_colstats_workspace(int64_t rows, int32_t cols) {

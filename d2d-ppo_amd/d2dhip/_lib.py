@@ -24,7 +24,8 @@ if VARIANT:
     if VARIANT != "asan" and os.environ.get("D2D_ALLOW_ABLATION") != "1":
         raise RuntimeError(f"D2D_LIB_VARIANT={VARIANT} selects an ablation build of libd2dhip (wrong results "
                            f"by design); set D2D_ALLOW_ABLATION=1 as well to load it, or unset it")
-    LIB_PATH = os.path.join(PKG_DIR, "lib", f"libd2dhip_{VARIANT}.so")
+    LIB_PATH = (os.path.join(PKG_DIR, "build", "asan", "libd2dhip_asan.so") if VARIANT == "asan"
+                else os.path.join(PKG_DIR, "lib", f"libd2dhip_{VARIANT}.so"))
     print(f"[d2dhip] WARNING: loading {'sanitizer' if VARIANT == 'asan' else 'ablation'} build {LIB_PATH} "
           f"(not a product library)", file=sys.stderr, flush=True)
 
@@ -36,7 +37,7 @@ def refuse_ablation(what):
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 7
+ABI_VERSION = 8
 D2D_OBS_F32, D2D_OBS_U8 = 0, 1
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
@@ -109,6 +110,12 @@ _SIGS = {
     "d2d_colstats_finalize": (ctypes.c_int, [ctypes.c_int32, _p, _p, ctypes.c_double, ctypes.c_int32, _p, _p, _p,
                                               _p]),
     "d2d_normalize_columns": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, _p, _p, _p, _p, _p]),
+    "d2d_gae_moments_workspace": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "d2d_gae_scan_moments": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p,
+                                             ctypes.c_double, ctypes.c_double, ctypes.c_int32, ctypes.c_int32, _p, _p,
+                                             _p, _p, ctypes.c_int64, _p]),
+    "d2d_normalize_pair": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p,
+                                           _p, _p, _p, _p, _p, _p]),
     "d2d_set_option": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),
     "d2d_happo_chain": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p, _p, _p, _p]),
     "d2d_f32_to_bf16_exact": (ctypes.c_int, [ctypes.c_int64, _p, _p, _p, _p]),

@@ -79,6 +79,45 @@ def normalize_columns_(x2d, ddof, group=None, n_total=None, tce=None):
     return gate
 
 
+def moments_colsum(moments, multi_rank):
+    """two_pass_column_stats' colsum(center) from one rank's moments [3][cols] = (n, sum, M2 about the
+    local mean): Σx, and Σ(x - center)² = M2 + n (mean_local - center)²."""
+    n_loc, s_loc, m2_loc = moments[0], moments[1], moments[2]
+
+    def colsum(center):
+        if center is None:
+            return s_loc.clone()
+        if not multi_rank:
+            return m2_loc.clone()  # one rank: the local mean IS the mean (the correction is 0 up to rounding)
+        mean_loc = torch.where(n_loc > 0, s_loc / n_loc.clamp(min=1), center)
+        return m2_loc + n_loc * (mean_loc - center) ** 2
+    return colsum
+
+
+def moments_stats(moments, ddof, n, group=None):
+    """(mean, scale, gate) of one output from the scan's fused moments [3][cols] (n, sum, M2) of this
+    rank's elements, through the two_pass_column_stats protocol: Σx all-reduced, then
+    Σ(x - mean)² = M2 + n (mean_local - mean)² all-reduced -- the same sums a second pass over the data
+    would produce, from [cols] vectors."""
+    lib = _lib.require_gpu()
+    cols = moments.shape[1]
+    dev = moments.device
+    st = _lib.stream_ptr()
+    mean = torch.empty(cols, dtype=torch.float64, device=dev)
+    scale = torch.empty(cols, dtype=torch.float64, device=dev)
+    gate = torch.zeros(1, dtype=torch.int32, device=dev)
+    colsum = moments_colsum(moments, group is not None)
+
+    def finalize(s1, m2):
+        _lib.check(lib.d2d_colstats_finalize(cols, s1.data_ptr(), None if m2 is None else m2.data_ptr(), float(n),
+                                             ddof, mean.data_ptr(), None if m2 is None else scale.data_ptr(),
+                                             None if m2 is None else gate.data_ptr(), st), "d2d_colstats_finalize")
+        return mean, scale, gate
+
+    two_pass_column_stats(colsum, finalize, group)
+    return mean, scale, gate
+
+
 def gae_returns(rewards, values, dones, gamma, lam=0.97, normalize_adv=True, normalize_ret=True, group=None,
                 last_shard=True, n_envs_total=None, layout="tec"):
     """rewards [T][E] or [T][E][cols] float32, values [T][E][cols] float32, dones [T] (bool/uint8).
@@ -88,6 +127,8 @@ def gae_returns(rewards, values, dones, gamma, lam=0.97, normalize_adv=True, nor
     Returns (adv, ret), in the values' layout, float32:
       adv = the reference's compute_gae output (lambda-returns, ippo.py:92-102), normalised with ddof 0;
       ret = discount_rewards (ippo.py:104-116), normalised with ddof 1.
+    Two passes over the data: the scan (which also accumulates both outputs' column moments,
+    d2d_gae_scan_moments) and one normalisation pass over adv and ret together (d2d_normalize_pair).
     """
     lib = _lib.require_gpu()
     if values.dim() != 3:
@@ -111,17 +152,26 @@ def gae_returns(rewards, values, dones, gamma, lam=0.97, normalize_adv=True, nor
     d = dones.to(device=values.device, dtype=torch.uint8).contiguous()
     if d.numel() != T:
         raise ValueError("dones must have T entries")
+    dev = values.device
     adv = torch.empty_like(values)
     ret = torch.empty_like(values)
-    scan = lib.d2d_gae_scan_tce if tce else lib.d2d_gae_scan
-    _lib.check(scan(T, E, cols, rcols, rewards.data_ptr(), values.data_ptr(), d.data_ptr(), float(gamma),
-                    float(lam), 1 if last_shard else 0, adv.data_ptr(), ret.data_ptr(), _lib.stream_ptr()),
-               "d2d_gae_scan")
-    n_total = None if n_envs_total is None else T * int(n_envs_total)
-    for x, do, ddof in ((adv, normalize_adv, 0), (ret, normalize_ret, 1)):
+    lay = 1 if tce else 0
+    moments = torch.empty((2, 3, cols), dtype=torch.float64, device=dev)
+    ws = torch.empty(int(lib.d2d_gae_moments_workspace(E, cols, lay)), dtype=torch.float64, device=dev)
+    _lib.check(lib.d2d_gae_scan_moments(T, E, cols, rcols, rewards.data_ptr(), values.data_ptr(), d.data_ptr(),
+                                        float(gamma), float(lam), 1 if last_shard else 0, lay, adv.data_ptr(),
+                                        ret.data_ptr(), moments.data_ptr(), ws.data_ptr(), ws.numel(),
+                                        _lib.stream_ptr()), "d2d_gae_scan_moments")
+    n = T * E if n_envs_total is None else T * int(n_envs_total)
+    args = []
+    for x, do, k, ddof in ((adv, normalize_adv, 0, 0), (ret, normalize_ret, 1, 1)):
         if do:
-            if tce:
-                normalize_columns_(x, ddof, group, n_total, tce=(T, cols, E))
-            else:
-                normalize_columns_(x.view(T * E, cols), ddof, group, n_total)
+            mean, scale, gate = moments_stats(moments[k], ddof, n, group)
+            args += [x.data_ptr(), mean.data_ptr(), scale.data_ptr(), gate.data_ptr()]
+            args.append((mean, scale, gate))  # keep alive until the launch is queued
+        else:
+            args += [None, None, None, None, None]
+    if normalize_adv or normalize_ret:
+        _lib.check(lib.d2d_normalize_pair(T, E, cols, lay, *args[0:4], *args[5:9], _lib.stream_ptr()),
+                   "d2d_normalize_pair")
     return adv, ret

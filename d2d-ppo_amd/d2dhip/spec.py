@@ -48,6 +48,10 @@ def poisson_cdf_table(lam, kinds):
     pois = np.asarray(kinds) == POISSON
     if pois.any():
         lp = lam[pois]
+        # a threshold ceil(F_x * 2^32) - 1 needs F_x > 0: exp(-lam) underflows near lam = 745, and the
+        # uint8 cells already cap the mean at 64 (EnvSpec.agent_table), so refuse such means here too
+        if np.any(~(lp <= 64.0)):
+            raise NotImplementedError("Poisson means > 64 overflow the uint8 buffer cells")
         p = np.exp(-lam)[pois]  # the agent table's pois_p0, computed over the same array
         F = p.copy()
         cols = [F.copy()]

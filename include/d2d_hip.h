@@ -43,9 +43,9 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 7  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
+#define D2D_ABI_VERSION 8  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
                               6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_states_to_bf16_exact,
-                              d2d_critic_dpre_split */
+                              d2d_critic_dpre_split; 8: d2d_gae_scan_moments, d2d_normalize_pair */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -202,6 +202,21 @@ int d2d_colstats(int64_t rows, int32_t cols, const float* x, const double* cente
 int d2d_colstats_tce(int32_t T, int32_t cols, int32_t E, const float* x, const double* center, double* partial,
                      double* out, void* stream);
 
+/* The scan above with the normalisation statistics of BOTH outputs fused into it (ABI 8): one pass
+ * writes adv / ret and accumulates, per column, n, sum and M2 = sum of squared deviations from the
+ * column mean of the stored fp32 values (compute_gae's np.std / discount_rewards' torch std inputs,
+ * ippo.py:99-101, 113-115), combined in double with Chan's pairwise formula in a fixed order (bitwise
+ * reproducible, no atomics).  layout 0 = [T][E][cols] (d2d_gae_scan), 1 = [T][cols][E] (_tce).
+ *   moments [2][3][cols] doubles out: [0] adv, [1] ret; [k][0] n, [k][1] sum, [k][2] M2
+ *   workspace: d2d_gae_moments_workspace(E, cols, layout) doubles
+ * Data-parallel shards combine their moments with two all-reduces of [cols] vectors (d2dhip/gae.py);
+ * one rank passes sum / M2 straight to d2d_colstats_finalize. */
+int64_t d2d_gae_moments_workspace(int32_t E, int32_t cols, int32_t layout);
+int d2d_gae_scan_moments(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards,
+                         const float* values, const uint8_t* dones, double gamma, double lam, int32_t last_shard,
+                         int32_t layout, float* adv, float* ret, double* moments, double* workspace,
+                         int64_t workspace_len, void* stream);
+
 /* mean = sum / n ; when m2 != NULL: std = sqrt(m2 / (n - ddof)), scale = 1/std and
  * *gate = all columns std > 0 (ippo.py:100-101, 114-115); when m2 == NULL only mean. */
 int d2d_colstats_finalize(int32_t cols, const double* sum, const double* m2, double n, int32_t ddof,
@@ -213,6 +228,12 @@ int d2d_normalize_columns(int64_t rows, int32_t cols, float* x, const double* me
 /* the same on x [T][cols][E] */
 int d2d_normalize_columns_tce(int32_t T, int32_t cols, int32_t E, float* x, const double* mean, const double* scale,
                               const int32_t* gate, void* stream);
+
+/* Both outputs of the scan normalised in one pass (ABI 8): x_k = gate_k ? (x_k - mean_k) * scale_k : x_k
+ * per column, k = 0, 1; x1 (or x0) may be NULL; layout as d2d_gae_scan_moments; x 16-byte aligned. */
+int d2d_normalize_pair(int32_t T, int32_t E, int32_t cols, int32_t layout, float* x0, const double* mean0,
+                       const double* scale0, const int32_t* gate0, float* x1, const double* mean1,
+                       const double* scale1, const int32_t* gate1, void* stream);
 
 /* fp32 -> bf16 (the high 16 bits) of n floats in one pass, *inexact = 1 iff some x is not
  * bf16-exact (nonzero low 16 bits), else 0.  x 16-byte, out 8-byte aligned.  Replaces the

@@ -14,7 +14,7 @@ from .env_oracle import _Spec
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 # D2D_ORACLE_ASAN=1: the AddressSanitizer / UBSan build (make -C oracle asan; tests/test_sanitizers_cpu.py)
-LIB_PATH = os.path.join(HERE, "build", "libd2d_oracle_asan.so" if os.environ.get("D2D_ORACLE_ASAN") == "1"
+LIB_PATH = os.path.join(HERE, "build", "asan/libd2d_oracle_asan.so" if os.environ.get("D2D_ORACLE_ASAN") == "1"
                         else "libd2d_oracle.so")
 
 _p = ctypes.c_void_p

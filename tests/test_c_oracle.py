@@ -60,6 +60,15 @@ def test_poisson_cdf_table_equals_inversion():
         assert (x == want).all(), k
 
 
+def test_poisson_cdf_table_refuses_underflowing_means():
+    """exp(-lam) underflows to 0 near lam = 745, where ceil(F_x * 2^32) - 1 would wrap: such means
+    (and every mean past the uint8 cells' 64) are refused at table build time, not mis-tabulated."""
+    from d2dhip.spec import POISSON, poisson_cdf_table
+    for lam in (64.5, 800.0, np.inf, np.nan):
+        with pytest.raises(NotImplementedError):
+            poisson_cdf_table(np.array([0.5, lam]), np.array([POISSON, POISSON]))
+
+
 @pytest.mark.parametrize("name", env_fixture_names())
 def test_c_oracle_replays_reference(name):
     z = np.load(os.path.join(GOLDEN, f"env_{name}.npz"))

@@ -93,6 +93,16 @@ def _worker(rank, ws, port, outdir):
                 lambda s1, m2: colstats_finalize(s1, m2, 1000.0, ddof), dp.dist.group.WORLD)
             np.save(os.path.join(outdir, f"stats{rank}_{ddof}.npy"),
                     torch.stack([mean, 1.0 / scale, gate.double().expand(4)]).numpy())
+            # the same statistics from the scan's fused per-rank moments (n, sum, M2 about the local mean;
+            # d2d_gae_scan_moments) through gae.moments_colsum: no second pass over the data
+            from d2dhip.gae import moments_colsum
+            mom = torch.stack([torch.full((4,), 500.0, dtype=torch.float64), loc.sum(0),
+                               ((loc - loc.mean(0)) ** 2).sum(0)])
+            mean, scale, gate = two_pass_column_stats(moments_colsum(mom, True),
+                                                      lambda s1, m2: colstats_finalize(s1, m2, 1000.0, ddof),
+                                                      dp.dist.group.WORLD)
+            np.save(os.path.join(outdir, f"mstats{rank}_{ddof}.npy"),
+                    torch.stack([mean, 1.0 / scale, gate.double().expand(4)]).numpy())
     finally:
         dist.destroy_process_group()
 
@@ -120,6 +130,9 @@ def test_two_rank_update_equals_full_batch(tmp_path):
         np.testing.assert_allclose(s0[0], full.mean(0), rtol=0, atol=1e-12)
         np.testing.assert_allclose(s0[1], full.std(0, ddof=ddof), rtol=0, atol=1e-12)
         assert np.all(s0[2] == 1)
+        m0, m1 = np.load(tmp_path / f"mstats0_{ddof}.npy"), np.load(tmp_path / f"mstats1_{ddof}.npy")
+        np.testing.assert_allclose(m0, m1, rtol=0, atol=0)
+        np.testing.assert_allclose(m0, s0, rtol=0, atol=1e-12)
 
 
 def test_single_process_hooks_are_identity():

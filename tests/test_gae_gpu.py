@@ -115,3 +115,66 @@ def test_gae_kernel_tce_layout(T, E, cols, rcols):
         adv_o, ret_o = gae_returns_batched(rew, val, done, 0.6, 0.97)
         np.testing.assert_allclose(adv_t.transpose(0, 2, 1), adv_o, rtol=0, atol=ATOL)
         np.testing.assert_allclose(ret_t.transpose(0, 2, 1), ret_o, rtol=0, atol=ATOL)
+
+
+@pytest.mark.parametrize("layout,T,E,cols,rcols", [("tce", 200, 1000, 64, 1), ("tec", 200, 333, 64, 1),
+                                                   ("tec", 50, 300, 5, 5), ("tec", 120, 1, 4, 1),
+                                                   ("tec", 30, 7, 300, 1), ("tce", 17, 4097, 3, 3)])
+def test_gae_scan_moments_fused_stats(layout, T, E, cols, rcols):
+    """d2d_gae_scan_moments (the scan with both outputs' column moments fused in): adv / ret bitwise
+    equal to the plain scan, (n, sum, M2) per column equal to float64 statistics of the stored fp32
+    outputs (1e-12 relative), and bitwise reproducible run to run (fixed-order combines)."""
+    from d2dhip import _lib
+    lib = _lib.require_gpu()
+    dev = "cuda"
+    g = torch.Generator(device=dev)
+    g.manual_seed(T + E + cols)
+    tce = layout == "tce"
+    vshape = (T, cols, E) if tce else (T, E, cols)
+    val = torch.randn(vshape, device=dev, generator=g) * 3 + 1
+    rew = torch.randint(0, 5, (T, E) if rcols == 1 else vshape, device=dev, generator=g).float()
+    done = torch.zeros(T, dtype=torch.uint8, device=dev)
+    done[T // 2] = 1
+    done[-1] = 1
+    lay = 1 if tce else 0
+
+    def fused():
+        adv, ret = torch.empty_like(val), torch.empty_like(val)
+        mom = torch.empty((2, 3, cols), dtype=torch.float64, device=dev)
+        ws = torch.empty(int(lib.d2d_gae_moments_workspace(E, cols, lay)), dtype=torch.float64, device=dev)
+        _lib.check(lib.d2d_gae_scan_moments(T, E, cols, rcols, rew.data_ptr(), val.data_ptr(), done.data_ptr(), 0.6,
+                                            0.97, 1, lay, adv.data_ptr(), ret.data_ptr(), mom.data_ptr(),
+                                            ws.data_ptr(), ws.numel(), _lib.stream_ptr()), "scan_moments")
+        return adv, ret, mom
+
+    a1, r1, m1 = fused()
+    a2, r2, m2 = fused()
+    assert torch.equal(a1, a2) and torch.equal(r1, r2) and torch.equal(m1, m2)
+    a0, r0 = torch.empty_like(val), torch.empty_like(val)
+    scan = lib.d2d_gae_scan_tce if tce else lib.d2d_gae_scan
+    _lib.check(scan(T, E, cols, rcols, rew.data_ptr(), val.data_ptr(), done.data_ptr(), 0.6, 0.97, 1, a0.data_ptr(),
+                    r0.data_ptr(), _lib.stream_ptr()), "scan")
+    assert torch.equal(a1, a0) and torch.equal(r1, r0)
+    for k, x in enumerate((a1, r1)):
+        xc = (x.permute(1, 0, 2) if tce else x.permute(2, 0, 1)).reshape(cols, -1).double()   # [cols][T*E]
+        assert torch.equal(m1[k, 0], torch.full((cols,), float(T * E), dtype=torch.float64, device=dev))
+        torch.testing.assert_close(m1[k, 1], xc.sum(1), rtol=1e-12, atol=1e-9)
+        torch.testing.assert_close(m1[k, 2], ((xc - xc.mean(1, keepdim=True)) ** 2).sum(1), rtol=1e-11, atol=1e-9)
+
+
+def test_gae_constant_column_keeps_gate_closed():
+    """Quirk Q2 on the fused statistics: one constant column (std exactly 0) disables the
+    normalisation of every column, for adv (ddof 0) and ret (ddof 1) alike."""
+    from d2dhip.gae import gae_returns
+    T, E, cols = 40, 300, 3
+    dev = "cuda"
+    val = torch.randn(T, E, cols, device=dev)
+    val[..., 1] = 0.0
+    rew = torch.zeros(T, E, cols, device=dev)
+    rew[..., 0] = 1.0
+    done = torch.zeros(T, dtype=torch.uint8, device=dev)
+    done[-1] = 1
+    adv_raw, ret_raw = gae_returns(rew, val, done, 0.5, 0.97, normalize_adv=False, normalize_ret=False, last_shard=False)
+    adv, ret = gae_returns(rew, val, done, 0.5, 0.97, last_shard=False)
+    # column 1: rewards 0, values 0 -> adv = ret = 0 everywhere (std 0) -> no column is normalised
+    assert torch.equal(adv, adv_raw) and torch.equal(ret, ret_raw)

@@ -39,9 +39,11 @@ def cases():
     and on E > 1 envs (reference episode e * waves + w -> env e, wave w: the production multi-env path)."""
     out = []
     for n in names():
-        ep = 4 if n.endswith("_ep4") else 2
-        for E in ((1, 2, 4) if ep == 4 else (1, 2)):
-            out.append((n, E))
+        with np.load(os.path.join(GOLDEN, f"learner_{n}.npz")) as z:
+            ep = int(z["episodes"]) if "episodes" in z.files else 2
+        for E in (1, 2, 4):
+            if ep % E == 0:
+                out.append((n, E))
     return out
 
 
@@ -257,6 +259,59 @@ def test_graph_rollout_equals_eager(algo, kind):
                 assert torch.equal(x, y)
     # consecutive rollouts differ (fresh Philox counters on replay)
     assert not torch.equal(outs[1][1][1], outs[1][2][1])
+
+
+def test_episode_batches_draw_fresh_episodes():
+    """n_envs = 1 drivers roll num_episodes episodes side by side in private episode batches
+    (_learner._episode_batch).  Every episode must see fresh env draws, as the reference's single
+    global RNG stream gives: a train-size and a test-size batch must not replay each other's
+    arrivals / channel flips, and a batch rebuilt after eviction must not restart its counters.
+    With deterministic actions (test mode) two rollouts of the same weights on the same env draws
+    would be identical, so equal obs would reveal reused draws."""
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm GPU")
+    from algorithms.ippo import iPPO
+    from envs.combinatorial_env import CombinatorialEnv
+    N = 6
+    env = CombinatorialEnv(N, 4, np.array([4, 7] * 3), np.full(N, 0.4), episode_length=20,
+                           channel_switch=np.full((N, 4), 0.3), homogeneous_size=True, device="cuda", seed=9)
+    torch.manual_seed(0)
+    lr = iPPO(env, hidden_size=32, gamma=0.5, device="cuda", combinatorial=True, early_stopping=False)
+    obs = []
+    for n in (3, 5, 7, 3):  # the fourth rebuilds the evicted size-3 batch
+        ro = lr._collect(n, train=False)
+        assert ro.E == n
+        obs.append(ro.obs_f32[:, 0].clone())  # env 0's episode [T][N][F]
+    for i in range(len(obs)):
+        for j in range(i):
+            assert not torch.equal(obs[i], obs[j]), (i, j)
+    b = lr._episode_batch(5)
+    assert b.desc.env_base >= lr.EPISODE_ENV_BASE > env.batch().desc.env_base + env.batch().E
+    assert b.rng_step == lr._episode_rng_step > 0
+
+
+def test_rollout_graph_bound_to_its_batch():
+    """A captured rollout graph bakes in its env batch's buffers: evicting the batch drops the graph,
+    and a graph is replayed only for the very batch it was captured on."""
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a ROCm GPU")
+    from algorithms.ippo import iPPO
+    from envs.combinatorial_env import CombinatorialEnv
+    N = 6
+    env = CombinatorialEnv(N, 4, np.array([4, 7] * 3), np.full(N, 0.4), episode_length=10,
+                           channel_switch=np.full((N, 4), 0.3), homogeneous_size=True, device="cuda", seed=9)
+    torch.manual_seed(0)
+    lr = iPPO(env, hidden_size=32, gamma=0.5, device="cuda", combinatorial=True, early_stopping=False)
+    lr._collect(4, train=True)  # warm-up rollout + capture
+    (G,) = lr._rollout_graphs.values()
+    assert G["batch"] is lr._episode_batches[4]
+    lr._collect(5, train=False)
+    lr._collect(6, train=False)  # evicts the size-4 batch, and with it its graph
+    assert not lr._rollout_graphs
+    ro = lr._collect(4, train=True)  # a new size-4 batch: captured afresh, not replayed
+    (G2,) = lr._rollout_graphs.values()
+    assert G2["batch"] is lr._episode_batches[4] and G2 is not G
+    assert ro.E == 4
 
 
 @pytest.mark.parametrize("N", [12, 256])

@@ -486,8 +486,34 @@ LEARNER_VARIANTS = {
     "rnn_d2denv": ("single", True, False, 3),
 }
 
+# The reference drivers' own GRU shapes (gen_learner_drivers): hidden_size = 64 with a long window
+# (xp_load.py:78-89 runs D2D-PPO with history_len = n_agents), and run_ippo_combinatorial.py:29-89's
+# 6 agents x 16 channels (obs up to 14 + 2 * 16 = 46 inputs) with history_len = 6.
+# name: (env kind, useRNN, combinatorial, history_len, hidden, episode_length, algos, episodes)
+DRIVER_VARIANTS = {
+    "rnn_comb_h64L16": ("comb_xpload", True, True, 16, 64, 24, ("d2d", "ippo"), 1),
+    "rnn_comb16_h64": ("comb16", True, True, 6, 64, 20, ("ippo", "d2d"), 1),
+}
+
 
 def _learner_env(kind, episode_length=20):
+    if kind == "comb_xpload":
+        # xp_load.py:60-75 on setup_8_channels at load 1/2, homogeneous obs (14 + 2 * 8 = 30 inputs)
+        mod = ref_module("envs.combinatorial_env")
+        setup8 = safe_pickle.load(f"{DATA}/setup_8_channels.p")
+        p = dict(n_agents=6, n_channels=8, deadlines=setup8["deadlines"], lbdas=np.array([0.5] * 6),
+                 period=np.array([2] * 6), arrival_probs=setup8["arrival_probs"], offsets=setup8["offsets"],
+                 episode_length=episode_length, traffic_model="heterogeneous", homogeneous_size=True,
+                 periodic_devices=[0, 1, 2], channel_switch=setup8["channel_switch"])
+        return mod.CombinatorialEnv(**p), p
+    if kind == "comb16":
+        # run_ippo_combinatorial.py:29-76 at load 1 (1-D channel_switch broadcast over agents)
+        mod = ref_module("envs.combinatorial_env")
+        p = dict(n_agents=6, n_channels=16, deadlines=np.array([7, 14] * 3), lbdas=np.array([1.0] * 6),
+                 period=np.array([1.0] * 6), arrival_probs=np.array([0.4, 0.8] * 3), offsets=np.zeros(6),
+                 episode_length=episode_length, traffic_model="heterogeneous", periodic_devices=[0, 1],
+                 channel_switch=np.array([0.8] * 16))
+        return mod.CombinatorialEnv(**p), p
     if kind == "comb":
         mod = ref_module("envs.combinatorial_env")
         setup8 = safe_pickle.load(f"{DATA}/setup_8_channels.p")
@@ -512,28 +538,30 @@ def _learner_env(kind, episode_length=20):
     return mod.ChannelSelectionEnv(**p), p
 
 
-def gen_learner(only=None, episodes=2, suffix="", algos=("ippo", "d2d")):
+def gen_learner(only=None, episodes=2, suffix="", algos=("ippo", "d2d"), variants=None):
     import torch
     ippo = ref_module("algorithms.ippo")
     d2d = ref_module("algorithms.d2d_ppo")
     import sys as _sys
     if only is None:
         only = [a for a in _sys.argv[2:]]
-    for vname, (kind, useRNN, comb, hl) in LEARNER_VARIANTS.items():
+    if variants is None:
+        variants = {k: v + (16, 20, algos, episodes) for k, v in LEARNER_VARIANTS.items()}
+    for vname, (kind, useRNN, comb, hl, hidden, ep_len, v_algos, episodes) in variants.items():
         if only and vname not in only:
             continue
-        for algo in (("ippo",) if kind == "single" else algos):
-            out = {"kind": kind, "useRNN": useRNN, "combinatorial": comb, "history_len": hl, "hidden": 16,
-                   "gamma": 0.6, "episode_length": 20, "episodes": episodes}
-            env, params = _learner_env(kind)
+        for algo in (("ippo",) if kind == "single" else v_algos):
+            out = {"kind": "comb" if kind.startswith("comb") else kind, "useRNN": useRNN, "combinatorial": comb,
+                   "history_len": hl, "hidden": hidden, "gamma": 0.6, "episode_length": ep_len, "episodes": episodes}
+            env, params = _learner_env(kind, ep_len)
             out["params_json"] = json.dumps({k: _jsonable(v) for k, v in params.items()})
             torch.manual_seed(3)
             np.random.seed(5)
             if algo == "ippo":
-                lr = ippo.iPPO(env, hidden_size=16, gamma=0.6, policy_lr=3e-3, value_lr=1e-2, device="cpu",
+                lr = ippo.iPPO(env, hidden_size=hidden, gamma=0.6, policy_lr=3e-3, value_lr=1e-2, device="cpu",
                                useRNN=useRNN, combinatorial=comb, history_len=hl, early_stopping=False)
             else:
-                lr = d2d.D2DPPO(env, hidden_size=16, gamma=0.6, policy_lr=3e-3, value_lr=1e-2, beta_entropy=0.02,
+                lr = d2d.D2DPPO(env, hidden_size=hidden, gamma=0.6, policy_lr=3e-3, value_lr=1e-2, beta_entropy=0.02,
                                 device="cpu", useRNN=useRNN, combinatorial=comb, history_len=hl,
                                 early_stopping=False)
                 _put(out, "init/critic", _sd_np(lr.value_network))
@@ -609,6 +637,12 @@ def gen_learner4():
     gen_learner(only=["mlp_comb", "rnn_cat", "mlp_d2denv"], episodes=4, suffix="_ep4")
 
 
+def gen_learner_drivers():
+    """GRU traces at the reference drivers' own network shapes (DRIVER_VARIANTS): hidden 64 with a
+    16-step window, and the 6 x 16-channel env with 46 inputs."""
+    gen_learner(only=[], variants=DRIVER_VARIANTS)
+
+
 def gen_evaltest():
     """The reference's deterministic evaluation `test(num_episodes)` (ippo.py:345-388,
     d2d_ppo.py:341-383) for every learner variant: fixed weights, 4 episodes.  Recorded: the
@@ -654,7 +688,8 @@ def gen_evaltest():
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     table = {"data": gen_data, "env": gen_env, "d2denv": gen_d2denv, "gae": gen_gae, "learner": gen_learner,
-             "baselines": gen_baselines, "evaltest": gen_evaltest, "learner4": gen_learner4}
+             "baselines": gen_baselines, "evaltest": gen_evaltest, "learner4": gen_learner4,
+             "learner_drivers": gen_learner_drivers}
     # `learner <variant> ...` regenerates only the named learner variants
     which = sys.argv[1:2] if sys.argv[1:2] == ["learner"] else sys.argv[1:]
     for w in which or list(table):
