@@ -212,14 +212,47 @@ class PhaseTimer:
         return out
 
 
-def load_pmc_traffic(mode="fp32"):
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json" if mode == "fp32" else f"pmc_traffic_{mode}.json")
-    if not os.path.exists(p):
-        return None
+def load_profile_json(name):
+    """A committed measurement under profiles/ (rocprofv3 PMC summaries made by tools/gpu/*.sh on the GPU
+    box from a committed tree; each records the commit and the rocprofv3 output it came from).  Returns
+    (dict, repo-relative path) or (None, path)."""
+    rel = os.path.join("profiles", name)
     try:
-        return json.load(open(p))
+        return json.load(open(os.path.join(ROOT, rel))), rel
     except (OSError, ValueError):
+        return None, rel
+
+
+def load_pmc_traffic(mode="fp32"):
+    return load_profile_json("pmc_traffic.json" if mode == "fp32" else f"pmc_traffic_{mode}.json")
+
+
+def pmc_mfma(kernel_prefix):
+    """PMC-measured MFMA pipe utilisation of a kernel (profiles/pmc_mfma.json, tools/pmc_mfma.py:
+    SQ_VALU_MFMA_BUSY_CYCLES / (kernel cycles x 1024 SIMDs) over rocprofv3 --pmc passes), with its source."""
+    d, rel = load_profile_json("pmc_mfma.json")
+    if not d:
         return None
+    for k in d.get("kernels", []):
+        if k.get("kernel", "").startswith(kernel_prefix):
+            return {"mfma_busy_frac_pmc": k.get("mfma_busy_frac"), "valu_per_mfma_pmc": k.get("valu_per_mfma"),
+                    "source": rel, "commit": d.get("commit"), "workload": d.get("workload"),
+                    "pmc_kernel": k.get("kernel")}
+    return None
+
+
+def env_kernel_name(spec, record):
+    """The env-step kernel instantiation a step of this spec launches (csrc/env_kernels.hip dispatch_*),
+    as rocprofv3 names it."""
+    dw = {1: 1, 2: 2, 3: 3, 4: 4}.get(int(spec.DW), int(spec.DW))
+    large = "true" if spec.N > 64 else "false"
+    if spec.kind == "chsel":
+        return f"d2d::chsel_kernel<{dw}, {large}>"
+    if spec.kind == "single":
+        return f"d2d::single_kernel<{dw}, {large}>"
+    mask = "unsigned char" if spec.C <= 8 else "unsigned short" if spec.C <= 16 else "unsigned int"
+    ct = spec.C if spec.C in (4, 8, 16) else 0
+    return f"d2d::comb_kernel<{mask}, {dw}, {large}, {ct}, false>" + (" (record)" if record else "")
 
 
 def rollout_leg(env, args, world):
@@ -272,12 +305,14 @@ def rollout_leg(env, args, world):
     F, H, A = lr.policy.F, lr.policy.H, lr.policy.A
     flop = 2 * (F * H + H * A) + 2 * (F * H + H)  # actor + critic forward per agent-step
     tflops = flop * b.E * b.spec.N / (pol_ms / 1e3) / 1e12
+    # the products run as exact bf16 splits: the algorithmic fp32 rate is no roofline;
+    # the roofline figure is the executed MFMA pipe's busy fraction (PMC, with its source file)
     return {"env_steps_per_s": v, "agent_steps_per_s": v * b.spec.N, "ms_per_step": el / K * 1e3, "steps": K,
             "policy": f"iPPO MLP H=64 actor+critic, 64 agents, Bernoulli sampling, fp32; {path}",
             "obs_format": "compact record (u8)" if lr._record_ok() else "fp32",
             "policy_kernel_us": pol_ms * 1e3, "env_kernel_us": env_ms * 1e3,
             "policy_flop_per_agent_step": flop, "policy_tflops_fp32_equiv": tflops,
-            "policy_frac_of_fp32_matrix_peak": tflops / 157.3}
+            "policy_mfma_pmc": pmc_mfma("d2d::policy_split_kernel")}
 
 
 def ppo_leg(args, rank, world, local):
@@ -355,9 +390,9 @@ def update_kernel_roofline(lr, ro, F, H, A, reps=4):
     for name, ms, fl in (("actor", ta, f_actor), ("critic", tc, f_critic)):
         tf = agent_samples * fl / (ms / 1e3) / 1e12
         busy = tiles * pipe[name] / simds / clock / (ms / 1e3)
-        res[name] = {"ms": ms, "flop_per_agent_sample": fl, "achieved_tflops": tf,
-                     "fp32_matrix_peak_tflops": 157.3, "mfma_cycles_per_tile": pipe[name],
-                     "mfma_pipe_busy_frac": busy, "bound": "mfma"}
+        res[name] = {"ms": ms, "flop_per_agent_sample": fl, "achieved_tflops_fp32_equiv": tf,
+                     "mfma_cycles_per_tile": pipe[name], "mfma_pipe_busy_frac_static": busy,
+                     "mfma_pmc": pmc_mfma(f"d2d::ppo_{name}_grad_kernel"), "bound": "mfma"}
     return res
 
 
@@ -405,29 +440,44 @@ def train_leg(env, args, rank, world, local):
             "path": "fused policy kernel + env kernel rollout, HIP GAE, fused PPO gradient kernels + Adam"}
 
 
-def _env_rate(env, steps=40):
-    """Env-step throughput of a batched env (device-sampled actions + env kernel, obs emitted)."""
+def _env_rate(env, steps=40, bytes_per_agent_step=None):
+    """Env-step throughput of a batched env (device-sampled actions + env kernel, fp32 obs emitted)
+    and the env kernel's own HBM roofline: its average HIP-event time against SURVEY §8(d)'s
+    algorithmic bytes per agent-step."""
     b = env.batch()
     act = b.action_buffer()
     b.reset(want_obs=True)
     for _ in range(5):
         b.sample_actions(0.1, out=act)
         b.step(act, want_obs=True)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
         if b.timestep >= env.episode_length:
             b.reset(want_obs=True)
         b.sample_actions(0.1, out=act)
+        evs[i][0].record()
         b.step(act, want_obs=True)
+        evs[i][1].record()
     torch.cuda.synchronize()
-    return b.E * steps / (time.perf_counter() - t0)
+    rate = b.E * steps / (time.perf_counter() - t0)
+    kern_us = float(np.mean([x.elapsed_time(y) for x, y in evs])) * 1e3
+    roof = {"kernel": env_kernel_name(b.spec, False), "kernel_avg_us": kern_us,
+            "step_us": 1e6 * b.E / rate}
+    if bytes_per_agent_step:
+        launch = bytes_per_agent_step * b.spec.N * b.E
+        roof.update({"bytes_per_agent_step": bytes_per_agent_step, "bytes_per_launch": launch,
+                     "achieved_GBps": launch / (kern_us / 1e6) / 1e9,
+                     "hbm_frac": launch / (kern_us / 1e6) / 1e9 / HBM_PEAK_GBS})
+    return rate, roof
 
 
 def _d2d_iteration(env, n_epoch, combinatorial):
     """One D2D-PPO training iteration (d2d_ppo.py:405-448 loop body without test()): rollout of
     every env, returns, n_epoch epochs (critic values, GAE, chain over a random agent cycle,
-    fused actor gradients, clip + Adam, central critic).  Seconds, after one warm-up iteration."""
+    fused actor gradients, clip + Adam, central critic).  Seconds after one warm-up iteration, the
+    fused-update flag and the iteration's phase split (HIP events at the learner's phase marks, ms)."""
     from algorithms.d2d_ppo import D2DPPO
     torch.manual_seed(3)
     np.random.seed(3)
@@ -443,10 +493,14 @@ def _d2d_iteration(env, n_epoch, combinatorial):
 
     it(1)
     torch.cuda.synchronize()
+    lr.phase_timer = PhaseTimer()
     t0 = time.perf_counter()
     it(n_epoch)
     torch.cuda.synchronize()
-    return time.perf_counter() - t0, lr._fused_update_ok()
+    el = time.perf_counter() - t0
+    phases = lr.phase_timer.totals_ms()
+    lr.phase_timer = None
+    return el, lr._fused_update_ok(), phases
 
 
 def configs_leg(args, rank, world, local):
@@ -466,10 +520,11 @@ def configs_leg(args, rank, world, local):
               traffic_model="aperiodic", periodic_devices=[], channel_switch=np.full(5, 0.8))
     env = ChannelSelectionEnv(**p2, n_envs=4096, device=dev, seed=21)
     env.shard(rank, world)
-    rate = _env_rate(env)
-    it_s, fused = _d2d_iteration(env, 5, combinatorial=False)
+    # chsel B_as = 1 + 2D + 4(D + C + 1) + 2(C + 1)/N = 63.6 B at D = 7, C = 4, N = 16
+    rate, roof = _env_rate(env, bytes_per_agent_step=1 + 2 * 7 + 4 * (7 + 4 + 1) + 2 * 5 / N)
+    it_s, fused, phases = _d2d_iteration(env, 5, combinatorial=False)
     out["c2"] = {"envs_per_gpu": 4096, "agents": N, "channels": 4, "env_steps_per_s": rate * world,
-                 "d2d_iteration_s": it_s, "fused_update": fused,
+                 "env_kernel": roof, "d2d_iteration_s": it_s, "fused_update": fused, "phase_ms": phases,
                  "d2d_env_steps_per_s_end_to_end": 4096 * world * args.episode_length / it_s}
     del env
     sweep = []
@@ -479,10 +534,11 @@ def configs_leg(args, rank, world, local):
                   periodic_devices=[], channel_switch=np.ones((N, 8)) * 0.8)
         env = CombinatorialEnv(**p5, n_envs=4096, device=dev, seed=22)
         env.shard(rank, world)
-        rate = _env_rate(env)
-        it_s, fused = _d2d_iteration(env, 5, combinatorial=True)
+        # comb B_as = 6D + 11C = 130 B at D = 7, C = 8 (fp32 obs rows)
+        rate, roof = _env_rate(env, bytes_per_agent_step=6 * 7 + 11 * 8)
+        it_s, fused, phases = _d2d_iteration(env, 5, combinatorial=True)
         sweep.append({"agents": N, "env_steps_per_s": rate * world, "agent_steps_per_s": rate * world * N,
-                      "d2d_iteration_s": it_s, "fused_update": fused})
+                      "env_kernel": roof, "d2d_iteration_s": it_s, "fused_update": fused, "phase_ms": phases})
         del env
         torch.cuda.empty_cache()
     out["c5"] = {"envs_per_gpu": 4096, "channels": 8, "sweep": sweep}
@@ -653,19 +709,23 @@ def gru_leg(args, rank, world, local):
     torch.cuda.synchronize()
     it_s = max_over_ranks(time.perf_counter() - t0, world)
     peak = 157.3
+    it_ = 1 if F + 1 <= 16 else 2 if F + 1 <= 32 else 3 if F + 1 <= 48 else 4
+    # the policy step runs bf16 MFMAs on exact splits (its fp32-equivalent rate is no roofline: the
+    # roofline figure is the executed MFMA pipe's busy fraction); the update's products are fp32 MFMAs
     out = {"config": f"xp_load.py learner: D2D-PPO, GRU H={H}, history_len={L}, {N} agents x 8 channels",
            "policy_slot": {"envs_per_gpu": E, "window": L,
-                           "kernel": "d2d::gru_policy_kernel<4, 2, 0, sample, split>",
+                           "kernel": f"d2d::gru_policy_kernel<4, {2 if it_ <= 2 else 4}, 0, 0, {'true' if it_ <= 2 else 'false'}>",
                            "ms": pol_ms, "agent_steps_per_s": E * world * N / (pol_ms / 1e3),
                            "env_steps_per_s": E * world / (pol_ms / 1e3),
                            "flop": pol_flop, "achieved_tflops_fp32_equiv": pol_flop / (pol_ms / 1e3) / 1e12,
-                           "peak_tflops_fp32_mfma": peak, "frac_of_fp32_peak": pol_flop / (pol_ms / 1e3) / 1e12 / peak,
-                           "mfma_pipe_busy_frac": pol_pipe, "bound": "mfma"},
+                           "mfma_pipe_busy_frac_static": pol_pipe, "mfma_pmc": pmc_mfma("d2d::gru_policy_kernel"),
+                           "bound": "mfma"},
            "update": {"envs_per_gpu": E2, "slots": ro.T, "agent_samples": samples,
-                      "kernel": "d2d::gru_grad_kernel<4, 2, 0>", "ms": grad_ms,
+                      "kernel": f"d2d::gru_grad_kernel<4, {it_}, 0, true>", "ms": grad_ms,
                       "agent_samples_per_s": samples * world / (grad_ms / 1e3), "flop": grad_flop,
                       "achieved_tflops": grad_flop / (grad_ms / 1e3) / 1e12, "peak_tflops_fp32_mfma": peak,
-                      "frac": grad_flop / (grad_ms / 1e3) / 1e12 / peak},
+                      "frac": grad_flop / (grad_ms / 1e3) / 1e12 / peak,
+                      "mfma_pmc": pmc_mfma("d2d::gru_grad_kernel")},
            "d2d_iteration_s": it_s, "d2d_iteration_envs_per_gpu": E2, "n_epoch": 5,
            "d2d_env_steps_per_s_end_to_end": E2 * world * ro.T / it_s,
            "flop_per_agent_step_cell": cell}
@@ -749,13 +809,16 @@ def main():
         bpas = RECORD_BYTES_PER_AGENT_STEP if mode == "record" else BYTES_PER_AGENT_STEP
         bytes_per_launch = bpas * N * E
         achieved = bytes_per_launch / (kern_avg_ms / 1e3) / 1e9
-        pmc = load_pmc_traffic(mode)
-        traffic = None
+        pmc, pmc_rel = load_pmc_traffic(mode)
+        traffic = src = None
+        # the committed PMC profile applies only to the very workload it measured
         if pmc and pmc.get("kernel_prefix") and pmc.get("envs") == E and pmc.get("agents") == N:
             traffic = pmc.get("bytes_per_launch")
+            src = {"file": pmc_rel, "commit": pmc.get("commit"), "rocprofv3": pmc.get("source"),
+                   "traffic_over_algorithmic": pmc.get("traffic_over_algorithmic")}
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "d2d::comb_kernel<uint8_t, 4, false, 8, false>", "kernel_avg_us": kern_avg_ms * 1e3,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+                "kernel": env_kernel_name(b.spec, mode == "record"), "kernel_avg_us": kern_avg_ms * 1e3,
                 "bytes_per_launch": bytes_per_launch, "bytes_per_agent_step": bpas}
         return total_envs * K / t, t, roof
 
@@ -796,8 +859,10 @@ def main():
             "dtype": "u8",
             "obs_format": modes[0],
             "data": "synthetic (Philox actions/channels/arrivals; reference channel_switch_8 tiled to 64 agents)",
-            "config": {"workload": "combinatorial_env 64 agents x 8 channels, 65536 envs per GPU (BASELINE.json "
-                                   "configs[2]); step = synthetic-action sampling + env-step kernel emitting "
+            "config": {"workload": f"combinatorial_env {N} agents x {C} channels, {E} envs per GPU"
+                                   + (" (BASELINE.json configs[2])" if (N, C, E) == (64, 8, 65536) else
+                                      " (NOT the BASELINE.json configs[2] batch)")
+                                   + "; step = synthetic-action sampling + env-step kernel emitting "
                                    + ("the compact obs record" if modes[0] == "record" else "fp32 obs rows"),
                        "agents": N, "channels": C, "envs_per_gpu": E, "global_envs": total_envs,
                        "episode_length": args.episode_length, "parallelism": f"dp{world} (env shards, no collective)"},

@@ -136,10 +136,11 @@ class BatchedLearnerBase(DataParallelMixin):
 
     def _gru_ok(self):
         """The GRU window-policy kernels (csrc/gru_kernels.hip) cover the RNN learners with H <= 64,
-        A <= 16 and F + 1 <= 32 (the update kernel's input tile; the reference's envs have F <= 30)."""
+        A <= 16 and F + 1 <= 64 inputs (up to four 16-column input tiles: xp_load's 30 inputs and
+        run_ippo_combinatorial.py's 6 x 16-channel env with 14 + 2 * 16 = 46)."""
         if getattr(self, "_gru", None) is None:
             p = self.policy
-            self._gru = (self.useRNN and p.kind == "rnn" and p.H <= 64 and p.A <= 16 and p.F + 1 <= 32
+            self._gru = (self.useRNN and p.kind == "rnn" and p.H <= 64 and p.A <= 16 and p.F + 1 <= 64
                          and (self.kind == "comb") == bool(self.combinatorial)
                          and os.environ.get("D2D_FUSED_POLICY", "1") != "0")
         return self._gru

@@ -1009,7 +1009,7 @@ template <int HT>
 static void launch_policy_it(const GruArgs& a, dim3 grid, hipStream_t s) {
   if (a.F + 1 <= 16) launch_policy_kind<HT, 1>(a, grid, s);
   else if (a.F + 1 <= 32) launch_policy_kind<HT, 2>(a, grid, s);
-  else launch_policy_kind<HT, 4>(a, grid, s);
+  else launch_policy_kind<HT, 4>(a, grid, s);  // (the swizzled fp32 images need 16 / 32 / 64 columns)
 }
 
 static int check_gru_desc(const d2d_gru_desc* d, const void* obs) {
@@ -1104,8 +1104,9 @@ static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, 
   w.partial = 0;
   w.hist = up(G * N * P);
   w.wimg = w.hist + up(waves * 2 * L * 64 * 4 * htp);  // per wave: the tile's h history + the padding table
-  // fp32 input images [N][3 HW][32] or the split ones [N][3 htp][1][3 parts][64] 16-byte words
-  w.hacc = w.wimg + up(N * std::max<int64_t>(3 * HW * 32, 3 * htp * 3 * 64 * 4));
+  // fp32 input images [N][3 HW][16 itp] or the split ones [N][3 htp][CI][3 parts][64] 16-byte words
+  const int64_t ci = (itp + 1) / 2;
+  w.hacc = w.wimg + up(N * std::max<int64_t>(3 * HW * 16 * itp, 3 * htp * ci * 3 * 64 * 4));
   w.himg = w.hacc + up(waves * 64 * (htp * htp * 4 + htp * 8 + 4));
   w.ghist = w.himg + up(N * (HW * HW + 16 * HW + HW + 16));
   w.gpart = w.ghist + up(waves * L * 5 * HW * 16);
@@ -1113,13 +1114,16 @@ static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, 
   return w;
 }
 
+// 16-column input tiles of the x operand (the inputs and the bias column F): F + 1 <= 64
+static int gru_input_tiles(int F) { return F + 1 <= 16 ? 1 : F + 1 <= 32 ? 2 : F + 1 <= 48 ? 3 : 4; }
+
 extern "C" int64_t d2d_gru_grad_workspace(const d2d_gru_desc* d, int32_t T) {
   if (!d || d->n_agents <= 0 || T <= 0 || d->n_envs <= 0 || d->hidden < 1 || d->history_len < 1) return 0;
   const int A = d->kind == 2 ? 1 : d->n_out, H = d->hidden, ht = H <= 16 ? 1 : H <= 32 ? 2 : 4;
   const int64_t tiles = (int64_t)T * ((d->n_envs + 15) / 16);
   const int G = gru_grad_blocks(d->n_agents, tiles);
   const GruOff o(H, d->obs_dim, A);
-  return gru_ws_layout(G, d->n_agents, o.P, d->history_len, ht, d->obs_dim + 1 <= 16 ? 1 : 2).total;
+  return gru_ws_layout(G, d->n_agents, o.P, d->history_len, ht, gru_input_tiles(d->obs_dim)).total;
 }
 
 #ifndef D2D_GRU_GRAD_SPLIT
@@ -1146,13 +1150,28 @@ __global__ void gru_wih_split_image_kernel(GruW w, int N, int H, int F, bf16x8* 
   const int k = (int)(idx / PER), rel = (int)(idx - (int64_t)k * PER);
   store_parts(img + (size_t)k * S::WIH + split_word(rel), split_frag<HT, IT>(w, k, H, F, true, rel));
 }
+template <int HT, int IT>
+static void launch_wih_split_it(const GruArgs& a, hipStream_t s) {
+  using S = GruSplit<HT, IT>;
+  const int64_t n = (int64_t)a.N * S::NT * S::CI * 64;
+  bf16x8* img = reinterpret_cast<bf16x8*>(a.wimg);
+  hipLaunchKernelGGL((gru_wih_split_image_kernel<HT, IT>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a.w, a.N,
+                     a.H, a.F, img);
+}
 template <int HT>
 static void launch_wih_split(const GruArgs& a, int itp, hipStream_t s) {
-  const int64_t n = (int64_t)a.N * 3 * HT * 64;  // CI = 1 for IT <= 2
-  const dim3 grid((unsigned)((n + 255) / 256));
-  bf16x8* img = reinterpret_cast<bf16x8*>(a.wimg);
-  if (itp == 1) hipLaunchKernelGGL((gru_wih_split_image_kernel<HT, 1>), grid, dim3(256), 0, s, a.w, a.N, a.H, a.F, img);
-  else hipLaunchKernelGGL((gru_wih_split_image_kernel<HT, 2>), grid, dim3(256), 0, s, a.w, a.N, a.H, a.F, img);
+  if (itp == 1) launch_wih_split_it<HT, 1>(a, s);
+  else if (itp == 2) launch_wih_split_it<HT, 2>(a, s);
+  else if (itp == 3) launch_wih_split_it<HT, 3>(a, s);
+  else launch_wih_split_it<HT, 4>(a, s);
+}
+
+template <int HT>
+static void launch_grad_it(const GruArgs& a, int itp, dim3 grid, hipStream_t s) {
+  if (itp == 1) launch_grad_kind<HT, 1>(a, grid, s);
+  else if (itp == 2) launch_grad_kind<HT, 2>(a, grid, s);
+  else if (itp == 3) launch_grad_kind<HT, 3>(a, grid, s);
+  else launch_grad_kind<HT, 4>(a, grid, s);
 }
 
 extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, const void* actions,
@@ -1162,7 +1181,6 @@ extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, c
                             float* g_b2, float* stats, float* workspace, int64_t workspace_floats, void* stream) {
   int rc = check_gru_desc(d, obs);
   if (rc) return rc;
-  if (d->obs_dim + 1 > 32) { d2d_set_error("d2d_gru_grad: obs_dim=%d > 31", d->obs_dim); return D2D_EUNSUPPORTED; }
   if (!obs || !weight || !weight_strides || !g_w_ih || !g_w_hh || !g_b_ih || !g_b_hh || !g_w1 || !g_b1 || !g_w2 ||
       !g_b2 || !workspace || (d->kind != 2 && (!actions || !logp_old || !logp_strides))) {
     d2d_set_error("d2d_gru_grad: NULL argument");
@@ -1188,7 +1206,7 @@ extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, c
   a.G = gru_grad_blocks(a.N, tiles);
   const GruOff o(a.H, a.F, a.A);
   a.P = o.P;
-  const int ht = (a.H + 15) / 16, htp = ht <= 1 ? 1 : ht <= 2 ? 2 : 4, itp = a.F + 1 <= 16 ? 1 : 2;
+  const int ht = (a.H + 15) / 16, htp = ht <= 1 ? 1 : ht <= 2 ? 2 : 4, itp = gru_input_tiles(a.F);
   const GruWs ws = gru_ws_layout(a.G, a.N, a.P, a.L, htp, itp);
   a.partial = workspace + ws.partial;
   a.hist = workspace + ws.hist;
@@ -1220,10 +1238,9 @@ extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, c
     a.G = 1;
   } else {
     dim3 grid(a.N, a.G);
-    const bool it1 = itp == 1;
-    if (ht <= 1) { if (it1) launch_grad_kind<1, 1>(a, grid, s); else launch_grad_kind<1, 2>(a, grid, s); }
-    else if (ht <= 2) { if (it1) launch_grad_kind<2, 1>(a, grid, s); else launch_grad_kind<2, 2>(a, grid, s); }
-    else { if (it1) launch_grad_kind<4, 1>(a, grid, s); else launch_grad_kind<4, 2>(a, grid, s); }
+    if (ht <= 1) launch_grad_it<1>(a, itp, grid, s);
+    else if (ht <= 2) launch_grad_it<2>(a, itp, grid, s);
+    else launch_grad_it<4>(a, itp, grid, s);
     D2D_CHECK_HIP(hipGetLastError());
   }
   const int64_t n = (int64_t)a.N * a.P;

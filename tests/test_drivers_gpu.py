@@ -123,6 +123,10 @@ def test_run_ippo_combinatorial_sequence(xp_dir):
                            channel_switch=np.array([0.8] * n_channels), verbose=False)
     ippo = iPPO(env, hidden_size=64, gamma=0.4, policy_lr=3e-4, value_lr=1e-3, device=None, useRNN=True,
                 save_path=None, combinatorial=True, history_len=10, early_stopping=False)
+    # 46 inputs (14 + 2 * 16): the GRU rollout / update kernels with three input tiles and the compact
+    # record (64-byte rows), not the torch fallback
+    assert env.observation_space[1].shape[0] == 46
+    assert ippo._gru_ok() and ippo._fused_update_ok() and ippo._record_ok()
     res = ippo.train(2, 2, 2, 100)   # positional: (num_iter, n_epoch, num_episodes, test_freq), ippo.py:406
     assert len(res[0]) == 4 and len(res[1]) == 2
     score, jains, ch, rew = ippo.test(4)

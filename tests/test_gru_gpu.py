@@ -83,6 +83,8 @@ CASES = [
     ("softmax", 2, 25, 64, 2, 3, 6, 12, 17),
     (None, 3, 30, 64, 1, 6, 10, 20, 37),
     (None, 2, 15, 16, 1, 5, 7, 14, 19),              # F + 1 = 16: one input tile
+    ("sigmoid", 3, 46, 64, 16, 6, 10, 20, 37),      # run_ippo_combinatorial.py: 6 x 16 channels, 46 inputs
+    (None, 2, 46, 64, 1, 6, 10, 20, 21),
 ]
 
 
@@ -186,6 +188,9 @@ GRAD_CASES = [
     ("softmax", 2, 15, 16, 4, 8, 6, 12, 16),         # L > episode
     (None, 3, 30, 64, 1, 5, 8, 16, 18),
     (None, 2, 12, 32, 1, 3, 6, 12, 21),
+    ("sigmoid", 2, 46, 64, 16, 6, 8, 16, 18),       # run_ippo_combinatorial.py's 46 inputs: three input tiles
+    (None, 2, 46, 64, 1, 6, 8, 16, 18),
+    ("softmax", 2, 60, 32, 5, 4, 8, 16, 17),        # four input tiles
 ]
 
 
@@ -392,6 +397,7 @@ def test_gru_grads_at_xp_load_window(kind):
     from torch.distributions import Bernoulli
     c = XP
     N, F, H, A, L, ep, T, E = (c[k] for k in ("N", "F", "H", "A", "L", "ep", "T", "E"))
+    A = 1 if kind is None else A  # the value network: Linear(H, 1) head (the RNN critic, ippo.py:146)
     p, dims = make_net(N, F, H, A, seed=31)
     dev = "cuda"
     obs = make_obs(T, E, N, F, dims, seed=32).to(dev)

@@ -13,9 +13,14 @@ replay) and must reproduce the reference's obs/states (exact), log-probs,
 values, advantages and returns (1e-5); the training iteration must reproduce
 the reference's per-epoch losses and the final weights of every agent and
 critic.  Tolerances: 1e-5 absolute for rollout quantities and losses
-(BASELINE.json north_star); final weights 1e-4 absolute (two Adam steps at
-lr 3e-3..1e-2 amplify last-bit gradient differences in near-zero
-components: |dw| <= 2*lr*|g_err|/sqrt(v)).
+(BASELINE.json north_star).  Final weights: 1e-5 absolute plus, per Adam step,
+Adam's own sensitivity to the gradient error the kernels are held to
+(2e-5 * max|g| of the tensor, tests/test_update_gpu.py, test_gru_gpu.py): Adam
+normalises every element by its own gradient history (its first step is
+lr * g / (|g| + eps), i.e. +-lr whatever |g| is), so an element whose gradient
+is within that error of zero moves by up to 2 lr on either sign, while one whose
+|g| is far above it moves exactly as the reference's does.  Per element and step
+the bound is 2 lr min(1, 2e-5 max|g| / |g|); see adam_tolerance().
 """
 import glob
 import json
@@ -58,6 +63,60 @@ def _sd(z, prefix):
         if k.startswith(prefix + "/"):
             out[k[len(prefix) + 1:]] = torch.from_numpy(z[k].copy())
     return out
+
+
+class GradRecorder:
+    """Snapshots the gradients every Adam step of a learner consumes (the .grad of the agent-stacked
+    parameters at each optimizer.step), to bound the final-weight comparison per element."""
+
+    def __init__(self, lr):
+        self.steps = []  # [(optimizer lr, {id(param): grad clone})]
+        for opt in [v for v in vars(lr).values() if isinstance(v, torch.optim.Optimizer)]:
+            self._wrap(opt)
+
+    def _wrap(self, opt):
+        step = opt.step
+
+        def rec(*a, **kw):
+            grads = {}
+            for grp in opt.param_groups:
+                for p in grp["params"]:
+                    if p.grad is not None:
+                        grads[p.untyped_storage().data_ptr()] = (p.grad.detach().clone(), p.storage_offset())
+            self.steps.append((opt.param_groups[0]["lr"], grads))
+            return step(*a, **kw)
+        opt.step = rec
+
+    def swing(self, view):
+        """Adam's largest possible total move of an element: 2 lr per step that updated it."""
+        key = view.untyped_storage().data_ptr()
+        return sum(2 * lr_ for lr_, grads in self.steps if key in grads)
+
+    def tolerance(self, view, rel_err=2e-5, base=1e-5):
+        """Per-element bound for a parameter view (an agent module's tensor inside a stacked one)."""
+        tol = torch.full(view.shape, base, dtype=torch.float64)
+        key = view.untyped_storage().data_ptr()
+        for lr_, grads in self.steps:
+            if key not in grads:
+                continue
+            g, off = grads[key]
+            gv = torch.as_strided(g, view.size(), view.stride(), view.storage_offset() - off).double().cpu()
+            err = rel_err * gv.abs().max().item()  # the agent's own tensor
+            # an exactly-zero gradient (an input column that is always 0, a hidden unit dead on every
+            # sample) is zero in any arithmetic: Adam leaves the element where it was, in both runs
+            tol += torch.where(gv == 0, torch.zeros_like(gv), 2 * lr_ * torch.clamp(err / gv.abs().clamp(min=1e-30), max=1.0))
+        return tol.numpy()
+
+
+def assert_weights_close(got, want, tol, msg, swing):
+    d = np.abs(got.astype(np.float64) - want)
+    bad = d > tol
+    assert not bad.any(), (f"{msg}: {int(bad.sum())} / {d.size} elements beyond the Adam-aware bound; "
+                           f"worst |d| {d[bad].max():.3g} at tol {tol[bad][np.argmax(d[bad])]:.3g}")
+    # the bound is tight (1e-5 + 4e-3 lr per step) for every element whose gradient is >= 1 % of its
+    # tensor's largest, and loosens only towards |g| -> 0 (sparse inputs, nearly dead units): the typical
+    # element must be held to a small part of Adam's full swing (2 lr per step), or the check is vacuous
+    assert np.median(tol) <= 0.05 * swing, f"{msg}: median bound {np.median(tol):.3g} vs swing {swing:.3g}"
 
 
 def build(z, n_envs=1):
@@ -117,11 +176,15 @@ def test_learner_matches_reference(name, E):
     if bool(z["useRNN"]):
         win = lr.preprocess_input_for_rnn(torch.from_numpy(z["ro/obs0"]).cuda()).cpu().numpy()
         assert np.array_equal(win, z["rnnwin/agent0"])
+        # every reference GRU shape (incl. hidden 64 / 16-step windows and the 46-input 6 x 16-channel
+        # env) rolls out and trains on the HIP GRU kernels, not the torch fallback
+        assert lr._gru_ok() and lr._fused_update_ok()
 
     # --- one training iteration on the same rollout
     lr._rollout = lambda num_episodes, teacher=None, _ro=ro: _ro
     lr.test = lambda num_episodes: (0.5, 1.0, 0, 0.0)
     np.random.seed(21)
+    rec = GradRecorder(lr)
     if algo == "ippo":
         res = lr.train(1, n_epoch=2, num_episodes=n_ep, test_freq=10 ** 9)
         np.testing.assert_allclose(res[2], z["train/policy_loss"], rtol=0, atol=1e-5)
@@ -130,17 +193,16 @@ def test_learner_matches_reference(name, E):
         res = lr.train(1, num_episodes=n_ep, n_epoch=2, test_freq=10 ** 9)
         np.testing.assert_allclose(np.array(res[2]), z["train/policy_loss"], rtol=0, atol=1e-5)
         np.testing.assert_allclose([float(v) for v in res[3]], z["train/value_loss"], rtol=0, atol=1e-5)
-    for i, ag in enumerate(lr.agents):
-        for k, v in ag.policy_network.state_dict().items():
-            np.testing.assert_allclose(v.cpu().numpy(), z[f"final/agent{i}/policy/{k}"], rtol=0, atol=1e-4,
-                                       err_msg=f"agent {i} policy {k}")
-        if algo == "ippo":
-            for k, v in ag.value_network.state_dict().items():
-                np.testing.assert_allclose(v.cpu().numpy(), z[f"final/agent{i}/value/{k}"], rtol=0, atol=1e-4,
-                                           err_msg=f"agent {i} value {k}")
-    if algo == "d2d":
-        for k, v in lr.value_network.state_dict().items():
-            np.testing.assert_allclose(v.cpu().numpy(), z[f"final/critic/{k}"], rtol=0, atol=1e-4, err_msg=k)
+    assert rec.steps, "no optimizer step recorded"
+    nets = [(f"agent {i} policy", f"final/agent{i}/policy", ag.policy_network) for i, ag in enumerate(lr.agents)]
+    if algo == "ippo":
+        nets += [(f"agent {i} value", f"final/agent{i}/value", ag.value_network) for i, ag in enumerate(lr.agents)]
+    else:
+        nets.append(("critic", "final/critic", lr.value_network))
+    for msg, pre, net in nets:
+        for k, v in net.named_parameters():
+            assert_weights_close(v.detach().cpu().numpy(), z[f"{pre}/{k}"], rec.tolerance(v.detach()), f"{msg} {k}",
+                                 rec.swing(v.detach()))
 
 
 def evaltest_names():
