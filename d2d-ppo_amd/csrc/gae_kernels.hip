@@ -241,8 +241,15 @@ __global__ __launch_bounds__(256) void gae_moments_reduce_kernel(int nb, int col
   }
 }
 
-// x_k = gate_k ? (x_k - mean_k) * scale_k : x_k for both outputs in one pass (x1 may be null)
-__global__ __launch_bounds__(256) void normalize_pair_kernel(int64_t n4, int64_t n, int cols, int inner,
+// x_k = gate_k ? (x_k - mean_k) * scale_k : x_k for both outputs in one pass (x1 may be null).
+// No integer division per element (a 64-bit divide is a ~100-instruction software sequence):
+//   [T][cols][E] (TCE): block (bx, row = t * cols + c) streams float4s of one row -- the column and its
+//                       mean / scale are wave-uniform scalars, loaded once per block;
+//   [T][E][cols]:       flat float4 stream, column of element j = j mod cols in 32-bit arithmetic.
+__device__ __forceinline__ float nrm(float v, double m, double sc) { return (float)(((double)v - m) * sc); }
+
+template <bool TCE>
+__global__ __launch_bounds__(256) void normalize_pair_kernel(int64_t n, int rows, int E, int cols,
                                                              float* __restrict__ x0, const double* __restrict__ mean0,
                                                              const double* __restrict__ scale0,
                                                              const int32_t* __restrict__ gate0, float* __restrict__ x1,
@@ -251,43 +258,69 @@ __global__ __launch_bounds__(256) void normalize_pair_kernel(int64_t n4, int64_t
                                                              const int32_t* __restrict__ gate1) {
   const bool g0 = x0 && *gate0, g1 = x1 && *gate1;
   if (!g0 && !g1) return;
-  auto col = [&](int64_t j) { return inner > 0 ? (int)((j / inner) % cols) : (int)(j % cols); };
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
-    const int64_t j = q << 2;
-    int cc[4];
-    if (inner > 0 && (inner & 3) == 0) {  // [T][cols][E], E % 4 == 0: one column per float4
-      cc[0] = cc[1] = cc[2] = cc[3] = col(j);
-    } else if (inner > 0) {
+  if constexpr (TCE) {
+    for (int row = blockIdx.y; row < rows; row += gridDim.y) {
+      const int c = row % cols;
+      const double m0 = g0 ? mean0[c] : 0.0, s0 = g0 ? scale0[c] : 1.0;
+      const double m1 = g1 ? mean1[c] : 0.0, s1 = g1 ? scale1[c] : 1.0;
+      const int64_t base = (int64_t)row * E;
+      if ((E & 3) == 0) {  // rows of whole float4s (16-byte aligned: x 16-byte aligned, E % 4 == 0)
+        const int E4 = E >> 2;
+        for (int q = blockIdx.x * 256 + threadIdx.x; q < E4; q += gridDim.x * 256) {
+          if (g0) {
+            float4* p = reinterpret_cast<float4*>(x0 + base) + q;
+            float4 v = *p;
+            v = make_float4(nrm(v.x, m0, s0), nrm(v.y, m0, s0), nrm(v.z, m0, s0), nrm(v.w, m0, s0));
+            *p = v;
+          }
+          if (g1) {
+            float4* p = reinterpret_cast<float4*>(x1 + base) + q;
+            float4 v = *p;
+            v = make_float4(nrm(v.x, m1, s1), nrm(v.y, m1, s1), nrm(v.z, m1, s1), nrm(v.w, m1, s1));
+            *p = v;
+          }
+        }
+      } else {
+        for (int e = blockIdx.x * 256 + threadIdx.x; e < E; e += gridDim.x * 256) {
+          if (g0) x0[base + e] = nrm(x0[base + e], m0, s0);
+          if (g1) x1[base + e] = nrm(x1[base + e], m1, s1);
+        }
+      }
+    }
+  } else {
+    const int64_t n4 = n >> 2;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const bool small = n < ((int64_t)1 << 31);
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
+      const int64_t j = q << 2;
+      const int c0 = cols == 1 ? 0 : small ? (int)((uint32_t)j % (uint32_t)cols) : (int)(j % cols);
+      int cc[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) cc[u] = col(j + u);
-    } else {  // [T][E][cols]: consecutive columns, wrapping
-      const int c0 = col(j);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) cc[u] = (c0 + u) % cols;
+      for (int u = 0; u < 4; ++u) {
+        const int cu = c0 + u;
+        cc[u] = cols == 1 ? 0 : cu < cols ? cu : cu % cols;
+      }
+      if (g0) {
+        float4* p = reinterpret_cast<float4*>(x0) + q;
+        float4 v = *p;
+        v = make_float4(nrm(v.x, mean0[cc[0]], scale0[cc[0]]), nrm(v.y, mean0[cc[1]], scale0[cc[1]]),
+                        nrm(v.z, mean0[cc[2]], scale0[cc[2]]), nrm(v.w, mean0[cc[3]], scale0[cc[3]]));
+        *p = v;
+      }
+      if (g1) {
+        float4* p = reinterpret_cast<float4*>(x1) + q;
+        float4 v = *p;
+        v = make_float4(nrm(v.x, mean1[cc[0]], scale1[cc[0]]), nrm(v.y, mean1[cc[1]], scale1[cc[1]]),
+                        nrm(v.z, mean1[cc[2]], scale1[cc[2]]), nrm(v.w, mean1[cc[3]], scale1[cc[3]]));
+        *p = v;
+      }
     }
-    if (g0) {
-      float4 v = reinterpret_cast<float4*>(x0)[q];
-      v.x = (float)(((double)v.x - mean0[cc[0]]) * scale0[cc[0]]);
-      v.y = (float)(((double)v.y - mean0[cc[1]]) * scale0[cc[1]]);
-      v.z = (float)(((double)v.z - mean0[cc[2]]) * scale0[cc[2]]);
-      v.w = (float)(((double)v.w - mean0[cc[3]]) * scale0[cc[3]]);
-      reinterpret_cast<float4*>(x0)[q] = v;
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {  // tail
+      const int64_t j = (n4 << 2) + threadIdx.x;
+      const int c = (int)(j % cols);
+      if (g0) x0[j] = nrm(x0[j], mean0[c], scale0[c]);
+      if (g1) x1[j] = nrm(x1[j], mean1[c], scale1[c]);
     }
-    if (g1) {
-      float4 v = reinterpret_cast<float4*>(x1)[q];
-      v.x = (float)(((double)v.x - mean1[cc[0]]) * scale1[cc[0]]);
-      v.y = (float)(((double)v.y - mean1[cc[1]]) * scale1[cc[1]]);
-      v.z = (float)(((double)v.z - mean1[cc[2]]) * scale1[cc[2]]);
-      v.w = (float)(((double)v.w - mean1[cc[3]]) * scale1[cc[3]]);
-      reinterpret_cast<float4*>(x1)[q] = v;
-    }
-  }
-  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {  // tail
-    const int64_t j = (n4 << 2) + threadIdx.x;
-    const int c = col(j);
-    if (g0) x0[j] = (float)(((double)x0[j] - mean0[c]) * scale0[c]);
-    if (g1) x1[j] = (float)(((double)x1[j] - mean1[c]) * scale1[c]);
   }
 }
 
@@ -503,11 +536,22 @@ extern "C" int d2d_normalize_pair(int32_t T, int32_t E, int32_t cols, int32_t la
   }
   const int64_t n = (int64_t)T * E * cols;
   if (n == 0) return D2D_OK;
-  const int64_t n4 = n >> 2;
-  int64_t grid = (n4 + 255) / 256;
-  grid = grid < 1 ? 1 : grid > 16384 ? 16384 : grid;
-  hipLaunchKernelGGL(normalize_pair_kernel, dim3((unsigned)grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     n4, n, cols, layout ? E : 0, x0, mean0, scale0, gate0, x1, mean1, scale1, gate1);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (layout) {
+    // a block streams 4 float4s per lane of one row; rows beyond gridDim.y loop
+    const int64_t rows = (int64_t)T * cols;
+    if (rows > 0x7FFFFFFF) { d2d_set_error("d2d_normalize_pair: T * cols too large"); return D2D_EINVAL; }
+    const int per = (E & 3) == 0 ? 4 * 256 * 4 : 256 * 4;
+    const unsigned gx = (unsigned)((E + per - 1) / per);
+    const unsigned gy = (unsigned)(rows < 65535 ? rows : 65535);
+    hipLaunchKernelGGL(normalize_pair_kernel<true>, dim3(gx, gy), dim3(256), 0, s, n, (int)rows, E, cols, x0, mean0,
+                       scale0, gate0, x1, mean1, scale1, gate1);
+  } else {
+    int64_t grid = ((n >> 2) + 255) / 256;
+    grid = grid < 1 ? 1 : grid > 16384 ? 16384 : grid;
+    hipLaunchKernelGGL(normalize_pair_kernel<false>, dim3((unsigned)grid), dim3(256), 0, s, n, 0, E, cols, x0, mean0,
+                       scale0, gate0, x1, mean1, scale1, gate1);
+  }
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
 }

@@ -57,6 +57,9 @@
 // instead of dHv (32), the relu' select and the dv * v2 products go, and v2 scales the sums once
 #define D2D_CRITIC_MASK 1
 #endif
+#ifndef D2D_UPD_WAVES
+#define D2D_UPD_WAVES 2  // waves per SIMD the update kernels are register-budgeted for (KC = 1)
+#endif
 #ifndef D2D_LOGITS_BF16
 // logits Z^T = W2 . relu(HT) on bf16 MFMAs: W2's three-way split against a two-way RNE split of
 // relu(HT) (<= 2^-17 relative per product), 3 x 16 instead of 4 x 32 MFMA cycles per hidden tile
@@ -162,6 +165,36 @@ __device__ __forceinline__ float ld_sample(const __amdgpu_buffer_rsrc_t& r, cons
   return uf(__builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)(d * (int)st[1]) * 4u, 0, 0));
 }
 
+// (slot t, first env e0) of a sample tile; a wave's tiles advance by a fixed stride, so the cursor
+// moves without the per-tile scalar division tile / tiles_per_t (a ~20-instruction sequence, twice
+// per tile: the look-ahead load and the staging)
+struct TileCur {
+  int tile, t, e0;
+};
+__device__ __forceinline__ TileCur tile_at(const UpdArgs& a, int tile) {
+  const int t = tile / a.tiles_per_t;
+  return TileCur{tile, t, (tile - t * a.tiles_per_t) * 32};
+}
+struct TileStride {
+  int tiles, dt, de, row;  // stride in tiles = dt * tiles_per_t + de / 32; row = 32 * tiles_per_t
+  __device__ __forceinline__ TileStride(const UpdArgs& a, int stride) {
+    tiles = stride;
+    dt = stride / a.tiles_per_t;
+    de = (stride - dt * a.tiles_per_t) * 32;
+    row = 32 * a.tiles_per_t;
+  }
+  __device__ __forceinline__ TileCur next(TileCur c) const {
+    c.tile += tiles;
+    c.t += dt;
+    c.e0 += de;
+    if (c.e0 >= row) {
+      c.e0 -= row;
+      c.t += 1;
+    }
+    return c;
+  }
+};
+
 // Per-tile inputs of the actor kernel, loaded one tile ahead (registers): the obs rows of the
 // 32 samples (lane (g, i) of half s: x[sample 16s + i][32c + 8g + j], raw -- columns past F and
 // samples past E are fixed up by stage_tile) and the per-sample action / logp_old / weight of
@@ -220,10 +253,9 @@ __device__ __forceinline__ void record_signs(uint32_t (&sm)[KC][2], const UpdArg
 }
 
 template <int KC, bool PAIR, bool U8>
-__device__ __forceinline__ void load_actor_in(ActorIn<KC, PAIR, U8>& in, const UpdArgs& a, int tile, int k, int g,
+__device__ __forceinline__ void load_actor_in(ActorIn<KC, PAIR, U8>& in, const UpdArgs& a, TileCur c, int k, int g,
                                               int i) {
-  const int t = tile / a.tiles_per_t;
-  const int e0 = (tile - t * a.tiles_per_t) * 32;
+  const int t = c.t, e0 = c.e0;
   load_rows<KC, U8>(in.x, a, t, e0, k, g, i);
   const __amdgpu_buffer_rsrc_t rl = sample_rsrc(a.logp_old, a.lo_st, a.lo_ext, t, e0, k);
   const __amdgpu_buffer_rsrc_t rw = sample_rsrc(a.weight, a.w_st, a.w_ext, t, e0, k);
@@ -283,7 +315,7 @@ __device__ __forceinline__ void lds_row(float (&v)[8], const float (*xw)[XS], in
 // v_mfma_f32_16x16x4_f32 (an exact fmaf chain) straight from the accumulator registers; the
 // weight gradients dW1, dW2 on two-way RNE splits of their per-tile operands.
 template <int KC, int HT, int KIND, bool PAIR, bool U8, int AFIX = 0>
-__global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(UpdArgs a) {
+__global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_grad_kernel(UpdArgs a) {
   constexpr int QT = 2 * KC;  // input tiles of 16 in dW1
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, i = lane & 15;
@@ -398,9 +430,8 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
   record_signs<KC, U8>(sm, a, k, g);
   // ---- inputs: bias column, zeros past it; bf16 high parts; the tile to LDS for dW1.
   // Returns whether every input of the tile is bf16-exact (wave-uniform).
-  auto stage = [&](const ActorIn<KC, PAIR, U8>& src, int tile) -> bool {
-    const int t = tile / a.tiles_per_t;
-    e0 = (tile - t * a.tiles_per_t) * 32;
+  auto stage = [&](const ActorIn<KC, PAIR, U8>& src, TileCur c) -> bool {
+    e0 = c.e0;
 #pragma unroll
     for (int s = 0; s < (PAIR ? 1 : 2); ++s) {
       cur.act[s] = src.act[s];
@@ -658,20 +689,24 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_actor_grad_kernel(Up
     // carries the other's live ranges or branches.
     ActorIn<KC, PAIR, U8> in;
     bool deferred = false;
-    if (tile0 < a.n_tiles) load_actor_in<KC, PAIR, U8>(in, a, tile0, k, g, i);
-    for (int tile = tile0; tile < a.n_tiles; tile += stride) {
-      const bool x_exact = stage(in, tile);
-      if (tile + stride < a.n_tiles) load_actor_in<KC, PAIR, U8>(in, a, tile + stride, k, g, i);
+    const TileStride ts(a, stride);
+    TileCur cur_t = tile_at(a, tile0);
+    if (tile0 < a.n_tiles) load_actor_in<KC, PAIR, U8>(in, a, cur_t, k, g, i);
+    while (cur_t.tile < a.n_tiles) {
+      const bool x_exact = stage(in, cur_t);
+      const TileCur nxt = ts.next(cur_t);
+      if (nxt.tile < a.n_tiles) load_actor_in<KC, PAIR, U8>(in, a, nxt, k, g, i);
       if (x_exact)
         body(std::true_type{});
       else
         deferred = true;
       lds_order();
+      cur_t = nxt;
     }
     if (deferred) {
-      for (int tile = tile0; tile < a.n_tiles; tile += stride) {
-        load_actor_in<KC, PAIR, U8>(in, a, tile, k, g, i);
-        if (!stage(in, tile)) body(std::false_type{});
+      for (TileCur c = tile_at(a, tile0); c.tile < a.n_tiles; c = ts.next(c)) {
+        load_actor_in<KC, PAIR, U8>(in, a, c, k, g, i);
+        if (!stage(in, c)) body(std::false_type{});
         lds_order();
       }
     }
@@ -750,9 +785,8 @@ struct CriticIn {
 };
 
 template <int KC, bool U8>
-__device__ __forceinline__ void load_critic_in(CriticIn<KC, U8>& in, const UpdArgs& a, int tile, int k, int g, int i) {
-  const int t = tile / a.tiles_per_t;
-  const int e0 = (tile - t * a.tiles_per_t) * 32;
+__device__ __forceinline__ void load_critic_in(CriticIn<KC, U8>& in, const UpdArgs& a, TileCur c, int k, int g, int i) {
+  const int t = c.t, e0 = c.e0;
   load_rows<KC, U8>(in.x, a, t, e0, k, g, i);
   const __amdgpu_buffer_rsrc_t rw = sample_rsrc(a.weight, a.w_st, a.w_ext, t, e0, k);
 #pragma unroll
@@ -762,7 +796,7 @@ __device__ __forceinline__ void load_critic_in(CriticIn<KC, U8>& in, const UpdAr
 }
 
 template <int KC, int HT, bool U8>
-__global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(UpdArgs a) {
+__global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_critic_grad_kernel(UpdArgs a) {
   constexpr int QT = 2 * KC;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, i = lane & 15;
@@ -816,9 +850,8 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
   bf16x8 xh[2][KC];
   uint32_t sm[KC][2];
   record_signs<KC, U8>(sm, a, k, g);
-  auto stage = [&](const CriticIn<KC, U8>& src, int tile) -> bool {
-    const int t = tile / a.tiles_per_t;
-    e0 = (tile - t * a.tiles_per_t) * 32;
+  auto stage = [&](const CriticIn<KC, U8>& src, TileCur c) -> bool {
+    e0 = c.e0;
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -973,21 +1006,25 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void ppo_critic_grad_kernel(U
     };
     CriticIn<KC, U8> in;
     bool deferred = false;
-    if (tile0 < a.n_tiles) load_critic_in<KC, U8>(in, a, tile0, k, g, i);
-    for (int tile = tile0; tile < a.n_tiles; tile += stride) {
-      const bool x_exact = stage(in, tile);
-      if (tile + stride < a.n_tiles) load_critic_in<KC, U8>(in, a, tile + stride, k, g, i);
+    const TileStride ts(a, stride);
+    TileCur cur_t = tile_at(a, tile0);
+    if (tile0 < a.n_tiles) load_critic_in<KC, U8>(in, a, cur_t, k, g, i);
+    while (cur_t.tile < a.n_tiles) {
+      const bool x_exact = stage(in, cur_t);
+      const TileCur nxt = ts.next(cur_t);
+      if (nxt.tile < a.n_tiles) load_critic_in<KC, U8>(in, a, nxt, k, g, i);
       lds_order();
       if (x_exact)
         body(std::true_type{});
       else
         deferred = true;
       lds_order();
+      cur_t = nxt;
     }
     if (deferred) {
-      for (int tile = tile0; tile < a.n_tiles; tile += stride) {
-        load_critic_in<KC, U8>(in, a, tile, k, g, i);
-        const bool x_exact = stage(in, tile);
+      for (TileCur c = tile_at(a, tile0); c.tile < a.n_tiles; c = ts.next(c)) {
+        load_critic_in<KC, U8>(in, a, c, k, g, i);
+        const bool x_exact = stage(in, c);
         lds_order();
         if (!x_exact) body(std::false_type{});
         lds_order();

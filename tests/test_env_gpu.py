@@ -267,6 +267,35 @@ def test_full_size_bit_exact_slots():
     assert np.array_equal(b.channels_host(), c.chan)
 
 
+def test_full_size_record_slots_bit_exact():
+    """The headline instantiation itself (the bench's `value`): 64 agents x 8 channels x 65,536 envs
+    emitting the compact obs record (256-lane record-only blocks, comb_kernel<u8, 4, false, 8, false>
+    in record mode).  Over 6 slots incl. the reset, the decoded record equals the C oracle's fp32 obs
+    bit for bit, and rewards / buffers / channels match."""
+    from oracle.c_oracle import COracle
+    params = _config3_params()
+    E = 65536
+    env = make_env("comb", params, n_envs=E, device="cuda", seed=43)
+    b = env.batch()
+    c = COracle("comb", params, n_envs=E, seed=43, nthreads=16)
+    rec = b.record
+    b.reset(want_obs=True, out_obs=rec)
+    rc = c.reset(rng_step=0, want_state=False)
+    assert np.array_equal(rec.decode().cpu().numpy(), rc["obs"])
+    rew = torch.empty((E,), dtype=torch.int32, device=b.device)
+    for t in range(6):
+        rs = b.rng_step
+        a = b.sample_actions(0.1)
+        ac = c.sample_actions(rs, p=0.1)
+        rs = b.rng_step
+        b.step(a, want_obs=True, out_obs=rec, out_reward=rew)
+        oc = c.step(ac, rng_step=rs, want_state=False)
+        assert np.array_equal(rec.decode().cpu().numpy(), oc["obs"]), t
+        assert np.array_equal(rew.cpu().numpy(), oc["reward"]), t
+    assert np.array_equal(b.buffers_host(), c.buf)
+    assert np.array_equal(b.channels_host(), c.chan)
+
+
 def test_full_size_episode_invariants():
     """Whole episode at 64 x 8 x 65536: packet conservation, reward bounds, ACK alphabet."""
     params = _config3_params()

@@ -27,6 +27,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 E, N, C, L = 96, 8, 8, 20
+ALGOS = ("ippo", "d2d", "ippo_gru", "d2d_gru")
 OUT = os.path.join(ROOT, "gpurun_out", "dp")
 
 
@@ -45,11 +46,13 @@ def run(algo, n_envs):
     env = make_env(n_envs)
     kw = dict(hidden_size=64, gamma=0.6, policy_lr=3e-3, value_lr=1e-3, device="cuda:0", combinatorial=True,
               early_stopping=False)
-    lr = iPPO(env, **kw) if algo == "ippo" else D2DPPO(env, beta_entropy=0.02, **kw)
+    if algo.endswith("_gru"):  # the GRU window kernels (xp_load.py's learner shape, short window)
+        kw.update(useRNN=True, history_len=4)
+    lr = iPPO(env, **kw) if algo.startswith("ippo") else D2DPPO(env, beta_entropy=0.02, **kw)
     assert lr._fused_update_ok()
     ro = lr._rollout(n_envs)
     out = {"obs": ro.obs_f32, "actions": ro.actions, "logp": ro.logp}
-    if algo == "ippo":
+    if algo.startswith("ippo"):
         out["adv"], out["ret"] = ro.adv_tne, ro.ret_tne
     else:
         out["ret_mean"] = ro.ret_mean.view(n_envs, L)
@@ -59,7 +62,7 @@ def run(algo, n_envs):
     for k, p in params.items():
         out[f"grad/{k}"] = p.grad
         out[f"w/{k}"] = p.data
-    if algo == "d2d":
+    if algo.startswith("d2d"):
         for k, p in lr.value_network.named_parameters():
             out[f"cgrad/{k}"] = p.grad
     return {k: v.detach().cpu().clone() for k, v in out.items()}
@@ -71,14 +74,14 @@ def main():
     torch.cuda.set_device(0)
     os.makedirs(OUT, exist_ok=True)
     dist.init_process_group("gloo")
-    for algo in ("ippo", "d2d"):
+    for algo in ALGOS:
         torch.save(run(algo, E), os.path.join(OUT, f"{algo}_rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
     if rank != 0:
         return 0
     rep, bad = {}, []
-    for algo in ("ippo", "d2d"):
+    for algo in ALGOS:
         full = run(algo, E * ws)
         shards = [torch.load(os.path.join(OUT, f"{algo}_rank{r}.pt")) for r in range(ws)]
         d = {}

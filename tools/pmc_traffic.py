@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--agents", type=int, default=64)
     ap.add_argument("--algorithmic-bytes", type=float, default=172.0 * 64 * 65536)
+    ap.add_argument("--commit", default=None, help="the commit the profiled tree was built from")
     a = ap.parse_args()
     f = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
     w = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
@@ -52,7 +53,8 @@ def main():
            "bytes_per_launch": read_b + write_b,
            "bytes_per_launch_raw": (fk + wk) * 1024,
            "algorithmic_bytes_per_launch": a.algorithmic_bytes,
-           "traffic_over_algorithmic": (read_b + write_b) / a.algorithmic_bytes}
+           "traffic_over_algorithmic": (read_b + write_b) / a.algorithmic_bytes,
+           "commit": a.commit, "source": {"fetch": a.fetch, "write": a.write}}
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out))
 
