@@ -750,7 +750,7 @@ def main():
     ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
     ap.add_argument("--ppo-epochs", type=int, default=6)
     ap.add_argument("--train-epochs", type=int, default=4, help="n_epoch of the train leg")
-    ap.add_argument("--action-ring", type=int, default=8, help="distinct pre-generated synthetic action slots")
+    ap.add_argument("--action-ring", type=int, default=2, help="distinct pre-generated synthetic action slots")
     ap.add_argument("--env-mode", default="both", choices=["both", "record", "fp32"],
                     help="obs output of the headline env steps (value = the first of record, fp32)")
     args = ap.parse_args()

@@ -44,7 +44,31 @@
 #define D2D_GRU_DW_BF16 1
 #endif
 
+#ifndef D2D_GRU_DH_BF16
+// 1: the BPTT's dh_{j-1} = W_hh^T dg on v_mfma_f32_16x16x32_bf16: the transposed W_hh image holds a
+// two-way RNE bf16 split [W_h(4 rows) | W_m(4 rows)] per (unit, gate tile, lane group) -- 16 bytes, the
+// same LDS as the fp32 image -- and dg is split two ways per step, so one A fragment serves two MFMAs
+// (B = [g_h | g_h] and [g_m | g_m]: W_h g_h + W_m g_h + W_h g_m + W_m g_m, ~2^-16 relative per product).
+// 96 bf16 MFMAs of 16 cycles per step instead of 192 fp32 v_mfma_f32_16x16x4_f32 of 32.
+// 0: the fp32 MFMAs on the fp32 transposed image (exact products).
+#define D2D_GRU_DH_BF16 1
+#endif
+
 namespace d2d {
+
+// RNE bf16 pair (lo = a, hi = b) and the residual pair, as two dwords each (the dh GEMM's B operands)
+__device__ __forceinline__ uint32_t rne_pair(float a, float b) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  const bf2 v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ void split2_pairs(const float (&v)[4], uint32_t (&h)[2], uint32_t (&m)[2]) {
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    h[p] = rne_pair(v[2 * p], v[2 * p + 1]);
+    m[p] = rne_pair(v[2 * p] - __uint_as_float(h[p] << 16), v[2 * p + 1] - __uint_as_float(h[p] & 0xFFFF0000u));
+  }
+}
 
 // Two-way RNE bf16 split of 4 fp32 values as one dword per value, (RNE(v), RNE(v - RNE(v))): the A
 // fragment [h0 m0 h1 m1 h2 m2 h3 m3] of k-slots (value q, part p) = 2q + p
@@ -347,14 +371,34 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H, F = a.F, N = a.N, E = a.E, A = KIND == kGruValue ? 1 : a.A, L = a.L;
   float* sc = scr[wave];
+  // DH_BF16: the transposed image as 16-byte entries [unit u][gate tile T * 4 + lane group][W_h x4 | W_m x4],
+  // TE entries per unit row (one of padding: the 16 lanes' A-fragment reads hit distinct banks)
+  constexpr int TE = 3 * HT * 4 + 1;
+  static_assert(HW * TE * 16 <= HW * RT * 4, "bf16 transposed image exceeds the fp32 one");
   {
     const float* Whh = a.w.w_hh + (size_t)k * 3 * H * H;
     for (int idx = tid; idx < R3 * HW; idx += blockDim.x) {
       const int R = idx / HW, c = idx - R * HW, G = R / HW, u = R - G * HW;
       const float v = (u < H && c < H) ? Whh[(size_t)(G * H + u) * H + c] : 0.f;
       if constexpr (!SPLIT) whh_s[swz<HW>(R, c)] = v;
-      whhT_s[c * RT + R] = v;
+      if (!D2D_GRU_DH_BF16) whhT_s[c * RT + R] = v;
     }
+#if D2D_GRU_DH_BF16
+    bf16x8* whhTb = reinterpret_cast<bf16x8*>(whhT_s);
+    for (int idx = tid; idx < HW * 3 * HT * 4; idx += blockDim.x) {
+      const int c = idx / (3 * HT * 4), rem = idx - c * (3 * HT * 4), T = rem >> 2, gg = rem & 3;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int R = 16 * T + 4 * gg + r, G = R / HW, u = R - G * HW;
+        v[r] = (u < H && c < H) ? Whh[(size_t)(G * H + u) * H + c] : 0.f;
+      }
+      uint32_t hw[2], mw[2];
+      split2_pairs(v, hw, mw);
+      const u32x4v e = {hw[0], hw[1], mw[0], mw[1]};
+      whhTb[c * TE + T * 4 + gg] = __builtin_bit_cast(bf16x8, e);
+    }
+#endif
     if constexpr (SPLIT) load_gru_split_images<HT, IT>(nullptr, whh_b, a.w, k, H, F, tid, blockDim.x);
   }
   f32x4 bhn[HT];
@@ -643,13 +687,36 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       stage_rows(hp, nullptr, 4 * HW);
 #endif
       __builtin_amdgcn_sched_barrier(0);
-      // dh_{j-1} = g z + W_hh^T dgh: A fragments from the transposed image, 4 k-steps per ds_read_b128
+      // dh_{j-1} = g z + W_hh^T dgh: A fragments from the transposed image
       const float* wt = whhT_s + z;
+#if D2D_GRU_DH_BF16 && D2D_GRU_ABLATE != 2
+      // dg split two ways once per step: B1 = [g_h | g_h], B2 = [g_m | g_m] per gate tile (rows 16T + 4g + r)
+      bf16x8 gb1[3 * HT], gb2[3 * HT];
+#pragma unroll
+      for (int T = 0; T < 3 * HT; ++T) {
+        float v[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) v[s4] = T < HT ? drp[T][s4] : T < 2 * HT ? dzp[T - HT][s4] : dghn[T - 2 * HT][s4];
+        uint32_t hw[2], mw[2];
+        split2_pairs(v, hw, mw);
+        const u32x4v b1 = {hw[0], hw[1], hw[0], hw[1]}, b2 = {mw[0], mw[1], mw[0], mw[1]};
+        gb1[T] = __builtin_bit_cast(bf16x8, b1);
+        gb2[T] = __builtin_bit_cast(bf16x8, b2);
+      }
+      const bf16x8* wtb = reinterpret_cast<const bf16x8*>(wt);
+#endif
 #pragma unroll
       for (int t = 0; t < HT; ++t) {
         f32x4 dh = {gz[t][0], gz[t][1], gz[t][2], gz[t][3]};
 #if D2D_GRU_ABLATE == 2
         dh += f32x4{drp[t][0], dzp[t][1], dghn[t][2], wt[lane]};
+#elif D2D_GRU_DH_BF16
+#pragma unroll
+        for (int T = 0; T < 3 * HT; ++T) {
+          const bf16x8 af = wtb[(16 * t + i) * TE + T * 4 + g];
+          dh = mfma_bf16(af, gb1[T], dh);
+          dh = mfma_bf16(af, gb2[T], dh);
+        }
 #else
 #pragma unroll
         for (int T = 0; T < 3 * HT; ++T) {
