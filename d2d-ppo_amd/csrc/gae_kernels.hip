@@ -111,14 +111,30 @@ struct SeqMom {
   }
 };
 
-template <int TCE>
+//
+// MODE (ABI 9): 0 = write adv / ret and accumulate the moments; 1 = moments only (no writes: the first
+// of two scans when the outputs are normalised); 2 = write the NORMALISED outputs, no moments (the
+// second scan, after the statistics of the first have been finalised and, across ranks, all-reduced).
+// Recomputing the recursion costs a few f64 FMAs per element; it saves the separate normalisation
+// pass (8 B read + 8 B written per element) and the first pass's 8 B of writes: 16 B per element over
+// the two scans instead of 28 B for scan + normalise.  The recursion, the fp32 roundings and the
+// normalisation expression (nrm) are those of the scan and of normalize_pair_kernel, so every output
+// is bitwise the same as scan + normalise.
+struct NormArgs {
+  const double *mean0, *scale0, *mean1, *scale1;  // adv (0) and ret (1); NULL mean = written raw
+  const int32_t *gate0, *gate1;
+};
+__device__ __forceinline__ float nrm(float v, double m, double sc) { return (float)(((double)v - m) * sc); }
+
+template <int TCE, int MODE>
 __global__ __launch_bounds__(256) void gae_scan_moments_kernel(int T, int E, int cols, int rcols, int ct,
                                                                const float* __restrict__ rew,
                                                                const float* __restrict__ val,
                                                                const uint8_t* __restrict__ done, double gamma,
                                                                double lam, int last_shard, float* __restrict__ adv,
-                                                               float* __restrict__ ret, double* __restrict__ partial) {
-  __shared__ Mom red[2][256];
+                                                               float* __restrict__ ret, double* __restrict__ partial,
+                                                               NormArgs na) {
+  __shared__ Mom red[MODE == 2 ? 1 : 2][MODE == 2 ? 1 : 256];
   const int tid = threadIdx.x;
   const int epb = 256 / ct;
   const int el = tid / ct, cl = tid - (tid / ct) * ct;
@@ -128,6 +144,15 @@ __global__ __launch_bounds__(256) void gae_scan_moments_kernel(int T, int E, int
   const int64_t width = (int64_t)E * cols;
   const int64_t i = TCE ? (int64_t)c * E + e : (int64_t)e * cols + c;
   SeqMom ma{0.0, 0.0, 0.0}, mr{0.0, 0.0, 0.0};
+  // MODE 2: this thread's column statistics (gate off or no statistics = identity)
+  double m0 = 0.0, s0 = 1.0, m1 = 0.0, s1 = 1.0;
+  bool n0 = false, n1 = false;
+  if (MODE == 2 && active) {
+    n0 = na.mean0 && *na.gate0;
+    n1 = na.mean1 && *na.gate1;
+    if (n0) { m0 = na.mean0[c]; s0 = na.scale0[c]; }
+    if (n1) { m1 = na.mean1[c]; s1 = na.scale1[c]; }
+  }
   if (active) {
     const bool global_last = last_shard && (e == E - 1);
     // per-column rewards share the values' layout; broadcast rewards are [T][E]
@@ -179,14 +204,22 @@ __global__ __launch_bounds__(256) void gae_scan_moments_kernel(int T, int E, int
         v_next = v;
         const float af = (float)a, rf = (float)R;
         const int64_t o = (int64_t)t * width + i;
-        adv[o] = af;
-        ret[o] = rf;
-        // the statistics are those of the stored fp32 values, as a separate pass over adv / ret sees them
-        ma.add((double)af, t == T - 1);
-        mr.add((double)rf, t == T - 1);
+        if constexpr (MODE == 0) {
+          adv[o] = af;
+          ret[o] = rf;
+        } else if constexpr (MODE == 2) {
+          adv[o] = n0 ? nrm(af, m0, s0) : af;
+          ret[o] = n1 ? nrm(rf, m1, s1) : rf;
+        }
+        if constexpr (MODE != 2) {
+          // the statistics are those of the stored fp32 values, as a separate pass over adv / ret sees them
+          ma.add((double)af, t == T - 1);
+          mr.add((double)rf, t == T - 1);
+        }
       }
     }
   }
+  if constexpr (MODE == 2) return;
   red[0][tid] = ma.get(active ? T : 0);
   red[1][tid] = mr.get(active ? T : 0);
   __syncthreads();
@@ -246,8 +279,6 @@ __global__ __launch_bounds__(256) void gae_moments_reduce_kernel(int nb, int col
 //   [T][cols][E] (TCE): block (bx, row = t * cols + c) streams float4s of one row -- the column and its
 //                       mean / scale are wave-uniform scalars, loaded once per block;
 //   [T][E][cols]:       flat float4 stream, column of element j = j mod cols in 32-bit arithmetic.
-__device__ __forceinline__ float nrm(float v, double m, double sc) { return (float)(((double)v - m) * sc); }
-
 template <bool TCE>
 __global__ __launch_bounds__(256) void normalize_pair_kernel(int64_t n, int rows, int E, int cols,
                                                              float* __restrict__ x0, const double* __restrict__ mean0,
@@ -494,12 +525,25 @@ extern "C" int64_t d2d_gae_moments_workspace(int32_t E, int32_t cols, int32_t la
   return (int64_t)cols * g.x * 6;
 }
 
+template <int MODE>
+static void launch_scan(int32_t layout, dim3 grid, hipStream_t s, int T, int E, int cols, int rcols, int ct,
+                        const float* rew, const float* val, const uint8_t* done, double gamma, double lam,
+                        int last_shard, float* adv, float* ret, double* partial, NormArgs na) {
+  if (layout)
+    hipLaunchKernelGGL((gae_scan_moments_kernel<1, MODE>), grid, dim3(256), 0, s, T, E, cols, rcols, ct, rew, val, done,
+                       gamma, lam, last_shard, adv, ret, partial, na);
+  else
+    hipLaunchKernelGGL((gae_scan_moments_kernel<0, MODE>), grid, dim3(256), 0, s, T, E, cols, rcols, ct, rew, val, done,
+                       gamma, lam, last_shard, adv, ret, partial, na);
+}
+
 extern "C" int d2d_gae_scan_moments(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards,
                                     const float* values, const uint8_t* dones, double gamma, double lam,
                                     int32_t last_shard, int32_t layout, float* adv, float* ret, double* moments,
                                     double* workspace, int64_t workspace_len, void* stream) {
+  // adv == ret == NULL: moments only (ABI 9)
   if (T < 0 || E < 0 || cols < 1 || (reward_cols != 1 && reward_cols != cols) || (layout != 0 && layout != 1) ||
-      !rewards || !values || !dones || !adv || !ret || !moments || !workspace ||
+      !rewards || !values || !dones || (!adv != !ret) || !moments || !workspace ||
       workspace_len < d2d_gae_moments_workspace(E, cols, layout)) {
     d2d_set_error("d2d_gae_scan_moments: bad arguments");
     return D2D_EINVAL;
@@ -512,15 +556,38 @@ extern "C" int d2d_gae_scan_moments(int32_t T, int32_t E, int32_t cols, int32_t 
   int ct;
   dim3 grid;
   moments_grid(E, cols, layout, &ct, &grid);
-  if (layout)
-    hipLaunchKernelGGL(gae_scan_moments_kernel<1>, grid, dim3(256), 0, s, T, E, cols, reward_cols, ct, rewards, values,
-                       dones, gamma, lam, last_shard, adv, ret, workspace);
+  const NormArgs na{};
+  if (adv)
+    launch_scan<0>(layout, grid, s, T, E, cols, reward_cols, ct, rewards, values, dones, gamma, lam, last_shard, adv, ret,
+                   workspace, na);
   else
-    hipLaunchKernelGGL(gae_scan_moments_kernel<0>, grid, dim3(256), 0, s, T, E, cols, reward_cols, ct, rewards, values,
-                       dones, gamma, lam, last_shard, adv, ret, workspace);
+    launch_scan<1>(layout, grid, s, T, E, cols, reward_cols, ct, rewards, values, dones, gamma, lam, last_shard, adv, ret,
+                   workspace, na);
   D2D_CHECK_HIP(hipGetLastError());
   hipLaunchKernelGGL(gae_moments_reduce_kernel, dim3((unsigned)cols), dim3(256), 0, s, (int)grid.x, cols, workspace,
                      moments);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
+extern "C" int d2d_gae_scan_normalized(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards,
+                                       const float* values, const uint8_t* dones, double gamma, double lam,
+                                       int32_t last_shard, int32_t layout, float* adv, const double* mean0,
+                                       const double* scale0, const int32_t* gate0, float* ret, const double* mean1,
+                                       const double* scale1, const int32_t* gate1, void* stream) {
+  if (T < 0 || E < 0 || cols < 1 || (reward_cols != 1 && reward_cols != cols) || (layout != 0 && layout != 1) ||
+      !rewards || !values || !dones || !adv || !ret || (mean0 && (!scale0 || !gate0)) ||
+      (mean1 && (!scale1 || !gate1))) {
+    d2d_set_error("d2d_gae_scan_normalized: bad arguments");
+    return D2D_EINVAL;
+  }
+  if (T == 0 || E == 0) return D2D_OK;
+  int ct;
+  dim3 grid;
+  moments_grid(E, cols, layout, &ct, &grid);
+  const NormArgs na{mean0, scale0, mean1, scale1, gate0, gate1};
+  launch_scan<2>(layout, grid, reinterpret_cast<hipStream_t>(stream), T, E, cols, reward_cols, ct, rewards, values, dones,
+                 gamma, lam, last_shard, adv, ret, nullptr, na);
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
 }

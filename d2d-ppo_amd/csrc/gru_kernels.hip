@@ -66,7 +66,9 @@ __device__ __forceinline__ void split2_pairs(const float (&v)[4], uint32_t (&h)[
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
     h[p] = rne_pair(v[2 * p], v[2 * p + 1]);
-    m[p] = rne_pair(v[2 * p] - __uint_as_float(h[p] << 16), v[2 * p + 1] - __uint_as_float(h[p] & 0xFFFF0000u));
+    // h << 16 on v_perm_b32: written as a shift, the compiler re-derives it from a second conversion
+    m[p] = rne_pair(v[2 * p] - __uint_as_float(__builtin_amdgcn_perm(h[p], h[p], 0x01000c0cu)),
+                    v[2 * p + 1] - __uint_as_float(h[p] & 0xFFFF0000u));
   }
 }
 
@@ -74,13 +76,16 @@ __device__ __forceinline__ void split2_pairs(const float (&v)[4], uint32_t (&h)[
 // fragment [h0 m0 h1 m1 h2 m2 h3 m3] of k-slots (value q, part p) = 2q + p
 __device__ __forceinline__ u32x4v split_pairs(const f32x4 v) {
   u32x4v o;
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
-    const bf2 t = {(__bf16)v[q], (__bf16)0.f};  // v_cvt_pk_bf16_f32
-    const float r = v[q] - ffrom(__builtin_bit_cast(uint32_t, t) << 16);
-    const bf2 hm = {(__bf16)v[q], (__bf16)r};
-    o[q] = __builtin_bit_cast(uint32_t, hm);
+  for (int p = 0; p < 2; ++p) {
+    // one conversion rounds both values; their bf16 parts back as fp32 bits on v_perm_b32 / v_and
+    const uint32_t h = rne_pair(v[2 * p], v[2 * p + 1]);
+    const float r0 = v[2 * p] - ffrom(__builtin_amdgcn_perm(h, h, 0x01000c0cu));
+    const float r1 = v[2 * p + 1] - ffrom(h & 0xFFFF0000u);
+    const bf2 hm0 = {(__bf16)v[2 * p], (__bf16)r0}, hm1 = {(__bf16)v[2 * p + 1], (__bf16)r1};
+    o[2 * p] = __builtin_bit_cast(uint32_t, hm0);
+    o[2 * p + 1] = __builtin_bit_cast(uint32_t, hm1);
   }
   return o;
 }

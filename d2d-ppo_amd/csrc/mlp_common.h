@@ -64,6 +64,15 @@ __device__ __forceinline__ void xcd_block(int& bx, int& by) {
   by = (int)(b / nx);
 }
 
+constexpr float kLn2 = 0.693147180559945309f;
+
+// log2 on the hardware instruction (v_log_f32, ~1 ulp in log2).  Every caller passes a clamped
+// probability >= eps = 2^-23, far above the denormal range, so the library logf's denormal
+// rescaling and extended-precision ln 2 product (12 VALU per call; 8 calls per sample in the PPO
+// epilogue, ~90 VALU per 32-sample actor tile) buy nothing: callers sum log2 terms and scale by
+// ln 2 once (or multiply each result, where a single log is taken).
+__device__ __forceinline__ float hw_log2(float x) { return __builtin_amdgcn_logf(x); }
+
 // relu as one v_max_i32 on the bit pattern (negative floats are negative ints, -0 -> +0);
 // fmaxf(x, 0) costs a NaN-quieting canonicalize plus the max under the IEEE mode
 __device__ __forceinline__ float relu(float x) { return __int_as_float(max(__float_as_int(x), 0)); }

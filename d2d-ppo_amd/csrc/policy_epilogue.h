@@ -35,13 +35,13 @@ constexpr float kLog2e = 1.4426950408889634f;
 
 // torch.distributions.Bernoulli(probs).log_prob(t) = -BCEWithLogits(logit(clamp(p)), t) with p
 // clamped to [eps, 1-eps]: mathematically log(pc) for t = 1 and log(1 - pc) for t = 0.  One
-// hardware log (v_log_f32, ~1 ulp in log2) of the selected argument: 1 - pc is exact for
+// hardware log (hw_log2: v_log_f32, ~1 ulp in log2, times ln 2) of the selected argument: 1 - pc is exact for
 // pc >= 1/2 and within 2^-24 relative below, so the absolute error of the result is ~1e-7 (the
 // library logf/log1pf pair costs ~190 instructions per call; parity tolerance is 1e-5 absolute).
 __device__ __forceinline__ float bernoulli_logp(float p, bool t) {
   const float eps = 1.1920928955078125e-07f;
   const float pc = fminf(fmaxf(p, eps), 1.f - eps);
-  return __logf(t ? pc : 1.f - pc);
+  return hw_log2(t ? pc : 1.f - pc) * kLn2;
 }
 
 // Input index carried by lane group g at MFMA k-step s.  The k order is permuted so that a
@@ -206,7 +206,7 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
     float lpv = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (4 * ga + r == chosen) lpv = __logf(fminf(fmaxf(p[r] * __builtin_amdgcn_rcpf(tot), eps), 1.f - eps));
+      if (4 * ga + r == chosen) lpv = hw_log2(fminf(fmaxf(p[r] * __builtin_amdgcn_rcpf(tot), eps), 1.f - eps)) * kLn2;
     lpv = group_sum<HALF>(lpv);
     lp = lpv;
     out_id = chosen;

@@ -56,12 +56,13 @@ __device__ __forceinline__ f32x4 ppo_dz(const Args& a, f32x4 z, uint32_t act, fl
   float logp, ent;
   if constexpr (KIND == 0) {
     const uint32_t bits = act >> (4 * ga);
+    // log terms in log2 units (hw_log2); ln 2 is folded into the per-sample scales below
     float lsum = 0.f, esum = 0.f, logit[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float pc = fminf(fmaxf(p[r], kEps), 1.f - kEps);
       const bool inside = pc == p[r];  // == (p >= eps && p <= 1 - eps): the clamp passes p through
-      const float l1 = __logf(pc), l0 = __logf(1.f - pc);
+      const float l1 = hw_log2(pc), l0 = hw_log2(1.f - pc);
       const bool bit = (bits >> r) & 1u;
       lsum += valid[r] ? (bit ? l1 : l0) : 0.f;
       esum += valid[r] ? -(p[r] * l1 + (1.f - p[r]) * l0) : 0.f;
@@ -69,14 +70,15 @@ __device__ __forceinline__ f32x4 ppo_dz(const Args& a, f32x4 z, uint32_t act, fl
       // d log_prob / dp: 1/pc or -1/(1-pc) -- one reciprocal of the selected (signed) denominator
       dsur[r] = (valid[r] && inside) ? __builtin_amdgcn_rcpf(bit ? pc : -(1.f - pc)) : 0.f;
     }
-    logp = group_sum<HALF>(lsum) * a.inv_A;
-    ent = group_sum<HALF>(esum) * a.inv_A;
+    const float lA = kLn2 * a.inv_A;  // wave-uniform
+    logp = group_sum<HALF>(lsum) * lA;
+    ent = group_sum<HALF>(esum) * lA;
     const float ratio = __expf(logp - lo);
     const float cr = fminf(fmaxf(ratio, a.clip_lo), a.clip_hi);
     const float s1 = ratio * W, s2 = cr * W;
     const bool gate = (ratio >= a.clip_lo && ratio <= a.clip_hi) || s1 < s2;
     const float coef = gate ? -a.scale * ratio * W * a.inv_A : 0.f;
-    const float eb = a.beta * a.scale * a.inv_A;  // d(-beta*mean ent)/dp_c = +beta * logit_c / A / B
+    const float eb = a.beta * a.scale * lA;  // d(-beta*mean ent)/dp_c = +beta * logit_c / A / B (logit in log2 units)
 #pragma unroll
     for (int r = 0; r < 4; ++r) gr[r] = valid[r] ? coef * dsur[r] + eb * logit[r] : 0.f;
     surr_acc += (ok && ga == 0) ? fminf(s1, s2) : 0.f;
@@ -107,7 +109,7 @@ __device__ __forceinline__ f32x4 ppo_dz(const Args& a, f32x4 z, uint32_t act, fl
       q[r] = p[r] * ipsum;
       const float qc = fminf(fmaxf(q[r], kEps), 1.f - kEps);
       const bool inside = qc == q[r];  // the clamp passes q through
-      const float lq = __logf(qc);
+      const float lq = hw_log2(qc) * kLn2;
       const bool chosen = valid[r] && 4 * ga + r == aid;
       lsel += chosen ? lq : 0.f;
       esum += valid[r] ? q[r] * lq : 0.f;

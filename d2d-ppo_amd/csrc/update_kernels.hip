@@ -117,6 +117,9 @@ __device__ __forceinline__ uint32_t rne2(float a, float b) {
   const bf16x2_t v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32
   return __builtin_bit_cast(uint32_t, v);
 }
+// the low bf16 of a packed pair as fp32 bits (h << 16) on v_perm_b32: written as a shift, the
+// compiler re-derives it from the pair's first operand (a second v_cvt_pk_bf16_f32 plus the shift)
+__device__ __forceinline__ uint32_t bf16_lo_as_f32bits(uint32_t h) { return __builtin_amdgcn_perm(h, h, 0x01000c0cu); }
 struct Parts2x4 {
   uint32_t h[2], m[2];
 };
@@ -126,7 +129,7 @@ __device__ __forceinline__ Parts2x4 split2_4(const float (&v)[4]) {
   for (int p = 0; p < 2; ++p) {
     const uint32_t h = rne2(v[2 * p], v[2 * p + 1]);
     o.h[p] = h;
-    o.m[p] = rne2(v[2 * p] - ffrom(h << 16), v[2 * p + 1] - ffrom(h & 0xFFFF0000u));
+    o.m[p] = rne2(v[2 * p] - ffrom(bf16_lo_as_f32bits(h)), v[2 * p + 1] - ffrom(h & 0xFFFF0000u));
   }
   return o;
 }
@@ -134,12 +137,16 @@ __device__ __forceinline__ Parts2x4 split2_4(const float (&v)[4]) {
 // bf16 1.0 / 0.0 for h > 0 (the relu derivative, torch's convention at 0) of two values, packed; from
 // relu(h) (relu() above: the bit pattern is > 0 exactly when h > 0), one v_min_u32 each
 // (asm: the compiler turns a plain min into a float compare + select, two instructions)
+// Packed form: the two high halves side by side (v_perm_b32), min(., 1) per half (v_pk_min_u16) and
+// x 0x3F80 per half (v_pk_mul_lo_u16): 3 VALU per pair instead of 4.  The high half of relu(h) is
+// nonzero exactly when relu(h) >= 2^-133 (the actor's relu mask has the same bf16-underflow edge).
+// (asm: the compiler turns the packed min and multiply into a compare + select per half)
 __device__ __forceinline__ uint32_t relu_mask_pair(float r0, float r1) {
-  uint32_t m0, m1;
-  asm("v_min_u32 %0, %1, 1" : "=v"(m0) : "v"(r0));
-  asm("v_min_u32 %0, %1, 1" : "=v"(m1) : "v"(r1));
-  // 24-bit multiply (v_mul_u32_u24, full rate; a 32-bit constant multiply is v_mul_lo_u32, quarter rate)
-  return __umul24(m0 | (m1 << 16), 0x3F80u);
+  const uint32_t hi = __builtin_amdgcn_perm(fbits(r1), fbits(r0), 0x07060302u);
+  uint32_t m, o;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(hi), "s"(0x00010001u));
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(o) : "v"(m), "s"(0x3F803F80u));
+  return o;
 }
 
 // high parts only (bf16-exact values)
@@ -582,12 +589,15 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
         bf16x8 bx1[QT], bx2[QT];
 #pragma unroll
         for (int q = 0; q < QT; ++q) {
-          if constexpr (TR) {  // the bf16 image holds the (exact) inputs already as operand halves
-            uint32_t xh2[2];
-#pragma unroll
-            for (int p2 = 0; p2 < 2; ++p2)
-              xh2[p2] = (uint32_t)xw16[16 * s + 4 * g + 2 * p2][16 * q + i] |
-                        ((uint32_t)xw16[16 * s + 4 * g + 2 * p2 + 1][16 * q + i] << 16);
+          if constexpr (TR) {
+            // the bf16 image holds the (exact) inputs already as operand halves: samples 4g .. 4g + 3 of
+            // input column 16q + i in one transposing read (lane 4q' + p of each 16-lane group
+            // addresses row 16s + 4g + q', columns 16q + 4p .. 16q + 4p + 3)
+            typedef __attribute__((address_space(3))) v4i16* lds_v4i16;
+            const v4i16 xt = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (lds_v4i16)(&xw16[16 * s + 4 * g + (i >> 2)][16 * q + 4 * (i & 3)]));
+            const uint2 xu = __builtin_bit_cast(uint2, xt);
+            const uint32_t xh2[2] = {xu.x, xu.y};
             bx1[q] = cat(xh2, xh2);
             continue;
           }
@@ -923,10 +933,12 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_critic_g
           const float v = row_sum16(pv) + c2;
 #endif
           const bool ok = e0 + 16 * s + 4 * g + r < a.E;
-          const float d = v - R[s][r];
-          dvs[r] = ok ? 2.f * a.scale * d : 0.f;
-          if (ok && i == 0) loss_acc += d * d;
-          dc2 += i == 0 ? dvs[r] : 0.f;
+          // every lane of the row holds the same sample's v and R: all of them accumulate (no
+          // per-lane selects) and the partial keeps lane i = 0's sums (the same values and order)
+          const float d = ok ? v - R[s][r] : 0.f;
+          dvs[r] = 2.f * a.scale * d;
+          loss_acc += d * d;
+          dc2 += dvs[r];
         }
 #if D2D_CRITIC_MASK
 #pragma unroll
@@ -1077,8 +1089,8 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_critic_g
     const float v = group_sum(acc[n++]);
     if (g == 0 && 16 * t + i < H) out[OW2 + 16 * t + i] = v;
   }
-  const float dcs = group_sum(row_sum16(acc[n++]));
-  const float ls = group_sum(row_sum16(acc[n++]));
+  const float dcs = group_sum(row_sum16(i == 0 ? acc[n] : 0.f));
+  const float ls = group_sum(row_sum16(i == 0 ? acc[n + 1] : 0.f));
   if (lane == 0) {
     out[OB2] = dcs;
     out[OST] = ls;

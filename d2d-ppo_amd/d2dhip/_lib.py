@@ -37,7 +37,7 @@ def refuse_ablation(what):
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 8
+ABI_VERSION = 9
 D2D_OBS_F32, D2D_OBS_U8 = 0, 1
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
@@ -114,6 +114,9 @@ _SIGS = {
     "d2d_gae_scan_moments": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p,
                                              ctypes.c_double, ctypes.c_double, ctypes.c_int32, ctypes.c_int32, _p, _p,
                                              _p, _p, ctypes.c_int64, _p]),
+    "d2d_gae_scan_normalized": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p,
+                                                _p, ctypes.c_double, ctypes.c_double, ctypes.c_int32, ctypes.c_int32,
+                                                _p, _p, _p, _p, _p, _p, _p, _p, _p]),
     "d2d_normalize_pair": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _p, _p, _p,
                                            _p, _p, _p, _p, _p, _p]),
     "d2d_set_option": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32]),

@@ -43,9 +43,10 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 8  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
+#define D2D_ABI_VERSION 9  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
                               6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_states_to_bf16_exact,
-                              d2d_critic_dpre_split; 8: d2d_gae_scan_moments, d2d_normalize_pair */
+                              d2d_critic_dpre_split; 8: d2d_gae_scan_moments, d2d_normalize_pair;
+                              9: d2d_gae_scan_moments without outputs, d2d_gae_scan_normalized */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -216,6 +217,16 @@ int d2d_gae_scan_moments(int32_t T, int32_t E, int32_t cols, int32_t reward_cols
                          const float* values, const uint8_t* dones, double gamma, double lam, int32_t last_shard,
                          int32_t layout, float* adv, float* ret, double* moments, double* workspace,
                          int64_t workspace_len, void* stream);
+/* ABI 9: adv == ret == NULL computes the moments only (nothing written but moments): the first of the
+ * two scans of a normalised GAE.  The second, d2d_gae_scan_normalized, recomputes the same recursion
+ * and writes adv_k = gate_k ? (adv_k - mean_k) * scale_k : adv_k (and ret likewise; mean == NULL: raw)
+ * -- bitwise the outputs of d2d_gae_scan_moments + d2d_normalize_pair, with 16 B of HBM traffic per
+ * element instead of 28 (ippo.py:92-116: compute_gae + discount_rewards + their normalisation). */
+int d2d_gae_scan_normalized(int32_t T, int32_t E, int32_t cols, int32_t reward_cols, const float* rewards,
+                            const float* values, const uint8_t* dones, double gamma, double lam, int32_t last_shard,
+                            int32_t layout, float* adv, const double* mean0, const double* scale0,
+                            const int32_t* gate0, float* ret, const double* mean1, const double* scale1,
+                            const int32_t* gate1, void* stream);
 
 /* mean = sum / n ; when m2 != NULL: std = sqrt(m2 / (n - ddof)), scale = 1/std and
  * *gate = all columns std > 0 (ippo.py:100-101, 114-115); when m2 == NULL only mean. */

@@ -178,3 +178,53 @@ def test_gae_constant_column_keeps_gate_closed():
     adv, ret = gae_returns(rew, val, done, 0.5, 0.97, last_shard=False)
     # column 1: rewards 0, values 0 -> adv = ret = 0 everywhere (std 0) -> no column is normalised
     assert torch.equal(adv, adv_raw) and torch.equal(ret, ret_raw)
+
+
+@pytest.mark.parametrize("layout,T,E,cols,rcols", [("tce", 200, 1000, 64, 1), ("tec", 200, 333, 64, 1),
+                                                   ("tec", 50, 300, 5, 5), ("tce", 17, 4097, 3, 3),
+                                                   ("tec", 120, 1, 4, 1)])
+@pytest.mark.parametrize("which", ["both", "adv", "ret"])
+def test_gae_two_scan_normalised_equals_scan_plus_normalise(layout, T, E, cols, rcols, which):
+    """ABI 9: the moments-only scan + d2d_gae_scan_normalized (gae_returns' path) write bitwise the
+    outputs of the fused scan + d2d_normalize_pair (the ABI 8 path), for both outputs normalised or
+    only one (the other written raw), and the moments-only scan's statistics equal the fused scan's."""
+    from d2dhip import _lib
+    from d2dhip.gae import gae_returns, moments_stats
+    lib = _lib.require_gpu()
+    dev = "cuda"
+    g = torch.Generator(device=dev)
+    g.manual_seed(T * 3 + E + cols)
+    tce = layout == "tce"
+    vshape = (T, cols, E) if tce else (T, E, cols)
+    val = torch.randn(vshape, device=dev, generator=g) * 2 - 0.5
+    rew = torch.randint(0, 5, (T, E) if rcols == 1 else vshape, device=dev, generator=g).float()
+    done = torch.zeros(T, dtype=torch.uint8, device=dev)
+    done[T // 3] = 1
+    done[-1] = 1
+    lay = 1 if tce else 0
+    na, nr = which in ("both", "adv"), which in ("both", "ret")
+    # ABI 8 path
+    adv0, ret0 = torch.empty_like(val), torch.empty_like(val)
+    mom = torch.empty((2, 3, cols), dtype=torch.float64, device=dev)
+    ws = torch.empty(int(lib.d2d_gae_moments_workspace(E, cols, lay)), dtype=torch.float64, device=dev)
+    _lib.check(lib.d2d_gae_scan_moments(T, E, cols, rcols, rew.data_ptr(), val.data_ptr(), done.data_ptr(), 0.6, 0.97,
+                                        1, lay, adv0.data_ptr(), ret0.data_ptr(), mom.data_ptr(), ws.data_ptr(),
+                                        ws.numel(), _lib.stream_ptr()), "scan_moments")
+    mom_only = torch.empty_like(mom)
+    _lib.check(lib.d2d_gae_scan_moments(T, E, cols, rcols, rew.data_ptr(), val.data_ptr(), done.data_ptr(), 0.6, 0.97,
+                                        1, lay, None, None, mom_only.data_ptr(), ws.data_ptr(), ws.numel(),
+                                        _lib.stream_ptr()), "scan_moments (moments only)")
+    assert torch.equal(mom, mom_only)
+    args, keep = [], []
+    for x, do, k, ddof in ((adv0, na, 0, 0), (ret0, nr, 1, 1)):
+        if do:
+            st = moments_stats(mom[k], ddof, T * E)
+            keep.append(st)
+            args += [x.data_ptr()] + [t.data_ptr() for t in st]
+        else:
+            args += [None] * 4
+    _lib.check(lib.d2d_normalize_pair(T, E, cols, lay, *args, _lib.stream_ptr()), "normalize_pair")
+    # ABI 9 path
+    adv1, ret1 = gae_returns(rew, val, done, 0.6, 0.97, normalize_adv=na, normalize_ret=nr, layout=layout)
+    torch.cuda.synchronize()
+    assert torch.equal(adv1, adv0) and torch.equal(ret1, ret0)
