@@ -235,10 +235,17 @@ def pmc_mfma(kernel_prefix):
     if not d:
         return None
     for k in d.get("kernels", []):
-        if k.get("kernel", "").startswith(kernel_prefix):
-            return {"mfma_busy_frac_pmc": k.get("mfma_busy_frac"), "valu_per_mfma_pmc": k.get("valu_per_mfma"),
+        name = k.get("kernel", "")
+        if name.startswith("void "):  # rocprofv3 prints template kernels with their return type
+            name = name[5:]
+        if name.startswith(kernel_prefix):
+            pd = k.get("per_dispatch", {})
+            valu, mfma = pd.get("SQ_INSTS_VALU"), pd.get("SQ_INSTS_MFMA")
+            # SQ_INSTS_VALU counts the MFMAs too: non-MFMA vector instructions per MFMA
+            vpm = (valu - mfma) / mfma if valu is not None and mfma else None
+            return {"mfma_busy_frac_pmc": k.get("mfma_busy_frac"), "valu_per_mfma_pmc": vpm,
                     "source": rel, "commit": d.get("commit"), "workload": d.get("workload"),
-                    "pmc_kernel": k.get("kernel")}
+                    "pmc_kernel": k.get("kernel"), "avg_duration_us": k.get("avg_duration_us")}
     return None
 
 
@@ -701,6 +708,11 @@ def gru_leg(args, rank, world, local):
     grad_ms = max_over_ranks(ev[2].elapsed_time(ev[3]), world)
     samples = ro.T * E2 * N
     grad_flop = 3 * L * cell * samples + 3 * head * samples
+    # one untimed iteration first: the first update epochs of a process pay one-time host costs
+    # (kernel loads, hipBLASLt solution lookup for the central critic, allocator growth) of ~0.5-1 s
+    ro = lr._rollout(E2)
+    for _ in range(5):
+        lr._update_epoch(ro, lr._update_state(ro))
     torch.cuda.synchronize()
     barrier(world)
     t0 = time.perf_counter()
@@ -722,7 +734,9 @@ def gru_leg(args, rank, world, local):
                            "mfma_pipe_busy_frac_static": pol_pipe, "mfma_pmc": pmc_mfma("d2d::gru_policy_kernel"),
                            "bound": "mfma"},
            "update": {"envs_per_gpu": E2, "slots": ro.T, "agent_samples": samples,
-                      "kernel": f"d2d::gru_grad_kernel<4, {it_}, 0, true>", "ms": grad_ms,
+                      "kernel": f"d2d::gru_grad_kernel<4, {it_}, 0, true, {'true' if it_ <= 2 else 'false'}>",
+                      "weight_gradients": "cooperative LDS exchange" if it_ <= 2 else "per-wave global row history",
+                      "ms": grad_ms,
                       "agent_samples_per_s": samples * world / (grad_ms / 1e3), "flop": grad_flop,
                       "achieved_tflops": grad_flop / (grad_ms / 1e3) / 1e12, "peak_tflops_fp32_mfma": peak,
                       "frac": grad_flop / (grad_ms / 1e3) / 1e12 / peak,

@@ -1140,8 +1140,13 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
 }  // namespace
 
 extern int g_policy_f32_mfma;  // policy_kernels.hip
+extern int g_gru_grad_history;  // gru_kernels.hip
 
 extern "C" int d2d_set_option(int32_t option, int32_t value) {
+  if (option == D2D_OPT_GRU_GRAD_HISTORY) {
+    g_gru_grad_history = value ? 1 : 0;
+    return D2D_OK;
+  }
   if (option == D2D_OPT_NT_STORES) {
     g_nt_stores = value ? 1 : 0;
     return D2D_OK;

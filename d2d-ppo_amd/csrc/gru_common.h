@@ -73,18 +73,25 @@ struct SwzOff {
   }
 };
 
-// e^v to ~1 ulp on the hardware exp2: v * log2(e) is carried as th + tl (FMA residual plus the
-// low part of log2 e), 2^tl ~ 1 + tl ln 2.  (__expf rounds v * log2 e first: ~|v| ulp of error,
-// which the recurrence accumulates over the window.)
-__device__ __forceinline__ float exp_acc(float v) {
-  const float kL = 1.44269502162933349609375f, kLlo = 1.925963033500e-08f;
+// 1 + e^(kS v) to ~1 ulp on the hardware exp2 (the sigmoid / tanh denominators): kS v log2(e) is
+// carried as th + tl (FMA residual plus the low part of log2 e), 2^tl ~ 1 + tl ln 2, and the 1 + is
+// one more FMA.  (__expf rounds v * log2 e first: ~|v| ulp of error, which the recurrence accumulates
+// over the window.)  kS = 1 or 2 scales log2 e's split exactly.  The file is built with
+// -ffp-contract=off (the env kernels' oracle-exact arithmetic), so every multiply-add of the gate math
+// is an explicit fmaf: one VALU and one rounding instead of two of each (gate math 36 -> 25 VALU per
+// element).
+template <int kS = 1>
+__device__ __forceinline__ float one_plus_exp_acc(float v) {
+  const float kL = 1.44269502162933349609375f * kS, kLlo = 1.925963033500e-08f * kS;
   const float th = v * kL;
-  const float tl = fmaf(v, kL, -th) + v * kLlo;
-  return __builtin_amdgcn_exp2f(th) * fmaf(tl, 0.693147180559945f, 1.f);
+  const float tl = fmaf(v, kLlo, fmaf(v, kL, -th));
+  return fmaf(__builtin_amdgcn_exp2f(th), fmaf(tl, 0.693147180559945f, 1.f), 1.f);
 }
-__device__ __forceinline__ float sigmoidf_(float v) { return __builtin_amdgcn_rcpf(1.f + exp_acc(-v)); }
+__device__ __forceinline__ float sigmoidf_(float v) { return __builtin_amdgcn_rcpf(one_plus_exp_acc(-v)); }
 // tanh(v) = 1 - 2 / (e^{2v} + 1): absolute error ~1e-7, saturates cleanly at +-1
-__device__ __forceinline__ float tanhf_(float v) { return 1.f - 2.f * __builtin_amdgcn_rcpf(exp_acc(2.f * v) + 1.f); }
+__device__ __forceinline__ float tanhf_(float v) { return fmaf(-2.f, __builtin_amdgcn_rcpf(one_plus_exp_acc<2>(v)), 1.f); }
+// the candidate gate n = tanh(W_in x + b_in + r (W_hn h + b_hn)) from its two pre-activation parts
+__device__ __forceinline__ float gru_n(float ni, float rr, float nh) { return tanhf_(fmaf(rr, nh, ni)); }
 
 // Fill the input / recurrent images of agent k (all threads of the workgroup).
 template <int HT, int IT>
@@ -260,8 +267,8 @@ __device__ __forceinline__ void gru_gates(const f32x4 (&rz)[2 * HT], const f32x4
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float rr = sigmoidf_(rz[t][r]), zz = sigmoidf_(rz[HT + t][r]);
-      const float nn = tanhf_(ni[t][r] + rr * nh[t][r]);
-      h[t][r] = (1.f - zz) * nn + zz * h[t][r];
+      const float nn = gru_n(ni[t][r], rr, nh[t][r]);
+      h[t][r] = fmaf(zz, h[t][r] - nn, nn);  // (1 - z) n + z h
     }
 }
 
@@ -291,10 +298,33 @@ struct GruSplit {
   static constexpr int WIH = NT * CI * 3 * 64, WHH = NT * CH * 3 * 64;  // bf16x8 words
 };
 
+// Exact three-way split by rounding to nearest even: h = RNE(v), m = RNE(v - h), l = v - h - m (exact in
+// bf16: v's 24 significant bits span three 8-bit parts).  The update kernel's cooperative path splits
+// its W_hh image so, and its (h, m) parts ARE the RNE two-way split of W_hh: the dh = W_hh^T dg operands
+// come from the same image (whh_dh_frag) instead of a second, transposed copy.  The forward products
+// keep the six terms of mfma_split (|m| <= 2^-9 |v|, |l| <= 2^-18 |v|: the dropped ones are below 2^-26).
+__device__ __forceinline__ Parts split3_rne(const float (&v)[8]) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  uint32_t H[4], M[4], L[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float a = v[2 * p], b = v[2 * p + 1];
+    const bf2 hv = {(__bf16)a, (__bf16)b};
+    H[p] = __builtin_bit_cast(uint32_t, hv);
+    const float ar = a - ffrom(__builtin_amdgcn_perm(H[p], H[p], 0x01000c0cu)), br = b - ffrom(H[p] & 0xFFFF0000u);
+    const bf2 mv = {(__bf16)ar, (__bf16)br};
+    M[p] = __builtin_bit_cast(uint32_t, mv);
+    const float al = ar - ffrom(__builtin_amdgcn_perm(M[p], M[p], 0x01000c0cu)), bl = br - ffrom(M[p] & 0xFFFF0000u);
+    const bf2 lv = {(__bf16)al, (__bf16)bl};
+    L[p] = __builtin_bit_cast(uint32_t, lv);
+  }
+  return {as_frag(H), as_frag(M), as_frag(L)};
+}
+
 // Fragment `rel` of agent k's input (inp) or recurrent split image: rel = (T * NC + c) * 64 + lane,
 // its three parts stored 64 words apart ([T][c][part][lane]).  The input image carries the summed
 // r / z biases and b_in at column F (x_F = 1), as load_gru_images does for the fp32 image.
-template <int HT, int IT>
+template <int HT, int IT, bool RNE_HH = false>
 __device__ __forceinline__ Parts split_frag(const GruW& w, int k, int H, int F, bool inp, int rel) {
   using S = GruSplit<HT, IT>;
   const int NC = inp ? S::CI : S::CH;
@@ -319,7 +349,7 @@ __device__ __forceinline__ Parts split_frag(const GruW& w, int k, int H, int F, 
     }
     if (2 * c + (j >> 2) >= (inp ? IT : HT)) v[j] = 0.f;
   }
-  return split3(v);
+  return inp || !RNE_HH ? split3(v) : split3_rne(v);
 }
 __device__ __forceinline__ void store_parts(bf16x8* dst, const Parts& p) {
   dst[0] = p.h;
@@ -327,9 +357,16 @@ __device__ __forceinline__ void store_parts(bf16x8* dst, const Parts& p) {
   dst[128] = p.l;
 }
 __device__ __forceinline__ int split_word(int rel) { return (rel >> 6) * 3 * 64 + (rel & 63); }
+// Slot of lane l's A fragment in the W_hh split image (an involution inside each 16-slot group):
+// 16 g + 4 ((i >> 2) ^ g) + (i & 3) for l = 16 g + i.  The forward reads (one 16-byte slot per lane)
+// stay conflict-free, and the update kernel's transposing reads of the same image (the dh operands,
+// whh_dh_frag) touch 16 distinct 16-byte bank groups per 16 lanes instead of 4.
+__device__ __forceinline__ int whh_slot(int l) { return (l & 0x30) | ((((l >> 2) ^ (l >> 4)) & 3) << 2) | (l & 3); }
 
 // Fill agent k's split images in LDS (all threads of the workgroup); either may be NULL.
-template <int HT, int IT>
+// RNE_HH: the W_hh image split by rounding (split3_rne; the update kernel's cooperative path reads its
+// dh operands from it), else by truncation like every other split image.
+template <int HT, int IT, bool RNE_HH = false>
 __device__ void load_gru_split_images(bf16x8* wih_b, bf16x8* whh_b, const GruW& w, int k, int H, int F, int tid,
                                       int nthr) {
   using S = GruSplit<HT, IT>;
@@ -338,7 +375,8 @@ __device__ void load_gru_split_images(bf16x8* wih_b, bf16x8* whh_b, const GruW& 
       store_parts(wih_b + split_word(rel), split_frag<HT, IT>(w, k, H, F, true, rel));
   if (whh_b)
     for (int rel = tid; rel < S::NT * S::CH * 64; rel += nthr)
-      store_parts(whh_b + split_word(rel), split_frag<HT, IT>(w, k, H, F, false, rel));
+      store_parts(whh_b + (split_word(rel) & ~63) + whh_slot(rel & 63),
+                  split_frag<HT, IT, RNE_HH>(w, k, H, F, false, rel));
 }
 
 // Whether every input of a window step is bf16-exact (wave-uniform): always for the compact record,
@@ -412,6 +450,7 @@ __device__ __forceinline__ void gru_preact_split(const bf16x8* wih_b, const bf16
 #pragma unroll
   for (int t = 0; t < HT; ++t) nh[t] = bhn[t];
   if (h_zero) return;
+  const int hl = whh_slot(lane);
   Parts hp[S::CH];
 #pragma unroll
   for (int c = 0; c < S::CH; ++c) {
@@ -424,7 +463,7 @@ __device__ __forceinline__ void gru_preact_split(const bf16x8* wih_b, const bf16
     f32x4 acc = T < 2 * HT ? rz[T] : nh[T - 2 * HT];
 #pragma unroll
     for (int c = 0; c < S::CH; ++c) {
-      const bf16x8* wf = whh_b + ((T * S::CH + c) * 3) * 64 + lane;
+      const bf16x8* wf = whh_b + ((T * S::CH + c) * 3) * 64 + hl;
 #if D2D_GRU_SPLIT8  // ablation: eight terms
       acc = mfma_split8(Parts{wf[0], wf[64], wf[128]}, hp[c], acc);
 #else

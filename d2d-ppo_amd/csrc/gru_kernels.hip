@@ -351,6 +351,53 @@ struct GruOff {
   }
 };
 
+// COOP (H in (32, 64], compact-record inputs, F + 1 <= 32; D2D_GRU_COOP): the weight gradients without
+// the global row history.  The four waves run their tiles' BPTT steps in lockstep; every step each wave
+// in turn writes its 16 samples' rows -- the r, z, n_in and n_h pre-activation gradients and h_{j-1} as
+// RNE two-way bf16 split planes, x (bf16-exact) as one -- into ONE shared LDS region, and all four waves
+// accumulate their share of the dW_hh / dW_ih output tiles from it (wave w: hidden tile w of the r, z,
+// n gates, every column tile; 12 + 3 IT accumulator tiles held for the whole kernel).  The history's
+// 2.6 MB of HBM traffic per tile and the per-tile read-modify-writes of the wave sums are gone; the
+// products are the bf16 path's (a_h b_h + a_m b_h + a_h b_m, x exact), summed in a fixed order.
+// Region layout (bf16 elements): planes p = 0..9 (r h/m, z h/m, n_in h/m, n_h h/m, h_{j-1} h/m) of
+// [16 samples][64 rows], then x [16 samples][16 IT]; 4-element quads XOR-swizzled by sample so that
+// both the writers (ds_write_b64: 4 rows of one sample) and the transposing readers
+// (ds_read_b64_tr_b16: 4 samples of one row per lane) touch every bank pair at most twice per wave.
+template <int IT>
+struct CoopRegion {
+  static constexpr int PLANE = 16 * 64, X = 10 * PLANE, ELEMS = X + 16 * 16 * IT, BYTES = 2 * ELEMS;
+};
+__device__ __forceinline__ int coop_off(int plane, int s, int c) {
+  return plane * 1024 + s * 64 + (c ^ (((s >> 1) & 3) << 4));
+}
+template <int IT>
+__device__ __forceinline__ int coop_xoff(int s, int c) {
+  return CoopRegion<IT>::X + s * 16 * IT + (IT >= 2 ? (c ^ (((s >> 2) & 1) << 4)) : c);
+}
+typedef short v4i16_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16_t* lds_v4i16_t;
+// 4 samples (4g .. 4g + 3) of row `col` (16-column block base + i) of a plane: two dwords
+__device__ __forceinline__ uint2 coop_tr(const uint16_t* reg, int off) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t)(reg + off)));
+}
+__device__ __forceinline__ bf16x8 cat2(uint2 a, uint2 b) {
+  const u32x4v v = {a.x, a.y, b.x, b.y};
+  return __builtin_bit_cast(bf16x8, v);
+}
+// The A operand of dh = W_hh^T dg for unit tile t and gate tile T, [W_h x4 | W_m x4] of lane (g, i) =
+// W_hh[gate row 16T + 4g + r][unit 16t + i], r = 0..3 -- two transposing reads of the FORWARD split
+// image (split3_rne: its h, m parts are the RNE two-way split).  The forward fragment (T, c = t / 2)
+// holds W_hh[16T + i_f][unit 16 (2c + j / 4) + 4 g_f + j % 4] at slot 16 g_f + i_f, element j; output
+// element r of lane (g, i) comes from the chunk (8-byte half t % 2, element i & 3) addressed by lane
+// (g, 4r + (i >> 2)), so lane (g, L) addresses slot 16 (L & 3) + 4g + (L >> 2) (swizzled, whh_slot).
+template <int HT>
+__device__ __forceinline__ bf16x8 whh_dh_frag(const bf16x8* whh_b, int T, int t, int g, int i) {
+  constexpr int CH = (HT + 1) / 2;
+  const int slot = whh_slot(16 * (i & 3) + 4 * g + (i >> 2));
+  const uint16_t* base = reinterpret_cast<const uint16_t*>(whh_b + ((T * CH + (t >> 1)) * 3) * 64 + slot) + 4 * (t & 1);
+  return cat2(coop_tr(base, 0), coop_tr(base, 64 * 8));  // part h, then part m (64 words on)
+}
+
 // Workgroup = agent k x a strided set of 16-sample tiles; 4 waves (one per SIMD).
 // LDS (H = 64, !SPLIT): W_hh image 48 KB (forward A fragments) + its transpose 49 KB (the A fragments
 // of dh = W_hh^T dg, one ds_read_b128 per 4 MFMAs) + 4 x 12 KB wave scratch = 145 KB (SPLIT: below).
@@ -362,20 +409,28 @@ struct GruOff {
 // SPLIT (default): the forward and the BPTT recompute on the policy kernel's split step
 // (gru_preact_split: the 74 KB split W_hh image in LDS, the split W_ih image from L2); the scratch is
 // then 2 HW rows per wave (the step's gradient rows leave it in three passes), 155 KB in all.
-template <int HT, int IT, int KIND, bool SPLIT>
+template <int HT, int IT, int KIND, bool SPLIT, bool COOP = false>
 __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   constexpr int HW = 16 * HT, R3 = 3 * HW, RT = R3 + 4, SROWS = 2 * HW;
+  static_assert(!COOP || (HT == 4 && SPLIT && D2D_GRU_DH_BF16), "COOP: H in (32, 64], the split step, bf16 dh");
   using SP = GruSplit<HT, IT>;
+  using CR = CoopRegion<IT>;
   __shared__ __attribute__((aligned(16))) unsigned char whh_raw[SPLIT ? 16 * SP::WHH : 4 * R3 * HW];
   float* whh_s = reinterpret_cast<float*>(whh_raw);
   bf16x8* whh_b = reinterpret_cast<bf16x8*>(whh_raw);
-  __shared__ __attribute__((aligned(16))) float whhT_s[HW * RT];  // [unit u][gate row R], row stride R3 + 4
-  __shared__ __attribute__((aligned(16))) float scr[4][SROWS * 16];
+  // [unit u][gate row R], row stride R3 + 4 (COOP: none, the dh operands come from whh_b, whh_dh_frag)
+  __shared__ __attribute__((aligned(16))) float whhT_s[COOP ? 4 : HW * RT];
+  // COOP: one staging region per wave (also its head-phase scratch; region 0 the final reduction
+  // buffer) instead of the per-wave scratch blocks
+  __shared__ __attribute__((aligned(16))) float scr[COOP ? 1 : 4][COOP ? 4 : SROWS * 16];
+  __shared__ __attribute__((aligned(16))) unsigned char creg_raw[COOP ? 4 * CR::BYTES : 16];
+  static_assert(!COOP || CR::BYTES >= SROWS * 16 * 4, "COOP region holds the head scratch");
   const int k = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H, F = a.F, N = a.N, E = a.E, A = KIND == kGruValue ? 1 : a.A, L = a.L;
-  float* sc = scr[wave];
+  uint16_t* creg = reinterpret_cast<uint16_t*>(creg_raw);
+  float* sc = COOP ? reinterpret_cast<float*>(creg_raw + wave * CR::BYTES) : scr[COOP ? 0 : wave];
   // DH_BF16: the transposed image as 16-byte entries [unit u][gate tile T * 4 + lane group][W_h x4 | W_m x4],
   // TE entries per unit row (one of padding: the 16 lanes' A-fragment reads hit distinct banks)
   constexpr int TE = 3 * HT * 4 + 1;
@@ -390,7 +445,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     }
 #if D2D_GRU_DH_BF16
     bf16x8* whhTb = reinterpret_cast<bf16x8*>(whhT_s);
-    for (int idx = tid; idx < HW * 3 * HT * 4; idx += blockDim.x) {
+    for (int idx = tid; idx < (COOP ? 0 : HW * 3 * HT * 4); idx += blockDim.x) {
       const int c = idx / (3 * HT * 4), rem = idx - c * (3 * HT * 4), T = rem >> 2, gg = rem & 3;
       float v[4];
 #pragma unroll
@@ -404,7 +459,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       whhTb[c * TE + T * 4 + gg] = __builtin_bit_cast(bf16x8, e);
     }
 #endif
-    if constexpr (SPLIT) load_gru_split_images<HT, IT>(nullptr, whh_b, a.w, k, H, F, tid, blockDim.x);
+    if constexpr (SPLIT) load_gru_split_images<HT, IT, COOP>(nullptr, whh_b, a.w, k, H, F, tid, blockDim.x);
   }
   f32x4 bhn[HT];
   load_bhn<HT>(bhn, a.w, k, H, g);
@@ -428,7 +483,20 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   using WA = GruWAcc<HT, IT>;
   float* ghist = a.ghist + wave_id * (size_t)L * 5 * HW * 16;
   float* gpart = a.gpart + wave_id * (size_t)WA::NV * 64;
-  for (int v = 0; v < WA::NV; ++v) gpart[v * 64 + lane] = 0.f;
+  if constexpr (!COOP)
+    for (int v = 0; v < WA::NV; ++v) gpart[v * 64 + lane] = 0.f;
+  // COOP: this wave's output tiles, all tiles of the kernel: dW_hh [gate g3][column tile U] and dW_ih
+  // [g3][input tile U] of gate rows 16 (4 g3 + wave) + 4g + r
+  f32x4 cwh[COOP ? 3 : 1][COOP ? HT : 1], cwi[COOP ? 3 : 1][COOP ? IT : 1];
+  if constexpr (COOP) {
+#pragma unroll
+    for (int g3 = 0; g3 < 3; ++g3) {
+#pragma unroll
+      for (int U = 0; U < HT; ++U) cwh[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int U = 0; U < IT; ++U) cwi[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
   __syncthreads();
 
   // The front-padding steps of a training window (x = the bias input only, h0 = 0) give the same h_j
@@ -467,16 +535,22 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   }
 
   const int n_tiles = a.T * a.env_tiles;
-  for (int tile = blockIdx.y * 4 + wave; tile < n_tiles; tile += gridDim.y * 4) {  // wave-uniform
-    const int slot = tile / a.env_tiles;
-    const int e0 = (tile - slot * a.env_tiles) * 16;
+  // COOP: block-uniform rounds (the waves' BPTT steps meet at barriers); a wave without a tile in the
+  // last round runs an all-invalid tile (every sample masked: zero gradient rows) through the barriers
+  const int rounds = (n_tiles + 4 * (int)gridDim.y - 1) / (4 * (int)gridDim.y);
+  for (int rnd = 0; COOP ? rnd < rounds : true; ++rnd) {
+    const int tile = (rnd * (int)gridDim.y + (int)blockIdx.y) * 4 + wave;  // wave-uniform
+    if (!COOP && tile >= n_tiles) break;
+    const bool active = tile < n_tiles;
+    const int slot = active ? tile / a.env_tiles : 0;
+    const int e0 = active ? (tile - slot * a.env_tiles) * 16 : 0;
     const int env = e0 + i;
-    const bool ok = env < E;
+    const bool ok = active && env < E;
     const int pos = slot % a.ep_len;
     const int S = min(pos + 1, L);
     const int lo = slot - S + 1;
     const int pad = L - S;  // training windows: front-zero-padded to L (preprocess_input_for_rnn)
-    const GruIn in = load_gru_in<KIND>(a, slot, env, k, ok);
+    const GruIn in = active ? load_gru_in<KIND>(a, slot, env, k, ok) : GruIn{0u, 0.f, 0.f};
     auto row_of = [&](int j) { return ((size_t)(j < pad ? lo : lo + j - pad) * E + e0) * N + k; };
 
     // ---- forward over the window; h_j (j < L - 1) to the wave's scratch
@@ -516,7 +590,9 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       }
     }
 
-    // ---- head forward + loss gradient w.r.t. the head outputs
+    // ---- head forward + loss gradient w.r.t. the head outputs (COOP: the scratch is the wave's region)
+    float gcur[HT][4];
+    auto head_phase = [&]() {
     f32x4 pre1[HT], lg;
     float y[HT][4];
     const float* hi_ = himg + opaque_zero();
@@ -595,7 +671,6 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       }
       rmw_block(hacc, lane, HA::W1 + t * HT * 4, dw1);
     }
-    float gcur[HT][4];
 #pragma unroll
     for (int t = 0; t < HT; ++t) {
       f32x4 dh = {0.f, 0.f, 0.f, 0.f};
@@ -608,6 +683,8 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       for (int r = 0; r < 4; ++r) gcur[t][r] = dh[r];
     }
     lds_order();
+    };
+    head_phase();
 
     // ---- backpropagation through time, j = L-1 .. 0 (gates recomputed from h_{j-1}); the step's
     // h_{j-1} and x tile are loaded one step ahead
@@ -655,10 +732,10 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const float rr = sigmoidf_(rz[t][r]), zz = sigmoidf_(rz[HT + t][r]);
-          const float nn = tanhf_(ni[t][r] + rr * nh[t][r]);
+          const float nn = gru_n(ni[t][r], rr, nh[t][r]);
           const float gv = gcur[t][r];
           const float dn = gv * (1.f - zz), dz = gv * (hp[t][r] - nn);
-          dnp[t][r] = dn * (1.f - nn * nn);
+          dnp[t][r] = dn * fmaf(-nn, nn, 1.f);
           dghn[t][r] = dnp[t][r] * rr;
           drp[t][r] = dnp[t][r] * nh[t][r] * rr * (1.f - rr);
           dzp[t][r] = dz * zz * (1.f - zz);
@@ -687,9 +764,11 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
         lds_order();
       };
 #if D2D_GRU_ABLATE != 3
-      stage_rows(drp, dzp, 0);
-      stage_rows(dnp, dghn, 2 * HW);
-      stage_rows(hp, nullptr, 4 * HW);
+      if constexpr (!COOP) {
+        stage_rows(drp, dzp, 0);
+        stage_rows(dnp, dghn, 2 * HW);
+        stage_rows(hp, nullptr, 4 * HW);
+      }
 #endif
       __builtin_amdgcn_sched_barrier(0);
       // dh_{j-1} = g z + W_hh^T dgh: A fragments from the transposed image
@@ -718,7 +797,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #elif D2D_GRU_DH_BF16
 #pragma unroll
         for (int T = 0; T < 3 * HT; ++T) {
-          const bf16x8 af = wtb[(16 * t + i) * TE + T * 4 + g];
+          const bf16x8 af = COOP ? whh_dh_frag<HT>(whh_b, T, t, g, i) : wtb[(16 * t + i) * TE + T * 4 + g];
           dh = mfma_bf16(af, gb1[T], dh);
           dh = mfma_bf16(af, gb2[T], dh);
         }
@@ -736,7 +815,86 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) gcur[t][r] = dh[r];
       }
+#if D2D_GRU_DH_BF16 && D2D_GRU_ABLATE != 2
+      if constexpr (COOP) {
+        // this step's rows as split pairs (r, z, n_h: the dh operands' splits; n_in and h_{j-1} here)
+        uint32_t nih[HT][2], nim[HT][2], hph[HT][2], hpm[HT][2], xw[IT][2];
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+          split2_pairs(dnp[t], nih[t], nim[t]);
+          split2_pairs(hp[t], hph[t], hpm[t]);
+        }
+#pragma unroll
+        for (int q = 0; q < IT; ++q) {  // the record's inputs are bf16-exact: their high halves
+          xw[q][0] = pack_hi(x[q][0], x[q][1]);
+          xw[q][1] = pack_hi(x[q][2], x[q][3]);
+        }
+        uint16_t* own = creg + wave * CR::ELEMS;
+        auto put = [&](int plane, int t, uint32_t w0, uint32_t w1) {
+          *reinterpret_cast<uint2*>(own + coop_off(plane, i, 16 * t + 4 * g)) = make_uint2(w0, w1);
+        };
+        const int sA = 4 * g + (i >> 2), cq = 4 * (i & 3);  // this lane's transposing-read row / column
+        if (D2D_GRU_ABLATE != 6) {  // (ablation 6: no exchange)
+          __syncthreads();  // every wave has consumed the previous step's regions
+          {
+#pragma unroll
+            for (int t = 0; t < HT; ++t) {
+              const u32x4v rh = __builtin_bit_cast(u32x4v, gb1[t]), rm = __builtin_bit_cast(u32x4v, gb2[t]);
+              const u32x4v zh = __builtin_bit_cast(u32x4v, gb1[HT + t]), zm = __builtin_bit_cast(u32x4v, gb2[HT + t]);
+              const u32x4v nh_ = __builtin_bit_cast(u32x4v, gb1[2 * HT + t]), nm = __builtin_bit_cast(u32x4v, gb2[2 * HT + t]);
+              put(0, t, rh[0], rh[1]);
+              put(1, t, rm[0], rm[1]);
+              put(2, t, zh[0], zh[1]);
+              put(3, t, zm[0], zm[1]);
+              put(4, t, nih[t][0], nih[t][1]);
+              put(5, t, nim[t][0], nim[t][1]);
+              put(6, t, nh_[0], nh_[1]);
+              put(7, t, nm[0], nm[1]);
+              put(8, t, hph[t][0], hph[t][1]);
+              put(9, t, hpm[t][0], hpm[t][1]);
+            }
+#pragma unroll
+            for (int q = 0; q < IT; ++q)
+              *reinterpret_cast<uint2*>(own + coop_xoff<IT>(i, 16 * q + 4 * g)) = make_uint2(xw[q][0], xw[q][1]);
+          }
+          __syncthreads();
+        }
+#pragma unroll 1
+        for (int src = 0; src < (D2D_GRU_ABLATE >= 5 ? 0 : 4); ++src) {  // (ablation 5: barriers and writes only)
+          const uint16_t* reg = creg + src * CR::ELEMS;
+          // every wave: its output tiles += the writer's 16 samples (k = sample 4g + q x split part).
+          // All 18 fragment reads are issued before the first MFMA (one LDS wait per sub-phase).
+          uint2 th[HT], tm[HT], tx[IT], ta[4][2];
+#pragma unroll
+          for (int U = 0; U < HT; ++U) {
+            th[U] = coop_tr(reg, coop_off(8, sA, 16 * U + cq));
+            tm[U] = coop_tr(reg, coop_off(9, sA, 16 * U + cq));
+          }
+#pragma unroll
+          for (int U = 0; U < IT; ++U) tx[U] = coop_tr(reg, coop_xoff<IT>(sA, 16 * U + cq));
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {  // planes r, z, n_h (dW_hh rows; r, z also dW_ih rows), n_in
+            const int ph = q == 0 ? 0 : q == 1 ? 2 : q == 2 ? 6 : 4;
+            ta[q][0] = coop_tr(reg, coop_off(ph, sA, 16 * wave + cq));
+            ta[q][1] = coop_tr(reg, coop_off(ph + 1, sA, 16 * wave + cq));
+          }
+#pragma unroll
+          for (int g3 = 0; g3 < 3; ++g3) {
+            const bf16x8 ah = cat2(ta[g3][0], ta[g3][1]);
+#pragma unroll
+            for (int U = 0; U < HT; ++U) {
+              cwh[g3][U] = mfma_bf16(ah, cat2(th[U], th[U]), cwh[g3][U]);
+              cwh[g3][U] = mfma_bf16(ah, cat2(tm[U], make_uint2(0u, 0u)), cwh[g3][U]);
+            }
+            const bf16x8 ai = g3 < 2 ? ah : cat2(ta[3][0], ta[3][1]);
+#pragma unroll
+            for (int U = 0; U < IT; ++U) cwi[g3][U] = mfma_bf16(ai, cat2(tx[U], tx[U]), cwi[g3][U]);
+          }
+        }
+      }
+#endif
     }
+    if constexpr (COOP) __syncthreads();  // the regions' last readers are done before the next head phase
 
     // ---- the tile's weight-gradient GEMMs over the history, K = L steps x 16 samples, TBP hidden
     // tiles tb (their r, z, n gate tiles) per pass over the history: dW_hh += dgh h_{j-1}^T,
@@ -793,7 +951,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       }
     };
 #pragma unroll 1
-    for (int tb0 = 0; tb0 < (D2D_GRU_ABLATE == 1 ? 0 : HT); tb0 += TBP) {
+    for (int tb0 = 0; tb0 < (COOP || D2D_GRU_ABLATE == 1 ? 0 : HT); tb0 += TBP) {
       f32x4 dwh[TBP][3][HT], dwi[TBP][3][IT];
 #pragma unroll
       for (int p = 0; p < TBP; ++p)
@@ -901,8 +1059,8 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   // ---- cross-wave sum of the register partials (fixed order, through the scratch), then the
   // workgroup's partial: registers of wave 0 + the four waves' global weight-gradient sums
   constexpr int NV = GruSAcc<HT>::NV;
-  float* red = &scr[0][0];
-  static_assert(NV * 64 <= 4 * SROWS * 16, "reduction buffer");
+  float* red = COOP ? reinterpret_cast<float*>(creg_raw) : &scr[0][0];
+  static_assert(NV * 64 <= (COOP ? CR::BYTES / 4 : 4 * SROWS * 16), "reduction buffer");
 #pragma unroll 1
   for (int w = 1; w < 4; ++w) {
     __syncthreads();
@@ -913,6 +1071,30 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   __syncthreads();
   const GruOff o(H, F, A);
   float* part = a.partial + ((size_t)blockIdx.y * N + k) * a.P;
+  if constexpr (COOP) {  // every wave writes its own dW_hh / dW_ih tiles (disjoint rows)
+#pragma unroll
+    for (int g3 = 0; g3 < 3; ++g3)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int u = 16 * wave + 4 * g + r;
+        if (u >= H) continue;
+#pragma unroll
+        for (int U = 0; U < HT; ++U) {
+          const int c = 16 * U + i;
+          if (c < H) part[o.whh + (g3 * H + u) * H + c] = cwh[g3][U][r];
+        }
+#pragma unroll
+        for (int U = 0; U < IT; ++U) {
+          const int c = 16 * U + i;
+          const float v = cwi[g3][U][r];
+          if (c < F) part[o.wih + (g3 * H + u) * F + c] = v;
+          else if (c == F) {
+            part[o.bih + g3 * H + u] = v;
+            if (g3 < 2) part[o.bhh + g3 * H + u] = v;  // b_hr / b_hz enter exactly like b_ir / b_iz
+          }
+        }
+      }
+  }
   if (wave == 0) {
     const float* wb = a.gpart + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 * WA::NV * 64;
     auto wsum = [&](int v) {
@@ -920,7 +1102,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
              wb[(3 * WA::NV + v) * 64 + lane];
     };
 #pragma unroll 1
-    for (int T = 0; T < 3 * HT; ++T)
+    for (int T = 0; T < (COOP ? 0 : 3 * HT); ++T)
 #pragma unroll
       for (int U = 0; U < HT; ++U)
 #pragma unroll
@@ -930,7 +1112,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
           if (u < H && c < H) part[o.whh + (G * H + u) * H + c] = v;
         }
 #pragma unroll 1
-    for (int T = 0; T < 3 * HT; ++T)
+    for (int T = 0; T < (COOP ? 0 : 3 * HT); ++T)
 #pragma unroll
       for (int U = 0; U < IT; ++U)
 #pragma unroll
@@ -1169,10 +1351,22 @@ static int gru_grad_blocks(int N, int64_t n_tiles) {
 // Float offsets of the grad kernel's workspace pieces (each rounded to 64 floats: 16-byte vector
 // accesses stay aligned): partials, h history, input images, head sums, head images, the per-step
 // gradient-row history, the weight-gradient sums.
+#ifndef D2D_GRU_GRAD_SPLIT
+#define D2D_GRU_GRAD_SPLIT 1  // 0: the fp32-MFMA step in the update kernel (ablation builds)
+#endif
+constexpr bool kGradSplit = D2D_GRU_GRAD_SPLIT != 0;
+
 struct GruWs {
   int64_t partial, hist, wimg, hacc, himg, ghist, gpart, total;
 };
-static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, int itp) {
+int g_gru_grad_history = 0;  // d2d_set_option(D2D_OPT_GRU_GRAD_HISTORY, 1)
+// the cooperative weight-gradient path of gru_grad_kernel (COOP): hidden tiles 4 (H in (32, 64]),
+// input tiles <= 2 (F + 1 <= 32), the compact record (bf16-exact inputs), the split step
+static bool gru_coop(int htp, int itp, bool u8) {
+  return !g_gru_grad_history && htp == 4 && itp <= 2 && u8 && D2D_GRU_GRAD_SPLIT && D2D_GRU_DH_BF16 &&
+         (D2D_GRU_ABLATE == 0 || D2D_GRU_ABLATE >= 5);
+}
+static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, int itp, bool coop) {
   auto up = [](int64_t v) { return (v + 63) / 64 * 64; };
   const int64_t waves = G * N * 4, HW = 16 * htp;
   GruWs w;
@@ -1184,8 +1378,8 @@ static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, 
   w.hacc = w.wimg + up(N * std::max<int64_t>(3 * HW * 16 * itp, 3 * htp * ci * 3 * 64 * 4));
   w.himg = w.hacc + up(waves * 64 * (htp * htp * 4 + htp * 8 + 4));
   w.ghist = w.himg + up(N * (HW * HW + 16 * HW + HW + 16));
-  w.gpart = w.ghist + up(waves * L * 5 * HW * 16);
-  w.total = w.gpart + up(waves * 64 * (3 * htp * (htp + itp) * 4));
+  w.gpart = w.ghist + (coop ? 0 : up(waves * L * 5 * HW * 16));  // COOP: no row history, no wave sums
+  w.total = w.gpart + (coop ? 0 : up(waves * 64 * (3 * htp * (htp + itp) * 4)));
   return w;
 }
 
@@ -1198,16 +1392,23 @@ extern "C" int64_t d2d_gru_grad_workspace(const d2d_gru_desc* d, int32_t T) {
   const int64_t tiles = (int64_t)T * ((d->n_envs + 15) / 16);
   const int G = gru_grad_blocks(d->n_agents, tiles);
   const GruOff o(H, d->obs_dim, A);
-  return gru_ws_layout(G, d->n_agents, o.P, d->history_len, ht, gru_input_tiles(d->obs_dim)).total;
+  return gru_ws_layout(G, d->n_agents, o.P, d->history_len, ht, gru_input_tiles(d->obs_dim),
+                       gru_coop(ht, gru_input_tiles(d->obs_dim), d->obs_format == D2D_OBS_U8)).total;
 }
 
-#ifndef D2D_GRU_GRAD_SPLIT
-#define D2D_GRU_GRAD_SPLIT 1  // 0: the fp32-MFMA step in the update kernel (ablation builds)
-#endif
-constexpr bool kGradSplit = D2D_GRU_GRAD_SPLIT != 0;
 
 template <int HT, int IT>
-static void launch_grad_kind(const GruArgs& a, dim3 grid, hipStream_t s) {
+static void launch_grad_kind(const GruArgs& a, dim3 grid, hipStream_t s, bool coop) {
+  if constexpr (HT == 4 && IT <= 2 && kGradSplit && D2D_GRU_DH_BF16) {
+    if (coop) {
+      if (a.kind == kGruBernoulli)
+        hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruBernoulli, true, true>), grid, dim3(256), 0, s, a);
+      else if (a.kind == kGruCategorical)
+        hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruCategorical, true, true>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruValue, true, true>), grid, dim3(256), 0, s, a);
+      return;
+    }
+  }
   if (a.kind == kGruBernoulli)
     hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruBernoulli, kGradSplit>), grid, dim3(256), 0, s, a);
   else if (a.kind == kGruCategorical)
@@ -1242,11 +1443,11 @@ static void launch_wih_split(const GruArgs& a, int itp, hipStream_t s) {
 }
 
 template <int HT>
-static void launch_grad_it(const GruArgs& a, int itp, dim3 grid, hipStream_t s) {
-  if (itp == 1) launch_grad_kind<HT, 1>(a, grid, s);
-  else if (itp == 2) launch_grad_kind<HT, 2>(a, grid, s);
-  else if (itp == 3) launch_grad_kind<HT, 3>(a, grid, s);
-  else launch_grad_kind<HT, 4>(a, grid, s);
+static void launch_grad_it(const GruArgs& a, int itp, dim3 grid, hipStream_t s, bool coop) {
+  if (itp == 1) launch_grad_kind<HT, 1>(a, grid, s, coop);
+  else if (itp == 2) launch_grad_kind<HT, 2>(a, grid, s, coop);
+  else if (itp == 3) launch_grad_kind<HT, 3>(a, grid, s, coop);
+  else launch_grad_kind<HT, 4>(a, grid, s, coop);
 }
 
 extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, const void* actions,
@@ -1282,7 +1483,8 @@ extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, c
   const GruOff o(a.H, a.F, a.A);
   a.P = o.P;
   const int ht = (a.H + 15) / 16, htp = ht <= 1 ? 1 : ht <= 2 ? 2 : 4, itp = gru_input_tiles(a.F);
-  const GruWs ws = gru_ws_layout(a.G, a.N, a.P, a.L, htp, itp);
+  const bool coop = gru_coop(htp, itp, a.ov.u8 != 0);
+  const GruWs ws = gru_ws_layout(a.G, a.N, a.P, a.L, htp, itp, coop);
   a.partial = workspace + ws.partial;
   a.hist = workspace + ws.hist;
   a.wimg = workspace + ws.wimg;
@@ -1313,9 +1515,9 @@ extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, c
     a.G = 1;
   } else {
     dim3 grid(a.N, a.G);
-    if (ht <= 1) launch_grad_it<1>(a, itp, grid, s);
-    else if (ht <= 2) launch_grad_it<2>(a, itp, grid, s);
-    else launch_grad_it<4>(a, itp, grid, s);
+    if (ht <= 1) launch_grad_it<1>(a, itp, grid, s, false);
+    else if (ht <= 2) launch_grad_it<2>(a, itp, grid, s, false);
+    else launch_grad_it<4>(a, itp, grid, s, coop);
     D2D_CHECK_HIP(hipGetLastError());
   }
   const int64_t n = (int64_t)a.N * a.P;

@@ -41,6 +41,7 @@ ABI_VERSION = 9
 D2D_OBS_F32, D2D_OBS_U8 = 0, 1
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
+D2D_OPT_GRU_GRAD_HISTORY = 3  # 1: d2d_gru_grad through the global row history even where the LDS path applies
 
 _p = ctypes.c_void_p
 

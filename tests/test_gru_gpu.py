@@ -254,7 +254,8 @@ def test_gru_grads_match_autograd(case):
         torch.testing.assert_close(st[:, 1], s_ref[:, 1], rtol=1e-5, atol=1e-4)
 
 
-def test_gru_grads_bitwise_reproducible_and_large():
+@pytest.mark.parametrize("fmt", ["f32", "record"])
+def test_gru_grads_bitwise_reproducible_and_large(fmt):
     """64 agents x 64-step windows (xp_load.py's history_len = n_agents) on a 4-env x 2-episode batch:
     two launches give bitwise identical gradients and loss sums (every sum is accumulated in a fixed
     order: per-wave registers, per-wave global blocks summed in wave order; no atomics), finite
@@ -270,7 +271,7 @@ def test_gru_grads_bitwise_reproducible_and_large():
     pd = {k: v.to(dev).contiguous() for k, v in p.items()}
     lo = (-torch.rand(T, E, N, generator=g) * 3).to(dev)
     W = torch.randn(T, E, N, generator=g).to(dev)
-    od = obs.to(dev).contiguous()
+    od = obs.to(dev).contiguous() if fmt == "f32" else to_record(obs)  # record: the cooperative LDS path
     g1, s1 = gru.grads(pd, od, "sigmoid", L, ep, W, actions=acts.to(dev), logp_old=lo)
     g1 = {k: v.clone() for k, v in g1.items()}
     g2, s2 = gru.grads(pd, od, "sigmoid", L, ep, W, actions=acts.to(dev), logp_old=lo)
@@ -383,8 +384,41 @@ def test_gru_policy_at_xp_load_window(mode, policy_impl):
     assert bool((err[well] <= tol[well]).all()), (err[well].max().item(), (err / tol)[well].max().item())
 
 
+def to_record(obs):
+    """The compact obs record (d2dhip/record.py) of integer-valued fp32 obs [T][E][N][F]: one byte per
+    column (int8 where a column holds negatives), the bias byte 1 at column F, zeros past it."""
+    from d2dhip.record import ObsRecord
+    T, E, N, F = obs.shape
+    R = 32 * ((F + 1 + 31) // 32)
+    v = obs.round().to(torch.int32)
+    assert torch.equal(v.float(), obs.float()), "record inputs must be integers"
+    neg = (v < 0).reshape(-1, N, F).any(0)                                        # [N][F]
+    data = torch.zeros((T, E, N, R), dtype=torch.uint8)
+    data[..., :F] = (v & 0xFF).to(torch.uint8)
+    data[..., F] = 1                                                                # the bias input
+    sgn = torch.zeros((N, R // 32), dtype=torch.int64)
+    for k in range(N):
+        for c in range(F):
+            if neg[k, c]:
+                sgn[k, c // 32] |= 1 << (c % 32)
+    sgn = torch.where(sgn >= 2 ** 31, sgn - 2 ** 32, sgn).to(torch.int32)
+    return ObsRecord(data.cuda().contiguous(), F, sgn.cuda())
+
+
+@pytest.fixture(params=["f32", "record", "record-history"])
+def grad_input(request):
+    """Rollout-buffer format of the GRU update: fp32 rows (the row-history kernel), the compact record
+    (H = 64, F + 1 <= 32: the cooperative LDS weight-gradient path), or the record through the
+    row-history kernel (D2D_OPT_GRU_GRAD_HISTORY)."""
+    from d2dhip import _lib
+    lib = _lib.require_gpu()
+    lib.d2d_set_option(_lib.D2D_OPT_GRU_GRAD_HISTORY, 1 if request.param == "record-history" else 0)
+    yield request.param
+    lib.d2d_set_option(_lib.D2D_OPT_GRU_GRAD_HISTORY, 0)
+
+
 @pytest.mark.parametrize("kind", ["sigmoid", None])
-def test_gru_grads_at_xp_load_window(kind):
+def test_gru_grads_at_xp_load_window(kind, grad_input):
     """gru_grad_kernel at the bench's window (H = 64, L = 64, 64 agents, 200-slot episode, E = 4):
     the gradients of all eight tensors vs float64 autograd over the padded training windows, with the
     fp32-band rule of test_gru_grads_match_autograd (2e-5 * max|g| where torch fp32 itself lands in
@@ -443,10 +477,11 @@ def test_gru_grads_at_xp_load_window(kind):
     r32, s32 = ref(torch.float32)
     pd = {k: v.to(dev).contiguous() for k, v in p.items()}
     W_te = W.permute(1, 2, 0).contiguous()
+    xin = obs if grad_input == "f32" else to_record(obs.cpu())
     if kind is None:
-        got, st = gru.grads(pd, obs, None, L, ep, W_te)
+        got, st = gru.grads(pd, xin, None, L, ep, W_te)
     else:
-        got, st = gru.grads(pd, obs, "sigmoid", L, ep, W_te, actions=pack_masks_torch(bits.permute(1, 2, 0, 3)),
+        got, st = gru.grads(pd, xin, "sigmoid", L, ep, W_te, actions=pack_masks_torch(bits.permute(1, 2, 0, 3)),
                             logp_old=logp_old.permute(1, 2, 0).contiguous(), clip=clip, beta=beta)
     torch.cuda.synchronize()
     well = True
