@@ -351,7 +351,7 @@ struct GruOff {
   }
 };
 
-// COOP (H in (32, 64], compact-record inputs, F + 1 <= 32; D2D_GRU_COOP): the weight gradients without
+// COOP (H in (32, 64], compact-record inputs, F + 1 <= 48): the weight gradients without
 // the global row history.  The four waves run their tiles' BPTT steps in lockstep; every step each wave
 // in turn writes its 16 samples' rows -- the r, z, n_in and n_h pre-activation gradients and h_{j-1} as
 // RNE two-way bf16 split planes, x (bf16-exact) as one -- into ONE shared LDS region, and all four waves
@@ -371,8 +371,8 @@ __device__ __forceinline__ int coop_off(int plane, int s, int c) {
   return plane * 1024 + s * 64 + (c ^ (((s >> 1) & 3) << 4));
 }
 template <int IT>
-__device__ __forceinline__ int coop_xoff(int s, int c) {
-  return CoopRegion<IT>::X + s * 16 * IT + (IT >= 2 ? (c ^ (((s >> 2) & 1) << 4)) : c);
+__device__ __forceinline__ int coop_xoff(int s, int c) {  // (the swizzle needs a power-of-two row of >= 32)
+  return CoopRegion<IT>::X + s * 16 * IT + (IT == 2 || IT == 4 ? (c ^ (((s >> 2) & 1) << 4)) : c);
 }
 typedef short v4i16_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16_t* lds_v4i16_t;
@@ -1361,9 +1361,10 @@ struct GruWs {
 };
 int g_gru_grad_history = 0;  // d2d_set_option(D2D_OPT_GRU_GRAD_HISTORY, 1)
 // the cooperative weight-gradient path of gru_grad_kernel (COOP): hidden tiles 4 (H in (32, 64]),
-// input tiles <= 2 (F + 1 <= 32), the compact record (bf16-exact inputs), the split step
+// input tiles <= 3 (F + 1 <= 48: four staging regions + the W_hh image fit the 160 KB of LDS), the
+// compact record (bf16-exact inputs), the split step
 static bool gru_coop(int htp, int itp, bool u8) {
-  return !g_gru_grad_history && htp == 4 && itp <= 2 && u8 && D2D_GRU_GRAD_SPLIT && D2D_GRU_DH_BF16 &&
+  return !g_gru_grad_history && htp == 4 && itp <= 3 && u8 && D2D_GRU_GRAD_SPLIT && D2D_GRU_DH_BF16 &&
          (D2D_GRU_ABLATE == 0 || D2D_GRU_ABLATE >= 5);
 }
 static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, int itp, bool coop) {
@@ -1399,7 +1400,7 @@ extern "C" int64_t d2d_gru_grad_workspace(const d2d_gru_desc* d, int32_t T) {
 
 template <int HT, int IT>
 static void launch_grad_kind(const GruArgs& a, dim3 grid, hipStream_t s, bool coop) {
-  if constexpr (HT == 4 && IT <= 2 && kGradSplit && D2D_GRU_DH_BF16) {
+  if constexpr (HT == 4 && IT <= 3 && kGradSplit && D2D_GRU_DH_BF16) {
     if (coop) {
       if (a.kind == kGruBernoulli)
         hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruBernoulli, true, true>), grid, dim3(256), 0, s, a);

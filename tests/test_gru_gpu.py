@@ -194,8 +194,11 @@ GRAD_CASES = [
 ]
 
 
+@pytest.mark.parametrize("fmt", ["f32", "record"])
 @pytest.mark.parametrize("case", GRAD_CASES, ids=lambda c: f"{c[0]}-N{c[1]}-F{c[2]}-H{c[3]}-A{c[4]}-L{c[5]}-ep{c[6]}")
-def test_gru_grads_match_autograd(case):
+def test_gru_grads_match_autograd(case, fmt):
+    """fmt "record": the compact record (H = 64 with F + 1 <= 48 runs the cooperative LDS
+    weight-gradient path, the other shapes the row-history kernel on the record)."""
     from d2dhip import gru
     from d2dhip.envbatch import pack_masks_torch
     kind, N, F, H, A, L, ep, T, E = case
@@ -227,7 +230,8 @@ def test_gru_grads_match_autograd(case):
     # per-sample inputs in the rollout layout [T][E][N]
     W_te = W.permute(1, 2, 0).contiguous().to(dev)
     lo_te = None if logp_old is None else logp_old.permute(1, 2, 0).contiguous().to(dev)
-    got, stats = gru.grads(pd, obs.to(dev).contiguous(), kind, L, ep, W_te,
+    xin = obs.to(dev).contiguous() if fmt == "f32" else to_record(obs)
+    got, stats = gru.grads(pd, xin, kind, L, ep, W_te,
                            actions=None if acts_dev is None else acts_dev.to(dev), logp_old=lo_te, clip=clip, beta=beta)
     torch.cuda.synchronize()
     for name in r64:
