@@ -283,6 +283,9 @@ __device__ __forceinline__ void gru_gates(const f32x4 (&rz)[2 * HT], const f32x4
 // the weight images store each A fragment with the same permuted columns: fragment (T, c, part) of
 // lane (g, i) = the 8 k-slots of row 16T + i, as one 16-byte word ([T][c][part][lane], conflict-free
 // ds_read_b128).  Odd tile counts leave the upper half of the last chunk zero on both sides.
+#ifndef D2D_GRU_ABLATE_X
+#define D2D_GRU_ABLATE_X 0  // != 0 only in tools/gpu/build_ablate_gru.sh's variant 7 (timing only)
+#endif
 // bf16 high parts of 8 floats (their exact value when the inputs are bf16-exact)
 __device__ __forceinline__ bf16x8 hi_frag_(const float (&v)[8]) {
   uint32_t u[4];
@@ -418,12 +421,74 @@ __device__ __forceinline__ f32x4 mfma_split8(const Parts& w, const Parts& x, f32
 
 // gru_preact on the split images.  x_exact (wave-uniform): every input of the step is bf16-exact
 // (always for the compact record), so the input products need only the three weight parts.
-template <int HT, int IT>
+// XEXACT: the inputs are bf16-exact by construction (the compact record) -- no per-tile branch on
+// x_exact, so the input products of all gate tiles are one basic block and their W_ih fragment loads
+// (from L2 in the update kernel) are issued together instead of one latency per gate tile.
+template <int HT, int IT, bool XEXACT = false>
 __device__ __forceinline__ void gru_preact_split(const bf16x8* wih_b, const bf16x8* whh_b, int lane,
                                                  const float (&x)[IT][4], bool x_exact, const float (&h)[HT][4],
                                                  const f32x4 (&bhn)[HT], f32x4 (&rz)[2 * HT], f32x4 (&ni)[HT],
                                                  f32x4 (&nh)[HT], bool h_zero) {
   using S = GruSplit<HT, IT>;
+  if constexpr (XEXACT) {
+    // exact inputs (the update kernel's cooperative path, W_ih fragments from L2): every W_ih fragment
+    // load is issued first, the recurrent products (LDS-fed) run while they are in flight, and the
+    // input products come last -- the L2 latency is paid once per step behind 144 MFMAs instead of at
+    // the head of the step.  The input terms are summed in their own accumulator (smallest part first,
+    // as mfma_split does) and added to the recurrent sum with one fp32 add: accumulating them into the
+    // already large recurrent sum measured 50x the torch-fp32 band on the xp_load value-critic dW_ih.
+    bf16x8 wi[S::NT][S::CI][3];
+#pragma unroll
+    for (int T = 0; T < S::NT; ++T)
+#pragma unroll
+      for (int c = 0; c < S::CI; ++c)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) wi[T][c][q] = wih_b[((T * S::CI + c) * 3) * 64 + lane + 64 * q];
+    bf16x8 xh[S::CI];
+#pragma unroll
+    for (int c = 0; c < S::CI; ++c) {
+      float v[8];
+      chunk_vals<IT>(v, x, c);
+      xh[c] = hi_frag_(v);
+    }
+    f32x4 acc[S::NT];
+#pragma unroll
+    for (int T = 0; T < S::NT; ++T) acc[T] = T < 2 * HT ? f32x4{0.f, 0.f, 0.f, 0.f} : bhn[T - 2 * HT];
+    if (!h_zero) {
+      const int hl = whh_slot(lane);
+      Parts hp[S::CH];
+#pragma unroll
+      for (int c = 0; c < S::CH; ++c) {
+        float v[8];
+        chunk_vals<HT>(v, h, c);
+        hp[c] = split3(v);
+      }
+#pragma unroll
+      for (int T = 0; T < S::NT; ++T)
+#pragma unroll
+        for (int c = 0; c < S::CH; ++c) {
+          const bf16x8* wf = whh_b + ((T * S::CH + c) * 3) * 64 + hl;
+          acc[T] = mfma_split(Parts{wf[0], wf[64], wf[128]}, hp[c], false, acc[T]);
+        }
+    }
+#pragma unroll
+    for (int T = 0; T < S::NT; ++T) {
+      f32x4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < (D2D_GRU_ABLATE_X ? 0 : S::CI); ++c) {
+        a = mfma_bf16(wi[T][c][2], xh[c], a);
+        a = mfma_bf16(wi[T][c][1], xh[c], a);
+        a = mfma_bf16(wi[T][c][0], xh[c], a);
+      }
+      if (T < 2 * HT) {
+        rz[T] = a + acc[T];
+      } else {
+        ni[T - 2 * HT] = a;
+        nh[T - 2 * HT] = acc[T];
+      }
+    }
+    return;
+  }
   Parts xp[S::CI];
 #pragma unroll
   for (int c = 0; c < S::CI; ++c) {
@@ -440,7 +505,7 @@ __device__ __forceinline__ void gru_preact_split(const bf16x8* wih_b, const bf16
   for (int T = 0; T < S::NT; ++T) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < S::CI; ++c) {
+    for (int c = 0; c < (D2D_GRU_ABLATE_X ? 0 : S::CI); ++c) {  // (timing ablation: no input products)
       const bf16x8* wf = wih_b + ((T * S::CI + c) * 3) * 64 + lane;
       acc = mfma_split(Parts{wf[0], wf[64], wf[128]}, xp[c], x_exact, acc);
     }

@@ -525,7 +525,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     f32x4 rz[2 * HT], ni[HT], nh[HT];
     const int z = opaque_zero();
     if constexpr (SPLIT)
-      gru_preact_split<HT, IT>(wih_g + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), h, bhn, rz, ni, nh, j == 0);
+      gru_preact_split<HT, IT, COOP>(wih_g + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), h, bhn, rz, ni, nh, j == 0);
     else
       gru_preact<HT, IT, false>(wimg + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
     gru_gates<HT>(rz, ni, nh, h);
@@ -579,7 +579,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
       if constexpr (SPLIT)
-        gru_preact_split<HT, IT>(wih_g + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), h, bhn, rz, ni, nh, j == 0);
+        gru_preact_split<HT, IT, COOP>(wih_g + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), h, bhn, rz, ni, nh, j == 0);
       else
         gru_preact<HT, IT, false>(wimg + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
       gru_gates<HT>(rz, ni, nh, h);
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       }
 #else
       if constexpr (SPLIT)
-        gru_preact_split<HT, IT>(wih_g + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), hp, bhn, rz, ni, nh, j == 0);
+        gru_preact_split<HT, IT, COOP>(wih_g + z, whh_b + z, lane, x, x_exact_step<IT>(a.ov, x), hp, bhn, rz, ni, nh, j == 0);
       else
         gru_preact<HT, IT, false>(wimg + z, whh_s + z, oi, oh, x, hp, bhn, rz, ni, nh, g, i, j == 0);
 #endif
@@ -860,7 +860,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
           __syncthreads();
         }
 #pragma unroll 1
-        for (int src = 0; src < (D2D_GRU_ABLATE >= 5 ? 0 : 4); ++src) {  // (ablation 5: barriers and writes only)
+        for (int src = 0; src < (D2D_GRU_ABLATE == 5 || D2D_GRU_ABLATE == 6 ? 0 : 4); ++src) {  // (ablation 5: barriers and writes only)
           const uint16_t* reg = creg + src * CR::ELEMS;
           // every wave: its output tiles += the writer's 16 samples (k = sample 4g + q x split part).
           // All 18 fragment reads are issued before the first MFMA (one LDS wait per sub-phase).
