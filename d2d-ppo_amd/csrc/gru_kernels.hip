@@ -482,9 +482,11 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   for (int v = 0; v < GruHeadAcc<HT>::NV; ++v) hacc[v * 64 + lane] = 0.f;
   using WA = GruWAcc<HT, IT>;
   float* ghist = a.ghist + wave_id * (size_t)L * 5 * HW * 16;
-  float* gpart = a.gpart + wave_id * (size_t)WA::NV * 64;
-  if constexpr (!COOP)
-    for (int v = 0; v < WA::NV; ++v) gpart[v * 64 + lane] = 0.f;
+  // per-wave weight-gradient sums in global memory: the row-history GEMMs' (!COOP), or (COOP) the
+  // running sums the cooperative accumulators are flushed into after every tile
+  constexpr int NVC = (3 * HT + 3 * IT) * 4;  // COOP: this wave's 3 HT + 3 IT output tiles, 4 values per lane
+  float* gpart = a.gpart + wave_id * (size_t)(COOP ? NVC : WA::NV) * 64;
+  for (int v = 0; v < (COOP ? NVC : WA::NV); ++v) gpart[v * 64 + lane] = 0.f;
   // COOP: this wave's output tiles, all tiles of the kernel: dW_hh [gate g3][column tile U] and dW_ih
   // [g3][input tile U] of gate rows 16 (4 g3 + wave) + 4g + r
   f32x4 cwh[COOP ? 3 : 1][COOP ? HT : 1], cwi[COOP ? 3 : 1][COOP ? IT : 1];
@@ -894,7 +896,32 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       }
 #endif
     }
-    if constexpr (COOP) __syncthreads();  // the regions' last readers are done before the next head phase
+    if constexpr (COOP) {
+      __syncthreads();  // the regions' last readers are done before the next head phase
+      // flush the tile's sums into the wave's running sums (one fp32 add per tile): MFMA accumulation of
+      // every tile of the kernel into the same registers measured 2x the float64 band at 64 envs
+      float d[NVC];
+      int v = 0;
+#pragma unroll
+      for (int g3 = 0; g3 < 3; ++g3) {
+#pragma unroll
+        for (int U = 0; U < HT; ++U)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) d[v++] = cwh[g3][U][r];
+#pragma unroll
+        for (int U = 0; U < IT; ++U)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) d[v++] = cwi[g3][U][r];
+      }
+      rmw_block(gpart, lane, 0, d);
+#pragma unroll
+      for (int g3 = 0; g3 < 3; ++g3) {
+#pragma unroll
+        for (int U = 0; U < HT; ++U) cwh[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int U = 0; U < IT; ++U) cwi[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
 
     // ---- the tile's weight-gradient GEMMs over the history, K = L steps x 16 samples, TBP hidden
     // tiles tb (their r, z, n gate tiles) per pass over the history: dW_hh += dgh h_{j-1}^T,
@@ -1071,22 +1098,23 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   __syncthreads();
   const GruOff o(H, F, A);
   float* part = a.partial + ((size_t)blockIdx.y * N + k) * a.P;
-  if constexpr (COOP) {  // every wave writes its own dW_hh / dW_ih tiles (disjoint rows)
+  if constexpr (COOP) {  // every wave writes its own dW_hh / dW_ih tiles (disjoint rows) from its sums
 #pragma unroll
     for (int g3 = 0; g3 < 3; ++g3)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int u = 16 * wave + 4 * g + r;
         if (u >= H) continue;
+        const int v0 = g3 * (HT + IT) * 4;
 #pragma unroll
         for (int U = 0; U < HT; ++U) {
           const int c = 16 * U + i;
-          if (c < H) part[o.whh + (g3 * H + u) * H + c] = cwh[g3][U][r];
+          if (c < H) part[o.whh + (g3 * H + u) * H + c] = gpart[(v0 + 4 * U + r) * 64 + lane];
         }
 #pragma unroll
         for (int U = 0; U < IT; ++U) {
           const int c = 16 * U + i;
-          const float v = cwi[g3][U][r];
+          const float v = gpart[(v0 + 4 * (HT + U) + r) * 64 + lane];
           if (c < F) part[o.wih + (g3 * H + u) * F + c] = v;
           else if (c == F) {
             part[o.bih + g3 * H + u] = v;
@@ -1379,8 +1407,9 @@ static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, 
   w.hacc = w.wimg + up(N * std::max<int64_t>(3 * HW * 16 * itp, 3 * htp * ci * 3 * 64 * 4));
   w.himg = w.hacc + up(waves * 64 * (htp * htp * 4 + htp * 8 + 4));
   w.ghist = w.himg + up(N * (HW * HW + 16 * HW + HW + 16));
-  w.gpart = w.ghist + (coop ? 0 : up(waves * L * 5 * HW * 16));  // COOP: no row history, no wave sums
-  w.total = w.gpart + (coop ? 0 : up(waves * 64 * (3 * htp * (htp + itp) * 4)));
+  w.gpart = w.ghist + (coop ? 0 : up(waves * L * 5 * HW * 16));  // COOP: no row history
+  // wave sums: all dW tiles per wave (history), or (COOP) the wave's own 3 (HT + IT) tiles
+  w.total = w.gpart + up(waves * 64 * (coop ? 3 * (htp + itp) * 4 : 3 * htp * (htp + itp) * 4));
   return w;
 }
 

@@ -429,12 +429,26 @@ def test_gru_grads_at_xp_load_window(kind, grad_input):
     that band, else within 4x torch fp32's distance to float64).  The reference is accumulated over
     slot chunks (every loss is a sum of per-sample terms, so chunked backward passes add up to the
     full gradient)."""
+    xp_grads_check(kind, grad_input, XP["E"])
+
+
+@pytest.mark.parametrize("kind", ["sigmoid", None])
+def test_gru_grads_large_batch_record(kind):
+    """The cooperative path keeps one accumulator per output tile across all of a wave's tiles: at 64
+    envs (50 tiles x 64 steps x 4 regions of MFMA accumulation per wave) its gradients still meet the
+    float64 band rule of the xp_load test."""
+    xp_grads_check(kind, "record", 64)
+
+
+def xp_grads_check(kind, grad_input, E, check=True):
+    """The body of test_gru_grads_at_xp_load_window at E envs; returns {tensor: (err64, band, max|g|)}
+    (check=False: no assertions; tools/gpu/gru_coop_vs_history.py runs it at the bench's 256 envs)."""
     from algorithms._core import gru_window
     from d2dhip import gru
     from d2dhip.envbatch import pack_masks_torch
     from torch.distributions import Bernoulli
     c = XP
-    N, F, H, A, L, ep, T, E = (c[k] for k in ("N", "F", "H", "A", "L", "ep", "T", "E"))
+    N, F, H, A, L, ep, T = (c[k] for k in ("N", "F", "H", "A", "L", "ep", "T"))
     A = 1 if kind is None else A  # the value network: Linear(H, 1) head (the RNN critic, ippo.py:146)
     p, dims = make_net(N, F, H, A, seed=31)
     dev = "cuda"
@@ -489,18 +503,24 @@ def test_gru_grads_at_xp_load_window(kind, grad_input):
                             logp_old=logp_old.permute(1, 2, 0).contiguous(), clip=clip, beta=beta)
     torch.cuda.synchronize()
     well = True
+    errs = {}
     for name in r64:
         gk = got[name].double()
         scale = r64[name].abs().max().item()
         err64 = (gk - r64[name]).abs().max().item()
         band = (r32[name] - r64[name]).abs().max().item()
+        errs[name] = (err64, band, scale)
         print(f"  {name}: max|g| {scale:.3e}  |kernel-f64| {err64:.2e}  |torchf32-f64| {band:.2e}")
+        if not check:
+            continue
         tol = 2e-5 * scale + 1e-7
         if band <= tol:
             assert err64 <= tol, (name, err64, tol)
         else:
             well = False
             assert err64 <= 4 * band, (name, err64, band)
+    if not check:
+        return errs
     s_ref = s64 if well else s32
     torch.testing.assert_close(st.double()[:, 0], s_ref[:, 0], rtol=1e-5, atol=1e-4)
     if kind is not None:
