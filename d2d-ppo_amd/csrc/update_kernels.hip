@@ -61,8 +61,8 @@
 #define D2D_UPD_WAVES 2  // waves per SIMD the update kernels are register-budgeted for (KC = 1)
 #endif
 #ifndef D2D_LOGITS_BF16
-// logits Z^T = W2 . relu(HT) on bf16 MFMAs: W2's three-way split against a two-way RNE split of
-// relu(HT) (<= 2^-17 relative per product), 3 x 16 instead of 4 x 32 MFMA cycles per hidden tile
+// logits Z^T = W2 . relu(HT) on bf16 MFMAs: W2's three-way split against a three-way RNE split of
+// relu(HT) (every product term down to 2^-24), 3 x 16 instead of 4 x 32 MFMA cycles per hidden tile
 // (actor kernel 2.55 -> 2.44 ms per 26 M agent-samples); 0 = v_mfma_f32_16x16x4_f32 (exact fmaf chain)
 #define D2D_LOGITS_BF16 1
 #endif
@@ -123,16 +123,54 @@ __device__ __forceinline__ uint32_t bf16_lo_as_f32bits(uint32_t h) { return __bu
 struct Parts2x4 {
   uint32_t h[2], m[2];
 };
+// a packed bf16 pair back as two floats; the residual subtractions of a pair then issue as one
+// v_pk_add_f32 (float2 arithmetic) instead of two v_sub_f32
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2v bf16_pair_f32(uint32_t h) {
+  return f32x2v{ffrom(bf16_lo_as_f32bits(h)), ffrom(h & 0xFFFF0000u)};
+}
 __device__ __forceinline__ Parts2x4 split2_4(const float (&v)[4]) {
   Parts2x4 o;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    const uint32_t h = rne2(v[2 * p], v[2 * p + 1]);
+    const f32x2v x = {v[2 * p], v[2 * p + 1]};
+    const uint32_t h = rne2(x.x, x.y);
+    const f32x2v r = x - bf16_pair_f32(h);
     o.h[p] = h;
-    o.m[p] = rne2(v[2 * p] - ffrom(bf16_lo_as_f32bits(h)), v[2 * p + 1] - ffrom(h & 0xFFFF0000u));
+    o.m[p] = rne2(r.x, r.y);
   }
   return o;
 }
+// Three-way round-to-nearest split of 4 floats (v = h + m + l + e, |e| <= 2^-26 |v|): the two-way
+// split plus the remainder's part
+__device__ __forceinline__ Parts4 split3rne_4(const float (&v)[4]) {
+  Parts4 o;
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const f32x2v x = {v[2 * p], v[2 * p + 1]};
+    const uint32_t h = rne2(x.x, x.y);
+    const f32x2v r = x - bf16_pair_f32(h);
+    const uint32_t m = rne2(r.x, r.y);
+    const f32x2v r2 = r - bf16_pair_f32(m);
+    o.h[p] = h;
+    o.m[p] = m;
+    o.l[p] = rne2(r2.x, r2.y);
+  }
+  return o;
+}
+// Compensated (Kahan) running sum of per-tile sums: the scalar gradient and loss accumulators of
+// one lane add one tile sum per tile, 10^3-10^4 of them at the headline batch, where a plain fp32
+// running sum drifts by ~n ulps (measured: the critic's db2 at 65,536 envs, 20x torch fp32's error)
+struct KahanSum {
+  float s = 0.f, c = 0.f;
+  __device__ __forceinline__ void add(float x) {
+    const float y = x - c;
+    const float t = s + y;
+    c = (t - s) - y;
+    s = t;
+  }
+  __device__ __forceinline__ float value() const { return s; }
+};
 
 // bf16 1.0 / 0.0 for h > 0 (the relu derivative, torch's convention at 0) of two values, packed; from
 // relu(h) (relu() above: the bit pattern is > 0 exactly when h > 0), one v_min_u32 each
@@ -342,7 +380,7 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
   // the four consecutive registers the MFMA reads (no operand assembly moves)
   __shared__ __attribute__((aligned(16))) bf16x8 w2b_s[HT][3][64];
 #if D2D_LOGITS_BF16
-  __shared__ __attribute__((aligned(16))) bf16x8 w2z_s[HT][3][64];       // Z^T's bf16 A operands [h|h], [m|m], [l|0]
+  __shared__ __attribute__((aligned(16))) bf16x8 w2z_s[HT][3][64];       // Z^T's bf16 A operands [h|h], [m|m], [h|l]
 #else
   __shared__ __attribute__((aligned(16))) float w2f_s[HT][64][4];        // Z^T's fp32 A operand
 #endif
@@ -388,10 +426,9 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
 #else
       {
         const Parts4 pz = split3_4(wz);
-        const uint32_t zero2[2] = {0u, 0u};
         w2z_s[t][0][lane] = cat(pz.h, pz.h);
         w2z_s[t][1][lane] = cat(pz.m, pz.m);
-        w2z_s[t][2][lane] = cat(pz.l, zero2);
+        w2z_s[t][2][lane] = cat(pz.h, pz.l);
       }
 #endif
     }
@@ -407,7 +444,7 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
 #pragma unroll
     for (int q = 0; q < QT; ++q) dw1[t][q] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  f32x4 db2 = {0.f, 0.f, 0.f, 0.f};
+  KahanSum db2[4];
   float surr_acc = 0.f, ent_acc = 0.f;
 
   // per-wave LDS: the obs tile row-major (fp32; TR: its bf16 high parts, exact for the record) and
@@ -519,13 +556,16 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
             z = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[r], relu(ht[t2][r]), z, 0, 0, 0);
 #endif
 #else
-          {  // relu(HT) on a two-way RNE split in the k-slots [h_h | h_m] against W2's h, m, l parts
+          {  // relu(HT) on a three-way RNE split: k-slots [h_h | h_m] against W2's [h|h], [m|m] parts and
+             // [h_l | h_h] against [h|l] -- every product down to 2^-24 in 3 MFMAs (the two-way split
+             // alone leaves ~2^-18 per logit, which the PPO gradient's cancellation over 10^5-10^7
+             // samples amplified to ~2e-5 of max|g| at the headline batch)
             float hv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) hv[r] = relu(ht[t2][r]);
-            const Parts2x4 hp = split2_4(hv);
-            const bf16x8 bh = cat(hp.h, hp.m);
-            z = mfma_bf16(w2z_s[t2][2][lane], bh, z);
+            const Parts4 hp = split3rne_4(hv);
+            const bf16x8 bh = cat(hp.h, hp.m), bl = cat(hp.l, hp.h);
+            z = mfma_bf16(w2z_s[t2][2][lane], bl, z);
             z = mfma_bf16(w2z_s[t2][1][lane], bh, z);
             z = mfma_bf16(w2z_s[t2][0][lane], bh, z);
             if constexpr (TR) {
@@ -552,7 +592,8 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
 #else
         const f32x4 dzc = ppo_dz<KIND, true, false, AFIX>(a, zc, cur.act[0], cur.lo[0], cur.w[0], e < a.E, g & 1, surr_acc, ent_acc);
 #endif
-        db2 += dzc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) db2[r].add(dzc[r]);
         *reinterpret_cast<f32x4*>(&zb[g >> 1][i][4 * (g & 1)]) = dzc;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -565,7 +606,8 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
         for (int s = 0; s < 2; ++s) {
           const int e = e0 + 16 * s + i;
           dz[s] = ppo_dz<KIND, false>(a, zt[s], cur.act[s], cur.lo[s], cur.w[s], e < a.E, g, surr_acc, ent_acc);
-          db2 += dz[s];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) db2[r].add(dz[s][r]);
           *reinterpret_cast<f32x4*>(&zb[s][i][4 * g]) = dz[s];
         }
       }
@@ -737,7 +779,7 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[n++] = dw2[t][r];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[n++] = db2[r];
+    for (int r = 0; r < 4; ++r) acc[n++] = db2[r].value();
     acc[n++] = surr_acc;
     acc[n++] = ent_acc;
   }
@@ -839,14 +881,13 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_critic_g
   const float c2 = a.b2[k];
 
   f32x4 dv1[HT][QT];
-  float dv2[HT];
+  KahanSum dv2[HT];
 #pragma unroll
   for (int t = 0; t < HT; ++t) {
-    dv2[t] = 0.f;
 #pragma unroll
     for (int q = 0; q < QT; ++q) dv1[t][q] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  float dc2 = 0.f, loss_acc = 0.f;
+  KahanSum dc2, loss_acc;
   constexpr int XS = 32 * KC + 4;  // row stride = 4 mod 16 floats: sample-on-k reads hit 64 banks
   __shared__ __attribute__((aligned(16))) float xs[4][32][XS];
   constexpr int NV = HT * QT * 4 + HT + 2;
@@ -894,6 +935,10 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_critic_g
       uint32_t mk[HT][2][2];  // relu' of HV as bf16 pairs [t2][half][r pair]
       float dvh[2][4];        // dL/dv of samples 16s + 4g + r
 #endif
+      // this tile's sums of dL/db2, the loss and dL/dv2, added to the running sums once per tile
+      float tdc = 0.f, tls = 0.f, tv2[HT];
+#pragma unroll
+      for (int t2 = 0; t2 < HT; ++t2) tv2[t2] = 0.f;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         // HV = X . V1^T (sample 16s + 4g + r on rows, hidden 16t + i on lanes)
@@ -937,8 +982,8 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_critic_g
           // per-lane selects) and the partial keeps lane i = 0's sums (the same values and order)
           const float d = ok ? v - R[s][r] : 0.f;
           dvs[r] = 2.f * a.scale * d;
-          loss_acc += d * d;
-          dc2 += dvs[r];
+          tls = fmaf(d, d, tls);
+          tdc += dvs[r];
         }
 #if D2D_CRITIC_MASK
 #pragma unroll
@@ -947,7 +992,7 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_critic_g
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             hr[r] = relu(hv[t2][r]);
-            dv2[t2] = fmaf(dvs[r], hr[r], dv2[t2]);
+            tv2[t2] = fmaf(dvs[r], hr[r], tv2[t2]);
           }
 #pragma unroll
           for (int p = 0; p < 2; ++p) mk[t2][s][p] = relu_mask_pair(hr[2 * p], hr[2 * p + 1]);
@@ -1000,7 +1045,7 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_critic_g
           float dh[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            dv2[t2] = fmaf(dvs[r], relu(hv[t2][r]), dv2[t2]);
+            tv2[t2] = fmaf(dvs[r], relu(hv[t2][r]), tv2[t2]);
             dh[r] = hv[t2][r] > 0.f ? dvs[r] * v2f[t2] : 0.f;
           }
           const Parts2x4 dp = split2_4(dh);
@@ -1015,6 +1060,10 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_critic_g
         }
       }
 #endif
+      dc2.add(tdc);
+      loss_acc.add(tls);
+#pragma unroll
+      for (int t2 = 0; t2 < HT; ++t2) dv2[t2].add(tv2[t2]);
     };
     CriticIn<KC, U8> in;
     bool deferred = false;
@@ -1061,9 +1110,9 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_critic_g
 #endif
         }
 #pragma unroll
-    for (int t = 0; t < HT; ++t) acc[n++] = dv2[t];
-    acc[n++] = dc2;
-    acc[n++] = loss_acc;
+    for (int t = 0; t < HT; ++t) acc[n++] = dv2[t].value();
+    acc[n++] = dc2.value();
+    acc[n++] = loss_acc.value();
   }
   reduce_waves<NV>(acc, red, wave, lane);
   if (wave != 0) return;
@@ -1125,10 +1174,17 @@ static int64_t tensor_extent(const int64_t (&st)[3], int T, int E, int N) {
   return 1 + (int64_t)(T - 1) * st[0] + (int64_t)(E - 1) * st[1] + (int64_t)(N - 1) * st[2];
 }
 
+// Workgroups per agent: about 4 per CU over the whole grid, at least one tile per wave, and at most
+// kMaxWaveTiles tiles per wave.  A wave sums its tiles' weight gradients in MFMA accumulators, an
+// fp32 chain whose rounding error grows with its length: at the 65,536-env batch 16 workgroups per
+// agent left 6,400 tiles per wave and dW2 at 4x torch fp32's error against float64
+// (tools/gpu/ppo_grads_full_batch.py); the G partials are summed by update_reduce_kernel (G x N x P
+// floats, 0.26 GB at that batch).
+constexpr int64_t kMaxWaveTiles = 256;
 static int update_blocks(int N, int64_t n_tiles) {
-  // about 4 workgroups per CU over the whole grid, at least one tile per wave
-  int G = (int)std::max<int64_t>(1, std::min<int64_t>((1024 + N - 1) / N, (n_tiles + 3) / 4));
-  return G;
+  const int64_t fill = (1024 + N - 1) / N, cap = (n_tiles + 4 * kMaxWaveTiles - 1) / (4 * kMaxWaveTiles);
+  // (grid.y <= 65535: past that, more tiles per wave)
+  return (int)std::max<int64_t>(1, std::min<int64_t>({std::max(fill, cap), (n_tiles + 3) / 4, 65535}));
 }
 
 extern "C" int64_t d2d_ppo_workspace(int32_t n_agents, int32_t T, int32_t n_envs, int32_t obs_dim, int32_t hidden,

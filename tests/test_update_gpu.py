@@ -361,3 +361,26 @@ def test_happo_chain_kernel_matches_torch_loop():
         assert lib.d2d_happo_chain(N, T, E, adv.data_ptr(), lp_new.contiguous().data_ptr(), lp_old.data_ptr(),
                                    pt.data_ptr(), M.data_ptr(), _lib.stream_ptr()) == 0
         torch.testing.assert_close(M, ref, rtol=2e-6, atol=0)
+
+
+def test_grads_on_large_rollout_vs_float64():
+    """iPPO's fused actor and critic gradients on a real 8,192-env x 200-slot rollout of the c3 config
+    (64 agents x 8 channels, 1.6 M samples per agent: 51,200 tiles, 50 workgroups per agent, 256 tiles
+    per wave -- the longest accumulation chain update_blocks allows at any batch) against float64
+    autograd, agents 0 and 1: every tensor within max(4x torch fp32's own error, 2e-5) of max|g|.
+    (tools/gpu/ppo_grads_full_batch.py runs the same comparison at the 65,536-env headline batch.)"""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "gpu"))
+    from ppo_grads_full_batch import grads_vs_float64
+    out = grads_vs_float64(8192, (0, 1), emulate=False)
+    checked = 0
+    for key, err in out.items():
+        if key.count("/") != 2 or "torch32" in key:
+            continue
+        net, k, n = key.split("/")
+        band = out[f"{net}_torch32/{k}/{n}"]
+        print(f"  {key}: kernel {err:.2e}  torch fp32 {band:.2e}")
+        assert err <= max(4 * band, 2e-5), (key, err, band)
+        checked += 1
+    assert checked == 16

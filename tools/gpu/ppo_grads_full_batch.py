@@ -1,0 +1,120 @@
+"""Accuracy of the fused PPO gradient kernels at the headline batch (parity at the sizes the
+bench times): iPPO, 64 agents x 8 channels, E envs (default 65,536) x 200 slots on the compact record,
+the actor and critic gradients of agents 0..K-1 against float64 autograd of the reference losses
+(ippo.py:194-216: clipped surrogate + 0.01 entropy with Bernoulli(softmax) per channel; MSE value loss),
+accumulated over sample chunks.  Prints max |kernel - f64| / max |g| per tensor, and the same for fp32 torch autograd over the same
+chunks (the fp32 band the kernels are held to).
+The kernels' accumulation chains are long here: at 65,536 envs 409,600 32-sample tiles per agent, at
+most 256 per wave since round 3 (update_blocks); tests/test_update_gpu.py runs the comparison at 8,192 envs.
+usage (GPU box): python3 tools/gpu/ppo_grads_full_batch.py [E] [K]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "d2d-ppo_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def split2(v):
+    """v rounded to the kernels' two-way round-to-nearest bf16 split h + m (update_kernels.hip split2_4)."""
+    h = v.float().to(torch.bfloat16).to(v.dtype)
+    return h + (v.float() - h.float()).to(torch.bfloat16).to(v.dtype)
+
+
+def grads_vs_float64(E, agents, emulate=True, seed=11):
+    """Relative errors {"<net>/<agent>/<param>": max |g - g64| / max |g64|} of the kernels ("actor",
+    "critic"), of torch fp32 autograd ("actor_torch32", "critic_torch32") and, with emulate, of float64
+    with one kernel rounding emulated ("actor_emu_dh": dH on the two-way split of the dW1 operand;
+    "actor_emu_h": relu(H) on the two-way split in the logits)."""
+    import bench
+    from algorithms.ippo import iPPO
+    from d2dhip.update import actor_grads, critic_grads
+    from envs.combinatorial_env import CombinatorialEnv
+    env = CombinatorialEnv(**bench.config3_params(200), n_envs=E, device="cuda:0", seed=seed)
+    torch.manual_seed(3)
+    np.random.seed(3)
+    lr = iPPO(env, hidden_size=64, gamma=0.6, policy_lr=3e-4, value_lr=1e-3, device=env.batch().device,
+              combinatorial=True, early_stopping=False)
+    ro = lr._rollout(E)
+    pp = {k: v.data.contiguous() for k, v in lr.policy.params.items()}
+    vp = {k: v.data.contiguous() for k, v in lr.value.params.items()}
+    ga, _ = actor_grads(pp, ro.obs, ro.actions, ro.logp.permute(0, 2, 1), ro.adv_tne.permute(0, 2, 1), "comb",
+                        clip=0.1, beta=0.01)
+    ga = {k: v.double().clone() for k, v in ga.items()}
+    gc, _ = critic_grads(vp, ro.obs, ro.ret_tne.permute(0, 2, 1))
+    gc = {k: v.double().clone() for k, v in gc.items()}
+    torch.cuda.synchronize()
+    T = ro.T
+    B = T * E
+    C = env.batch().spec.C
+    rec = ro.obs
+    F = rec.obs_dim
+    sg = (rec.signed.to(torch.int64) & 0xFFFFFFFF)
+    out = {"E": E, "T": T, "samples_per_agent": B}
+    for k in agents:
+        cols = torch.arange(F, device="cuda")
+        neg = ((sg[k, cols // 32] >> (cols % 32)) & 1).bool()
+        q = {n: v[k].double().clone().requires_grad_() for n, v in pp.items()}
+        qv = {n: v[k].double().clone().requires_grad_() for n, v in vp.items()}
+        q32 = {n: v[k].clone().requires_grad_() for n, v in pp.items()}
+        qv32 = {n: v[k].clone().requires_grad_() for n, v in vp.items()}
+        qe1 = {n: v[k].double().clone().requires_grad_() for n, v in pp.items()}
+        qe2 = {n: v[k].double().clone().requires_grad_() for n, v in pp.items()}
+        runs = [(torch.float64, q, qv, 0), (torch.float32, q32, qv32, 0)]
+        if emulate:
+            runs += [(torch.float64, qe1, None, 1), (torch.float64, qe2, None, 2)]
+        chunk = max(1, (1 << 21) // E)
+        for t0 in range(0, T, chunk):
+            sl = slice(t0, min(T, t0 + chunk))
+            d = rec.data[sl, :, k, :F]
+            for dt, qa, qc, emu in runs:
+                x = torch.where(neg, d.view(torch.int8).to(dt), d.to(dt)).reshape(-1, F)
+                bits = ((ro.actions[sl, :, k].to(torch.int64).unsqueeze(-1) >> torch.arange(C, device="cuda")) & 1)
+                bits = bits.reshape(-1, C).to(dt)
+                lo = ro.logp[sl, k, :].to(dt).reshape(-1)
+                adv = ro.adv_tne[sl, k, :].to(dt).reshape(-1)
+                ret = ro.ret_tne[sl, k, :].to(dt).reshape(-1)
+                pre = x @ qa["w1"].t() + qa["b1"]
+                if emu == 1:  # dH on the kernel's two-way RNE bf16 split (the dW1 / db1 operand)
+                    pre.register_hook(split2)
+                h = torch.relu(pre)
+                if emu == 2:  # relu(H) on the two-way split in the logits (before round 3's three-way split)
+                    h = h + (split2(h) - h).detach()
+                probs = torch.softmax(h @ qa["w2"].t() + qa["b2"], -1)
+                dist = torch.distributions.Bernoulli(probs=probs, validate_args=False)
+                ratio = torch.exp(dist.log_prob(bits).mean(-1) - lo)
+                surr = torch.min(ratio * adv, torch.clamp(ratio, 0.9, 1.1) * adv)
+                (-(surr.sum() / B) - 0.01 * dist.entropy().mean(-1).sum() / B).backward()
+                if qc is None:
+                    continue
+                hv = torch.relu(x @ qc["w1"].t() + qc["b1"])
+                v = (hv @ qc["w2"].t() + qc["b2"])[:, 0]
+                (((v - ret) ** 2).sum() / B).backward()
+        tags = [("actor_torch32", q32)] + ([("actor_emu_dh", qe1), ("actor_emu_h", qe2)] if emulate else [])
+        for n in q:
+            ref = q[n].grad
+            out[f"actor/{k}/{n}"] = float((ga[n][k] - ref).abs().max() / ref.abs().max())
+            for tag, qq in tags:
+                out[f"{tag}/{k}/{n}"] = float((qq[n].grad.double() - ref).abs().max() / ref.abs().max())
+        for n in qv:
+            ref = qv[n].grad
+            out[f"critic/{k}/{n}"] = float((gc[n][k] - ref).abs().max() / ref.abs().max())
+            out[f"critic_torch32/{k}/{n}"] = float((qv32[n].grad.double() - ref).abs().max() / ref.abs().max())
+    return out
+
+
+if __name__ == "__main__":
+    E = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    K = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    out = grads_vs_float64(E, range(K))
+    print(json.dumps(out), flush=True)
+    summ = {}
+    for kk, vv in out.items():
+        if kk.count("/") == 2:
+            tag, _, n = kk.split("/")
+            summ.setdefault(f"{tag}/{n}", []).append(vv)
+    res = {"E": E, "T": out["T"], "agents": K, "samples_per_agent": out["samples_per_agent"]}
+    res.update({kk: {"max": max(vv), "median": float(np.median(vv))} for kk, vv in sorted(summ.items())})
+    print(json.dumps(res), flush=True)
