@@ -57,6 +57,12 @@
 // instead of dHv (32), the relu' select and the dv * v2 products go, and v2 scales the sums once
 #define D2D_CRITIC_MASK 1
 #endif
+#ifndef D2D_LOGITS_SPLIT3
+#define D2D_LOGITS_SPLIT3 1  // 0 (timing A/B only): relu(HT) on the two-way split in the logits
+#endif
+#ifndef D2D_SPLIT_DOT2
+#define D2D_SPLIT_DOT2 1  // 0 (timing A/B only): split residuals on v_perm + v_and + v_pk_add_f32
+#endif
 #ifndef D2D_UPD_WAVES
 #define D2D_UPD_WAVES 2  // waves per SIMD the update kernels are register-budgeted for (KC = 1)
 #endif
@@ -123,21 +129,41 @@ __device__ __forceinline__ uint32_t bf16_lo_as_f32bits(uint32_t h) { return __bu
 struct Parts2x4 {
   uint32_t h[2], m[2];
 };
-// a packed bf16 pair back as two floats; the residual subtractions of a pair then issue as one
-// v_pk_add_f32 (float2 arithmetic) instead of two v_sub_f32
-typedef float f32x2v __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2v bf16_pair_f32(uint32_t h) {
-  return f32x2v{ffrom(bf16_lo_as_f32bits(h)), ffrom(h & 0xFFFF0000u)};
+// v minus the low / high bf16 of a packed pair on one v_dot2c_f32_bf16 (h.lo * -1 + h.hi * 0 + v):
+// the split residuals, exact (v - h is representable: h is v rounded to 8 bits); replaces the pair's
+// unpacking (v_perm + v_and) and subtraction.  The (-1, 0) / (0, -1) bf16 pairs are held in SGPRs: the
+// compiler encodes 0x0000BF80 as the inline constant -1.0, which the hardware does not read as that
+// pair (tools/gpu/probe/dot2_probe.hip: 65,487 of 65,536 residuals wrong; register and 32-bit literal
+// forms exact on all)
+__device__ __forceinline__ uint32_t bf16_pair_neg1_lo() {
+  uint32_t c;
+  asm("s_mov_b32 %0, 0x0000bf80" : "=s"(c));
+  return c;
+}
+__device__ __forceinline__ uint32_t bf16_pair_neg1_hi() {
+  uint32_t c;
+  asm("s_mov_b32 %0, 0xbf800000" : "=s"(c));
+  return c;
+}
+__device__ __forceinline__ float sub_bf16_lo(float v, uint32_t h) {
+#if !D2D_SPLIT_DOT2
+  return v - ffrom(bf16_lo_as_f32bits(h));
+#endif
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, h), __builtin_bit_cast(bf16x2_t, bf16_pair_neg1_lo()), v, false);
+}
+__device__ __forceinline__ float sub_bf16_hi(float v, uint32_t h) {
+#if !D2D_SPLIT_DOT2
+  return v - ffrom(h & 0xFFFF0000u);
+#endif
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, h), __builtin_bit_cast(bf16x2_t, bf16_pair_neg1_hi()), v, false);
 }
 __device__ __forceinline__ Parts2x4 split2_4(const float (&v)[4]) {
   Parts2x4 o;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    const f32x2v x = {v[2 * p], v[2 * p + 1]};
-    const uint32_t h = rne2(x.x, x.y);
-    const f32x2v r = x - bf16_pair_f32(h);
+    const uint32_t h = rne2(v[2 * p], v[2 * p + 1]);
     o.h[p] = h;
-    o.m[p] = rne2(r.x, r.y);
+    o.m[p] = rne2(sub_bf16_lo(v[2 * p], h), sub_bf16_hi(v[2 * p + 1], h));
   }
   return o;
 }
@@ -147,14 +173,12 @@ __device__ __forceinline__ Parts4 split3rne_4(const float (&v)[4]) {
   Parts4 o;
 #pragma unroll
   for (int p = 0; p < 2; ++p) {
-    const f32x2v x = {v[2 * p], v[2 * p + 1]};
-    const uint32_t h = rne2(x.x, x.y);
-    const f32x2v r = x - bf16_pair_f32(h);
-    const uint32_t m = rne2(r.x, r.y);
-    const f32x2v r2 = r - bf16_pair_f32(m);
+    const uint32_t h = rne2(v[2 * p], v[2 * p + 1]);
+    const float r0 = sub_bf16_lo(v[2 * p], h), r1 = sub_bf16_hi(v[2 * p + 1], h);
+    const uint32_t m = rne2(r0, r1);
     o.h[p] = h;
     o.m[p] = m;
-    o.l[p] = rne2(r2.x, r2.y);
+    o.l[p] = rne2(sub_bf16_lo(r0, m), sub_bf16_hi(r1, m));
   }
   return o;
 }
@@ -376,11 +400,11 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
   // half per hidden tile) in LDS, shared by the workgroup's four waves
   Parts w1p[HT][KC];
   f32x4 b2i;
-  // dH's three B operands [l|h], [m|h], [h|m], stored whole so one ds_read_b128 lands each in
+  // dH's three B operands [h|l], [m|h], [h|m], stored whole so one ds_read_b128 lands each in
   // the four consecutive registers the MFMA reads (no operand assembly moves)
   __shared__ __attribute__((aligned(16))) bf16x8 w2b_s[HT][3][64];
 #if D2D_LOGITS_BF16
-  __shared__ __attribute__((aligned(16))) bf16x8 w2z_s[HT][3][64];       // Z^T's bf16 A operands [h|h], [m|m], [h|l]
+  __shared__ __attribute__((aligned(16))) bf16x8 w2z_s[HT][3][64];       // Z^T's bf16 A operands [h|h], [m|m], [l|h]
 #else
   __shared__ __attribute__((aligned(16))) float w2f_s[HT][64][4];        // Z^T's fp32 A operand
 #endif
@@ -410,7 +434,7 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
 #pragma unroll
       for (int j = 0; j < 4; ++j) wb[j] = (hok && 4 * g + j < A) ? W2[(size_t)(4 * g + j) * H + hrow] : 0.f;
       const Parts4 p4 = split3_4(wb);
-      w2b_s[t][0][lane] = cat(p4.l, p4.h);
+      w2b_s[t][0][lane] = cat(p4.h, p4.l);
       w2b_s[t][1][lane] = cat(p4.m, p4.h);
       w2b_s[t][2][lane] = cat(p4.h, p4.m);
       // A operand of Z^T = W2 . relu(HT): row = action i, k = hidden 16t + 4g + r
@@ -428,7 +452,11 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
         const Parts4 pz = split3_4(wz);
         w2z_s[t][0][lane] = cat(pz.h, pz.h);
         w2z_s[t][1][lane] = cat(pz.m, pz.m);
-        w2z_s[t][2][lane] = cat(pz.h, pz.l);
+#if D2D_LOGITS_SPLIT3
+        w2z_s[t][2][lane] = cat(pz.l, pz.h);
+#else
+        w2z_s[t][2][lane] = cat(pz.l, pz.l);
+#endif
       }
 #endif
     }
@@ -556,15 +584,22 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
             z = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[r], relu(ht[t2][r]), z, 0, 0, 0);
 #endif
 #else
-          {  // relu(HT) on a three-way RNE split: k-slots [h_h | h_m] against W2's [h|h], [m|m] parts and
-             // [h_l | h_h] against [h|l] -- every product down to 2^-24 in 3 MFMAs (the two-way split
+          {  // relu(HT) on a three-way RNE split: k-slots [h_m | h_h] against W2's [h|h], [m|m] parts and
+             // [h_h | h_l] against [l|h] -- every product down to 2^-24 in 3 MFMAs (the two-way split
              // alone leaves ~2^-18 per logit, which the PPO gradient's cancellation over 10^5-10^7
              // samples amplified to ~2e-5 of max|g| at the headline batch)
             float hv[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) hv[r] = relu(ht[t2][r]);
+#if D2D_LOGITS_SPLIT3
             const Parts4 hp = split3rne_4(hv);
-            const bf16x8 bh = cat(hp.h, hp.m), bl = cat(hp.l, hp.h);
+            // (part order m, h, l: the two operands can share h's registers)
+            const bf16x8 bh = cat(hp.m, hp.h), bl = cat(hp.h, hp.l);
+#else
+            const Parts2x4 hp = split2_4(hv);
+            const uint32_t z2[2] = {0u, 0u};
+            const bf16x8 bh = cat(hp.m, hp.h), bl = cat(hp.h, z2);
+#endif
             z = mfma_bf16(w2z_s[t2][2][lane], bl, z);
             z = mfma_bf16(w2z_s[t2][1][lane], bh, z);
             z = mfma_bf16(w2z_s[t2][0][lane], bh, z);
@@ -657,8 +692,9 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
           }
         }
         const float dv[4] = {dz[s][0], dz[s][1], dz[s][2], dz[s][3]};
-        const Parts4 zp = split3_4(dv);
-        const bf16x8 a_hm = cat(zp.h, zp.m), a_hl = cat(zp.h, zp.l);
+        const Parts4 zp = split3rne_4(dv);
+        // (part order l, h, m: the two operands can share h's registers)
+        const bf16x8 a_hm = cat(zp.h, zp.m), a_hl = cat(zp.l, zp.h);
 #pragma unroll
         for (int t2 = 0; t2 < HT; ++t2) {
           if constexpr (TR) {
