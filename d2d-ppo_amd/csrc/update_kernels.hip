@@ -1216,7 +1216,10 @@ static int64_t tensor_extent(const int64_t (&st)[3], int T, int E, int N) {
 // agent left 6,400 tiles per wave and dW2 at 4x torch fp32's error against float64
 // (tools/gpu/ppo_grads_full_batch.py); the G partials are summed by update_reduce_kernel (G x N x P
 // floats, 0.26 GB at that batch).
-constexpr int64_t kMaxWaveTiles = 256;
+#ifndef D2D_UPD_MAX_WAVE_TILES
+#define D2D_UPD_MAX_WAVE_TILES 256
+#endif
+constexpr int64_t kMaxWaveTiles = D2D_UPD_MAX_WAVE_TILES;
 static int update_blocks(int N, int64_t n_tiles) {
   const int64_t fill = (1024 + N - 1) / N, cap = (n_tiles + 4 * kMaxWaveTiles - 1) / (4 * kMaxWaveTiles);
   // (grid.y <= 65535: past that, more tiles per wave)
