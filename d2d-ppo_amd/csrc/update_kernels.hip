@@ -63,6 +63,12 @@
 #ifndef D2D_SPLIT_DOT2
 #define D2D_SPLIT_DOT2 1  // 0 (timing A/B only): split residuals on v_perm + v_and + v_pk_add_f32
 #endif
+#ifndef D2D_DW2_PAIRED
+// record-path actor: dW2^T = relu(H)^T . dZ over both 16-sample halves at once, k-slots = 4 samples of
+// half 0 | the same 4 of half 1: (h_h, h_m) x (dz_h, dz_m) in 3 MFMAs per hidden tile instead of 2 x 2
+// with the duplicated [dz_h | dz_h] and zero-padded [dz_m | 0] operands
+#define D2D_DW2_PAIRED 1
+#endif
 #ifndef D2D_UPD_WAVES
 #define D2D_UPD_WAVES 2  // waves per SIMD the update kernels are register-budgeted for (KC = 1)
 #endif
@@ -181,6 +187,12 @@ __device__ __forceinline__ Parts4 split3rne_4(const float (&v)[4]) {
     o.l[p] = rne2(sub_bf16_lo(r0, m), sub_bf16_hi(r1, m));
   }
   return o;
+}
+// two transposing LDS reads (four bf16 each, element 0 in the low half) as one MFMA operand
+__device__ __forceinline__ bf16x8 cat_tr(v4i16 a, v4i16 b) {
+  const uint2 x = __builtin_bit_cast(uint2, a), y = __builtin_bit_cast(uint2, b);
+  const u32x4v v = {x.x, x.y, y.x, y.y};
+  return __builtin_bit_cast(bf16x8, v);
 }
 // Compensated (Kahan) running sum of per-tile sums: the scalar gradient and loss accumulators of
 // one lane add one tile sum per tile, 10^3-10^4 of them at the headline batch, where a plain fp32
@@ -704,11 +716,6 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
             uint16_t* im = trimg + (((wave * 2 + s) * HT + t2) * 2) * 256 + (4 * g + (i >> 2)) * 16 + 4 * (i & 3);
             typedef __attribute__((address_space(3))) v4i16* lds_v4i16;
             const v4i16 th = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(im));
-            const v4i16 tm = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(im + 256));
-            const uint32_t hh[2] = {(uint16_t)th[0] | ((uint32_t)(uint16_t)th[1] << 16),
-                                    (uint16_t)th[2] | ((uint32_t)(uint16_t)th[3] << 16)};
-            const uint32_t mm[2] = {(uint16_t)tm[0] | ((uint32_t)(uint16_t)tm[1] << 16),
-                                    (uint16_t)tm[2] | ((uint32_t)(uint16_t)tm[3] << 16)};
             f32x4 acc = mfma_bf16(a_hl, w2b_s[t2][0][lane], f32x4{0.f, 0.f, 0.f, 0.f});
             acc = mfma_bf16(a_hm, w2b_s[t2][1][lane], acc);
             acc = mfma_bf16(a_hm, w2b_s[t2][2][lane], acc);
@@ -717,9 +724,12 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
             float dh[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) dh[r] = th[r] != 0 ? acc[r] : 0.f;
-            const bf16x8 h_hm = cat(hh, mm);
+#if !D2D_DW2_PAIRED
+            const v4i16 tm = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(im + 256));
+            const bf16x8 h_hm = cat_tr(th, tm);
             dw2[t2] = mfma_bf16(h_hm, bz2, dw2[t2]);
             dw2[t2] = mfma_bf16(h_hm, bz1, dw2[t2]);
+#endif
             const Parts2x4 dp = split2_4(dh);
             const bf16x8 d_hm = cat(dp.h, dp.m);
 #pragma unroll
@@ -770,6 +780,33 @@ __global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_gr
           }
         }
       }
+#if D2D_DW2_PAIRED
+      if constexpr (TR) {
+        // dW2^T += relu(H)^T . dZ for both halves: lane (g, i) k-slots = samples 4g .. 4g + 3 of half 0,
+        // then the same of half 1 (relu(HT)'s parts from the transposed image, dZ from its LDS transpose)
+        float d0[4], d1[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          d0[r] = zb[0][4 * g + r][i];
+          d1[r] = zb[1][4 * g + r][i];
+        }
+        const Parts2x4 z0 = split2_4(d0), z1 = split2_4(d1);
+        const bf16x8 bzh = cat(z0.h, z1.h), bzm = cat(z0.m, z1.m);
+#pragma unroll
+        for (int t2 = 0; t2 < HT; ++t2) {
+          typedef __attribute__((address_space(3))) v4i16* lds_v4i16;
+          uint16_t* im0 = trimg + (((wave * 2 + 0) * HT + t2) * 2) * 256 + (4 * g + (i >> 2)) * 16 + 4 * (i & 3);
+          uint16_t* im1 = trimg + (((wave * 2 + 1) * HT + t2) * 2) * 256 + (4 * g + (i >> 2)) * 16 + 4 * (i & 3);
+          const bf16x8 ah = cat_tr(__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(im0)),
+                                   __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(im1)));
+          const bf16x8 am = cat_tr(__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(im0 + 256)),
+                                   __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(im1 + 256)));
+          dw2[t2] = mfma_bf16(ah, bzm, dw2[t2]);  // h_h dz_m
+          dw2[t2] = mfma_bf16(am, bzh, dw2[t2]);  // h_m dz_h
+          dw2[t2] = mfma_bf16(ah, bzh, dw2[t2]);  // h_h dz_h
+        }
+      }
+#endif
     };
     // Exact tiles run the branch-free XE body as they stream by (one tile of look-ahead: the
     // next tile's loads are issued as soon as this tile is staged); a tile with fractional inputs
