@@ -64,10 +64,12 @@
 #define D2D_SPLIT_DOT2 1  // 0 (timing A/B only): split residuals on v_perm + v_and + v_pk_add_f32
 #endif
 #ifndef D2D_DW2_PAIRED
-// record-path actor: dW2^T = relu(H)^T . dZ over both 16-sample halves at once, k-slots = 4 samples of
-// half 0 | the same 4 of half 1: (h_h, h_m) x (dz_h, dz_m) in 3 MFMAs per hidden tile instead of 2 x 2
-// with the duplicated [dz_h | dz_h] and zero-padded [dz_m | 0] operands
-#define D2D_DW2_PAIRED 1
+// 1 (A/B only): record-path actor dW2^T = relu(H)^T . dZ over both 16-sample halves at once, k-slots =
+// 4 samples of half 0 | the same 4 of half 1: (h_h, h_m) x (dz_h, dz_m) in 3 MFMAs per hidden tile instead
+// of 2 x 2 with the duplicated [dz_h | dz_h] and zero-padded [dz_m | 0] operands.  ~1.5 % faster, but its
+// summation order differs from the fp32-row instantiation's, whose gradients the record path reproduces
+// bit for bit (tests/test_record_gpu.py); off
+#define D2D_DW2_PAIRED 0
 #endif
 #ifndef D2D_UPD_WAVES
 #define D2D_UPD_WAVES 2  // waves per SIMD the update kernels are register-budgeted for (KC = 1)
