@@ -74,7 +74,7 @@ __device__ __forceinline__ f32x4 ppo_dz(const Args& a, f32x4 z, uint32_t act, fl
     logp = group_sum<HALF>(lsum) * lA;
     ent = group_sum<HALF>(esum) * lA;
     const float ratio = __expf(logp - lo);
-    const float cr = fminf(fmaxf(ratio, a.clip_lo), a.clip_hi);
+    const float cr = __builtin_amdgcn_fmed3f(ratio, a.clip_lo, a.clip_hi);  // clamp: one v_med3_f32
     const float s1 = ratio * W, s2 = cr * W;
     const bool gate = (ratio >= a.clip_lo && ratio <= a.clip_hi) || s1 < s2;
     const float coef = gate ? -a.scale * ratio * W * a.inv_A : 0.f;
@@ -121,7 +121,7 @@ __device__ __forceinline__ f32x4 ppo_dz(const Args& a, f32x4 z, uint32_t act, fl
     logp = group_sum<HALF>(lsel);
     ent = -group_sum<HALF>(esum);
     const float ratio = __expf(logp - lo);
-    const float cr = fminf(fmaxf(ratio, a.clip_lo), a.clip_hi);
+    const float cr = __builtin_amdgcn_fmed3f(ratio, a.clip_lo, a.clip_hi);  // clamp: one v_med3_f32
     const float s1 = ratio * W, s2 = cr * W;
     const bool gate = (ratio >= a.clip_lo && ratio <= a.clip_hi) || s1 < s2;
     const float coef = gate ? -a.scale * ratio * W : 0.f;
