@@ -23,11 +23,14 @@ def split2(v):
     return h + (v.float() - h.float()).to(torch.bfloat16).to(v.dtype)
 
 
-def grads_vs_float64(E, agents, emulate=True, seed=11):
+def grads_vs_float64(E, agents, emulate=True, seed=11, reversed_fp32=False):
     """Relative errors {"<net>/<agent>/<param>": max |g - g64| / max |g64|} of the kernels ("actor",
     "critic"), of torch fp32 autograd ("actor_torch32", "critic_torch32") and, with emulate, of float64
     with one kernel rounding emulated ("actor_emu_dh": dH on the two-way split of the dW1 operand;
-    "actor_emu_h": relu(H) on the two-way split in the logits)."""
+    "actor_emu_h": relu(H) on the two-way split in the logits); with reversed_fp32, torch fp32 autograd
+    with the layer-1 inputs summed in reverse column order ("actor_torch32r": another, equally valid
+    fp32 rounding) and the number of (sample, hidden) relu masks each fp32 forward gets wrong against
+    float64 ("mask_flips32/<k>", "mask_flips32r/<k>")."""
     import bench
     from algorithms.ippo import iPPO
     from d2dhip.update import actor_grads, critic_grads
@@ -62,7 +65,11 @@ def grads_vs_float64(E, agents, emulate=True, seed=11):
         qv32 = {n: v[k].clone().requires_grad_() for n, v in vp.items()}
         qe1 = {n: v[k].double().clone().requires_grad_() for n, v in pp.items()}
         qe2 = {n: v[k].double().clone().requires_grad_() for n, v in pp.items()}
+        q32r = {n: v[k].clone().requires_grad_() for n, v in pp.items()}
         runs = [(torch.float64, q, qv, 0), (torch.float32, q32, qv32, 0)]
+        if reversed_fp32:
+            runs += [(torch.float32, q32r, None, 3)]
+        flips = [0, 0]
         if emulate:
             runs += [(torch.float64, qe1, None, 1), (torch.float64, qe2, None, 2)]
         chunk = max(1, (1 << 21) // E)
@@ -76,7 +83,14 @@ def grads_vs_float64(E, agents, emulate=True, seed=11):
                 lo = ro.logp[sl, k, :].to(dt).reshape(-1)
                 adv = ro.adv_tne[sl, k, :].to(dt).reshape(-1)
                 ret = ro.ret_tne[sl, k, :].to(dt).reshape(-1)
-                pre = x @ qa["w1"].t() + qa["b1"]
+                if emu == 3:  # fp32 with the input columns summed in reverse order
+                    pre = x.flip(-1) @ qa["w1"].flip(-1).t() + qa["b1"]
+                else:
+                    pre = x @ qa["w1"].t() + qa["b1"]
+                if reversed_fp32 and dt == torch.float32:
+                    with torch.no_grad():
+                        ref_pre = x.double() @ pp["w1"][k].double().t() + pp["b1"][k].double()
+                        flips[emu == 3] += int(((pre > 0) != (ref_pre > 0)).sum())
                 if emu == 1:  # dH on the kernel's two-way RNE bf16 split (the dW1 / db1 operand)
                     pre.register_hook(split2)
                 h = torch.relu(pre)
@@ -93,6 +107,9 @@ def grads_vs_float64(E, agents, emulate=True, seed=11):
                 v = (hv @ qc["w2"].t() + qc["b2"])[:, 0]
                 (((v - ret) ** 2).sum() / B).backward()
         tags = [("actor_torch32", q32)] + ([("actor_emu_dh", qe1), ("actor_emu_h", qe2)] if emulate else [])
+        if reversed_fp32:
+            tags += [("actor_torch32r", q32r)]
+            out[f"mask_flips32/{k}"], out[f"mask_flips32r/{k}"] = flips
         for n in q:
             ref = q[n].grad
             out[f"actor/{k}/{n}"] = float((ga[n][k] - ref).abs().max() / ref.abs().max())
@@ -108,7 +125,7 @@ def grads_vs_float64(E, agents, emulate=True, seed=11):
 if __name__ == "__main__":
     E = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     K = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    out = grads_vs_float64(E, range(K))
+    out = grads_vs_float64(E, range(K), reversed_fp32=len(sys.argv) > 3 and sys.argv[3] == "reversed")
     print(json.dumps(out), flush=True)
     summ = {}
     for kk, vv in out.items():
