@@ -15,6 +15,7 @@
 // obs/state rows are staged in LDS and written back as contiguous float4
 // streams, so every HBM write is a full-line coalesced store.
 // Randomness: recorded draws (replay, parity) or Philox4x32-10 (production).
+#include <atomic>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -1140,11 +1141,11 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
 }  // namespace
 
 extern int g_policy_f32_mfma;  // policy_kernels.hip
-extern int g_gru_grad_history;  // gru_kernels.hip
+extern std::atomic<int> g_gru_grad_history;  // gru_kernels.hip
 
 extern "C" int d2d_set_option(int32_t option, int32_t value) {
   if (option == D2D_OPT_GRU_GRAD_HISTORY) {
-    g_gru_grad_history = value ? 1 : 0;
+    g_gru_grad_history.store(value ? 1 : 0, std::memory_order_relaxed);
     return D2D_OK;
   }
   if (option == D2D_OPT_NT_STORES) {

@@ -17,6 +17,7 @@
 //    GEMM passes over it (K = window steps x 16 samples) add dW_hh / dW_ih into per-wave sums; the
 //    head's gradients are per-wave sums too; one partial per (workgroup, agent), summed in fixed
 //    order by gru_reduce_kernel (no atomics).
+#include <atomic>
 #include <algorithm>
 #include <cmath>
 
@@ -1387,12 +1388,16 @@ constexpr bool kGradSplit = D2D_GRU_GRAD_SPLIT != 0;
 struct GruWs {
   int64_t partial, hist, wimg, hacc, himg, ghist, gpart, total;
 };
-int g_gru_grad_history = 0;  // d2d_set_option(D2D_OPT_GRU_GRAD_HISTORY, 1)
+// d2d_set_option(D2D_OPT_GRU_GRAD_HISTORY, 1).  Atomic, and read ONCE per workspace query / launch: the
+// option selects the workspace layout, so it must be set before the query that sizes the caller's
+// buffer; d2d_gru_grad re-derives the size from its own snapshot and refuses (EINVAL) a buffer sized
+// for the other layout instead of overrunning it.
+std::atomic<int> g_gru_grad_history{0};
 // the cooperative weight-gradient path of gru_grad_kernel (COOP): hidden tiles 4 (H in (32, 64]),
 // input tiles <= 3 (F + 1 <= 48: four staging regions + the W_hh image fit the 160 KB of LDS), the
-// compact record (bf16-exact inputs), the split step
-static bool gru_coop(int htp, int itp, bool u8) {
-  return !g_gru_grad_history && htp == 4 && itp <= 3 && u8 && D2D_GRU_GRAD_SPLIT && D2D_GRU_DH_BF16 &&
+// compact record (bf16-exact inputs), the split step; `history` = the option's snapshot
+static bool gru_coop(int htp, int itp, bool u8, bool history) {
+  return !history && htp == 4 && itp <= 3 && u8 && D2D_GRU_GRAD_SPLIT && D2D_GRU_DH_BF16 &&
          (D2D_GRU_ABLATE == 0 || D2D_GRU_ABLATE >= 5);
 }
 static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, int itp, bool coop) {
@@ -1416,14 +1421,18 @@ static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, 
 // 16-column input tiles of the x operand (the inputs and the bias column F): F + 1 <= 64
 static int gru_input_tiles(int F) { return F + 1 <= 16 ? 1 : F + 1 <= 32 ? 2 : F + 1 <= 48 ? 3 : 4; }
 
-extern "C" int64_t d2d_gru_grad_workspace(const d2d_gru_desc* d, int32_t T) {
+static int64_t gru_grad_workspace(const d2d_gru_desc* d, int32_t T, bool history) {
   if (!d || d->n_agents <= 0 || T <= 0 || d->n_envs <= 0 || d->hidden < 1 || d->history_len < 1) return 0;
   const int A = d->kind == 2 ? 1 : d->n_out, H = d->hidden, ht = H <= 16 ? 1 : H <= 32 ? 2 : 4;
   const int64_t tiles = (int64_t)T * ((d->n_envs + 15) / 16);
   const int G = gru_grad_blocks(d->n_agents, tiles);
   const GruOff o(H, d->obs_dim, A);
   return gru_ws_layout(G, d->n_agents, o.P, d->history_len, ht, gru_input_tiles(d->obs_dim),
-                       gru_coop(ht, gru_input_tiles(d->obs_dim), d->obs_format == D2D_OBS_U8)).total;
+                       gru_coop(ht, gru_input_tiles(d->obs_dim), d->obs_format == D2D_OBS_U8, history)).total;
+}
+
+extern "C" int64_t d2d_gru_grad_workspace(const d2d_gru_desc* d, int32_t T) {
+  return gru_grad_workspace(d, T, g_gru_grad_history.load(std::memory_order_relaxed) != 0);
 }
 
 
@@ -1496,9 +1505,11 @@ extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, c
     d2d_set_error("d2d_gru_grad: T=%d is not a whole number of %d-slot episodes", T, d->episode_length);
     return D2D_EINVAL;
   }
-  const int64_t need = d2d_gru_grad_workspace(d, T);
+  const bool history = g_gru_grad_history.load(std::memory_order_relaxed) != 0;  // one snapshot per launch
+  const int64_t need = gru_grad_workspace(d, T, history);
   if (workspace_floats < need) {
-    d2d_set_error("workspace %lld < %lld floats", (long long)workspace_floats, (long long)need);
+    d2d_set_error("workspace %lld < %lld floats (D2D_OPT_GRU_GRAD_HISTORY=%d: set the option before the "
+                  "d2d_gru_grad_workspace query)", (long long)workspace_floats, (long long)need, (int)history);
     return D2D_EINVAL;
   }
   GruArgs a = make_gru_args(d, T, obs);
@@ -1513,7 +1524,7 @@ extern "C" int d2d_gru_grad(const d2d_gru_desc* d, int32_t T, const void* obs, c
   const GruOff o(a.H, a.F, a.A);
   a.P = o.P;
   const int ht = (a.H + 15) / 16, htp = ht <= 1 ? 1 : ht <= 2 ? 2 : 4, itp = gru_input_tiles(a.F);
-  const bool coop = gru_coop(htp, itp, a.ov.u8 != 0);
+  const bool coop = gru_coop(htp, itp, a.ov.u8 != 0, history);
   const GruWs ws = gru_ws_layout(a.G, a.N, a.P, a.L, htp, itp, coop);
   a.partial = workspace + ws.partial;
   a.hist = workspace + ws.hist;

@@ -142,7 +142,12 @@ struct Parts2x4 {
 // unpacking (v_perm + v_and) and subtraction.  The (-1, 0) / (0, -1) bf16 pairs are held in SGPRs: the
 // compiler encodes 0x0000BF80 as the inline constant -1.0, which the hardware does not read as that
 // pair (tools/gpu/probe/dot2_probe.hip: 65,487 of 65,536 residuals wrong; register and 32-bit literal
-// forms exact on all)
+// forms exact on all).  Contract: both values of the pair are finite.  The partner enters as h.x * 0, so
+// an inf / NaN partner makes the finite value's residual NaN (the per-value subtraction kept them apart);
+// the operands split here (relu(HT), dH, dZ, dv x) are finite for finite weights and inputs, and a
+// non-finite one already makes its gradient tensor non-finite through h itself, as in torch autograd.
+// Denormal values (|v| < 2^-126) may lose their residual (the probe prints what the hardware does):
+// an absolute error below 1.2e-38 per operand, far under any gradient's fp32 resolution.
 __device__ __forceinline__ uint32_t bf16_pair_neg1_lo() {
   uint32_t c;
   asm("s_mov_b32 %0, 0x0000bf80" : "=s"(c));

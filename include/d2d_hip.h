@@ -374,7 +374,10 @@ int d2d_gru_grad(const d2d_gru_desc* desc, int32_t T, const void* obs, const voi
  * D2D_OPT_POLICY_F32_MFMA: 1 = d2d_policy_mlp_step on v_mfma_f32_16x16x4_f32 instead of the
  *   default exact-split bf16 MFMA kernel (both fp32-accurate; for A/B timing and tests).
  * D2D_OPT_GRU_GRAD_HISTORY: 1 = d2d_gru_grad accumulates the weight gradients through the per-wave
- *   global row history also where the cooperative LDS path applies (ABI 9; A/B timing and tests). */
+ *   global row history also where the cooperative LDS path applies (ABI 9; A/B timing and tests).  It
+ *   selects the workspace layout: set it before the d2d_gru_grad_workspace query that sizes the buffer
+ *   (d2d_gru_grad re-checks the size against its own snapshot of the option and returns D2D_EINVAL
+ *   for a buffer sized under the other setting). */
 enum { D2D_OPT_NT_STORES = 1, D2D_OPT_POLICY_F32_MFMA = 2, D2D_OPT_GRU_GRAD_HISTORY = 3 };
 int d2d_set_option(int32_t option, int32_t value);
 

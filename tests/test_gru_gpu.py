@@ -341,10 +341,28 @@ def test_gru_policy_at_xp_load_window(mode, policy_impl):
     actions reproduces their log-probs bit for bit and they match float64 to the tolerance), the
     test()-time deterministic mode (p > 0.5 decisions exact away from ties), and D2D-PPO's forced
     log-prob pass over the padded training windows."""
+    xp_policy_check(mode, XP)
+
+
+# xp_n_agents.py:98-112's GRU learners take history_len = n_agents: at the c5 sweep's 128 and 256 agents
+# (C = 8, D = 7 -> 23 inputs) the windows are longer than the policy kernel's 63-step padding table
+# (gru_kernels.hip kGruPadTab), so the padding steps run inside every window, and L = 256 > the 200-slot
+# episode makes every rollout window start at the episode start.
+LONG = [dict(N=128, F=23, H=64, A=8, L=128, ep=200, T=200, E=4),
+        dict(N=256, F=23, H=64, A=8, L=256, ep=200, T=200, E=4)]
+
+
+@pytest.mark.parametrize("c", LONG, ids=lambda c: f"N{c['N']}-L{c['L']}")
+@pytest.mark.parametrize("mode", ["sampled", "deterministic", "forced_padded"])
+def test_gru_policy_long_window(mode, c, policy_impl):
+    """As test_gru_policy_at_xp_load_window, at history_len = n_agents = 128 / 256 (xp_n_agents)."""
+    xp_policy_check(mode, c)
+
+
+def xp_policy_check(mode, c):
     from d2dhip import gru
     from d2dhip.envbatch import pack_masks_torch
     from torch.distributions import Bernoulli
-    c = XP
     N, F, H, A, L, ep, T, E = (c[k] for k in ("N", "F", "H", "A", "L", "ep", "T", "E"))
     p, dims = make_net(N, F, H, A, seed=21)
     dev = "cuda"
@@ -356,7 +374,7 @@ def test_gru_policy_at_xp_load_window(mode, policy_impl):
     pd = {k: v.to(dev).contiguous() for k, v in p.items()}
     if mode == "deterministic":
         margin = (probs - 0.5).abs().min(-1).values                                  # [N][T][E]
-        for t in (0, 1, 63, 64, 150, T - 1):
+        for t in sorted({0, 1, 63, 64, min(L, T - 1), 150, T - 1}):
             a_t, _ = gru.policy(pd, obs, "sigmoid", L, ep, t, 1, deterministic=True)
             want = pack_masks_torch((probs[:, t] > 0.5).permute(1, 0, 2))             # [E][N]
             clear = (margin[:, t] > 1e-5).t()
@@ -440,14 +458,22 @@ def test_gru_grads_large_batch_record(kind):
     xp_grads_check(kind, "record", 64)
 
 
-def xp_grads_check(kind, grad_input, E, check=True):
+@pytest.mark.parametrize("c", LONG, ids=lambda c: f"N{c['N']}-L{c['L']}")
+@pytest.mark.parametrize("kind", ["sigmoid", None])
+def test_gru_grads_long_window(kind, c, grad_input):
+    """gru_grad_kernel at history_len = n_agents = 128 / 256 (xp_n_agents.py:98-112): all eight gradient
+    tensors vs float64 autograd over the padded training windows, the band rule of the xp_load test."""
+    xp_grads_check(kind, grad_input, c["E"], cfg=c)
+
+
+def xp_grads_check(kind, grad_input, E, check=True, cfg=None):
     """The body of test_gru_grads_at_xp_load_window at E envs; returns {tensor: (err64, band, max|g|)}
     (check=False: no assertions; tools/gpu/gru_coop_vs_history.py runs it at the bench's 256 envs)."""
     from algorithms._core import gru_window
     from d2dhip import gru
     from d2dhip.envbatch import pack_masks_torch
     from torch.distributions import Bernoulli
-    c = XP
+    c = cfg or XP
     N, F, H, A, L, ep, T = (c[k] for k in ("N", "F", "H", "A", "L", "ep", "T"))
     A = 1 if kind is None else A  # the value network: Linear(H, 1) head (the RNN critic, ippo.py:146)
     p, dims = make_net(N, F, H, A, seed=31)

@@ -20,7 +20,11 @@ normalises every element by its own gradient history (its first step is
 lr * g / (|g| + eps), i.e. +-lr whatever |g| is), so an element whose gradient
 is within that error of zero moves by up to 2 lr on either sign, while one whose
 |g| is far above it moves exactly as the reference's does.  Per element and step
-the bound is 2 lr min(1, 2e-5 max|g| / |g|); see adam_tolerance().
+the bound is 2 lr min(1, 2e-5 max|g| / |g|) with g the REFERENCE's gradient of that
+step (recorded by tools/gen_fixtures.py as grads/<net>/step<j>/<param>), so an
+implementation gradient wrongly near zero cannot loosen its own bound; see
+ref_adam_tolerance().  The first step's gradients (both learners at the fixture's
+initial weights) are also compared with the reference's directly.
 """
 import glob
 import json
@@ -92,20 +96,37 @@ class GradRecorder:
         key = view.untyped_storage().data_ptr()
         return sum(2 * lr_ for lr_, grads in self.steps if key in grads)
 
-    def tolerance(self, view, rel_err=2e-5, base=1e-5):
-        """Per-element bound for a parameter view (an agent module's tensor inside a stacked one)."""
-        tol = torch.full(view.shape, base, dtype=torch.float64)
+    def steps_of(self, view):
         key = view.untyped_storage().data_ptr()
-        for lr_, grads in self.steps:
-            if key not in grads:
-                continue
-            g, off = grads[key]
-            gv = torch.as_strided(g, view.size(), view.stride(), view.storage_offset() - off).double().cpu()
-            err = rel_err * gv.abs().max().item()  # the agent's own tensor
-            # an exactly-zero gradient (an input column that is always 0, a hidden unit dead on every
-            # sample) is zero in any arithmetic: Adam leaves the element where it was, in both runs
-            tol += torch.where(gv == 0, torch.zeros_like(gv), 2 * lr_ * torch.clamp(err / gv.abs().clamp(min=1e-30), max=1.0))
-        return tol.numpy()
+        return [grads[key] for _, grads in self.steps if key in grads]
+
+    def grad_at(self, view, j):
+        """The gradient of a parameter view at its j-th recorded optimizer step (float64, CPU)."""
+        g, off = self.steps_of(view)[j]
+        return torch.as_strided(g, view.size(), view.stride(), view.storage_offset() - off).double().cpu()
+
+
+def ref_grads(z, tag):
+    """The reference's per-step gradients of one net: [{param: ndarray}] in step order."""
+    steps = []
+    j = 0
+    while any(k.startswith(f"grads/{tag}/step{j}/") for k in z.files):
+        pre = f"grads/{tag}/step{j}/"
+        steps.append({k[len(pre):]: z[k] for k in z.files if k.startswith(pre)})
+        j += 1
+    return steps
+
+
+def ref_adam_tolerance(steps, name, lr_, shape, rel_err=2e-5, base=1e-5):
+    """Per-element bound on |w_got - w_ref| after the recorded Adam steps, from the reference's gradients:
+    2 lr min(1, rel_err max|g| / |g|) per step; an exactly-zero reference gradient (an input column that
+    is always 0, a hidden unit dead on every sample) is zero in any arithmetic and adds nothing."""
+    tol = np.full(shape, base, dtype=np.float64)
+    for st in steps:
+        g = np.abs(st[name].astype(np.float64))
+        err = rel_err * g.max()
+        tol += np.where(g == 0, 0.0, 2 * lr_ * np.minimum(err / np.maximum(g, 1e-30), 1.0))
+    return tol
 
 
 def assert_weights_close(got, want, tol, msg, swing):
@@ -194,15 +215,64 @@ def test_learner_matches_reference(name, E):
         np.testing.assert_allclose(np.array(res[2]), z["train/policy_loss"], rtol=0, atol=1e-5)
         np.testing.assert_allclose([float(v) for v in res[3]], z["train/value_loss"], rtol=0, atol=1e-5)
     assert rec.steps, "no optimizer step recorded"
+    nets = _nets(lr, algo)
+    # the first Adam step's gradients of the same learner on the torch agent-stacked fp32 path (a second
+    # fp32 implementation of the same losses): where the two fp32 implementations (the reference on the
+    # CPU, torch on the GPU) disagree by more than 4e-5 of max|g| -- saturated probabilities at torch's
+    # eps clamp, relu masks at 0 -- the kernels are held to 4x that disagreement instead
+    band_rec = _first_step_torch_path(z, E, algo, n_ep, teacher)
+    band_nets = _nets(band_rec.learner, algo)
+    for (msg, pre, net), (_, _, net_t) in zip(nets, band_nets):
+        tag = pre[len("final/"):]
+        steps = ref_grads(z, tag)
+        lr_ = common["value_lr"] if (tag == "critic" or tag.endswith("/value")) else common["policy_lr"]
+        assert len(steps) == len(rec.steps_of(next(net.parameters()))), (msg, len(steps))
+        for (k, v), (_, vt) in zip(net.named_parameters(), net_t.named_parameters()):
+            vd = v.detach()
+            # the first Adam step: both learners at the fixture's initial weights on the same rollout
+            g0 = rec.grad_at(vd, 0).numpy()
+            gt = band_rec.grad_at(vt.detach(), 0).numpy()
+            r0 = steps[0][k].astype(np.float64)
+            band = np.abs(gt - r0).max()
+            err = np.abs(g0 - r0).max()
+            tol = max(4e-5 * np.abs(r0).max(), 4 * band) + 1e-7
+            if err > 2e-5 * np.abs(r0).max():
+                print(f"  {msg} {k}: first-step |g - g_ref| {err:.2e}, torch path {band:.2e}, max|g_ref| "
+                      f"{np.abs(r0).max():.2e}")
+            assert err <= tol, (msg, k, float(err), float(band), float(np.abs(r0).max()))
+            assert_weights_close(vd.cpu().numpy(), z[f"{pre}/{k}"], ref_adam_tolerance(steps, k, lr_, tuple(vd.shape)),
+                                 f"{msg} {k}", rec.swing(vd))
+
+
+def _nets(lr, algo):
     nets = [(f"agent {i} policy", f"final/agent{i}/policy", ag.policy_network) for i, ag in enumerate(lr.agents)]
     if algo == "ippo":
         nets += [(f"agent {i} value", f"final/agent{i}/value", ag.value_network) for i, ag in enumerate(lr.agents)]
     else:
         nets.append(("critic", "final/critic", lr.value_network))
-    for msg, pre, net in nets:
-        for k, v in net.named_parameters():
-            assert_weights_close(v.detach().cpu().numpy(), z[f"{pre}/{k}"], rec.tolerance(v.detach()), f"{msg} {k}",
-                                 rec.swing(v.detach()))
+    return nets
+
+
+def _first_step_torch_path(z, E, algo, n_ep, teacher):
+    """The fixture's learner at its initial weights on the same teacher-forced rollout, one epoch on the
+    torch agent-stacked fp32 update (no fused kernels); returns its GradRecorder (.learner set)."""
+    env, kind, common, iPPO, D2DPPO = build(z, n_envs=E)
+    lr = iPPO(env, **common) if algo == "ippo" else D2DPPO(env, beta_entropy=0.02, **common)
+    for i, ag in enumerate(lr.agents):
+        ag.policy_network.load_state_dict(_sd(z, f"init/agent{i}/policy"))
+        if algo == "ippo":
+            ag.value_network.load_state_dict(_sd(z, f"init/agent{i}/value"))
+    if algo == "d2d":
+        lr.value_network.load_state_dict(_sd(z, "init/critic"))
+    lr._fused_upd = False
+    ro = lr._rollout(n_ep, teacher=teacher)
+    lr._rollout = lambda num_episodes, teacher=None, _ro=ro: _ro
+    lr.test = lambda num_episodes: (0.5, 1.0, 0, 0.0)
+    np.random.seed(21)
+    rec = GradRecorder(lr)
+    lr.train(1, n_epoch=1, num_episodes=n_ep, test_freq=10 ** 9)
+    rec.learner = lr
+    return rec
 
 
 def evaltest_names():
@@ -376,22 +446,34 @@ def test_rollout_graph_bound_to_its_batch():
     assert ro.E == 4
 
 
-@pytest.mark.parametrize("N", [12, 256])
-def test_d2d_central_critic_split_gemm_matches_fp32(N):
+@pytest.mark.parametrize("case", ["comb12", "chsel16", "comb8", "comb16", "comb256"])
+def test_d2d_central_critic_split_gemm_matches_fp32(case):
     """The central critic on bf16 split GEMMs (exact bf16 states x three-way split W1; dPre two-way
     split) == torch fp32 autograd of mse(Value(state), returns): values to 1e-5 relative,
-    gradients to 2e-5 of their largest entry.  N = 256: the configs[4] sweep's widest state
-    (S = 15 N + 8 = 3,848 with deadlines 7)."""
+    gradients to 2e-5 of their largest entry.  comb256: the configs[4] sweep's widest state
+    (S = 15 N + 8 = 3,848 with deadlines 7); chsel16 / comb8 / comb16: the small widths the learners
+    now also run on the split path -- configs[1] (S = 16 x 7 + 5 = 117, not a multiple of 8) and the
+    sweep's 8 / 16 agents (S = 128 / 248)."""
     from algorithms.d2d_ppo import D2DPPO
+    from envs.channel_selection_env import ChannelSelectionEnv
     from envs.combinatorial_env import CombinatorialEnv
     C = 8
-    dl = np.array([7, 14] * (N // 2)) if N == 12 else np.full(N, 7)
-    env = CombinatorialEnv(N, C, dl, np.full(N, 0.4), episode_length=20,
-                           channel_switch=np.full((N, C), 0.3), n_envs=64, device="cuda", seed=4)
-    if N == 256:
-        assert env.state_space.shape[0] == 15 * N + 8
+    comb = case.startswith("comb")
+    N = int(case[4:] if comb else case[5:])
+    if comb:
+        dl = np.array([7, 14] * (N // 2)) if N == 12 else np.full(N, 7)
+        env = CombinatorialEnv(N, C, dl, np.full(N, 0.4), episode_length=20,
+                               channel_switch=np.full((N, C), 0.3), n_envs=64, device="cuda", seed=4)
+        if N != 12:
+            assert env.state_space.shape[0] == 15 * N + 8
+    else:
+        env = ChannelSelectionEnv(n_agents=N, n_channels=4, deadlines=np.full(N, 7), lbdas=np.full(N, 1 / 3.5),
+                                  period=np.full(N, 2), arrival_probs=np.full(N, 0.5), offsets=np.zeros(N),
+                                  episode_length=20, traffic_model="aperiodic", periodic_devices=[],
+                                  channel_switch=np.full(5, 0.8), n_envs=64, device="cuda", seed=4)
+        assert env.state_space.shape[0] == 117
     torch.manual_seed(2)
-    lr = D2DPPO(env, hidden_size=64, gamma=0.5, device="cuda", combinatorial=True, early_stopping=False)
+    lr = D2DPPO(env, hidden_size=64, gamma=0.5, device="cuda", combinatorial=comb, early_stopping=False)
     lr.CRITIC_SPLIT_MIN_DIM = 0
     ro = lr._rollout(64)
     crit = lr._critic_split_forward(ro)

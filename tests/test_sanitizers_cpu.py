@@ -22,11 +22,26 @@ ENV_BASE = {"ASAN_OPTIONS": "detect_leaks=0:alloc_dealloc_mismatch=0:abort_on_er
             "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1", "PYTHONDONTWRITEBYTECODE": "1"}
 
 
+def gcc_runtimes():
+    """The gcc ASan / UBSan runtimes (the C oracle's), or None when this host has none."""
+    paths = [subprocess.run(["gcc", f"-print-file-name={n}"], capture_output=True, text=True).stdout.strip()
+             for n in ("libasan.so", "libubsan.so")]
+    return paths if all(os.path.isabs(p) and os.path.exists(p) for p in paths) else None
+
+
+def clang_runtime():
+    """The clang ASan runtime of the ROCm toolchain (the HIP library's host code), or None."""
+    rts = glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so")
+    return rts[0] if rts else None
+
+
 def _build(target_dir, lib):
-    # incremental (a no-op when the sanitizer build is current; build() tries it up front)
-    r = subprocess.run(["make", "-s", "-j", str(min(8, os.cpu_count() or 2)), "-C", target_dir, "asan"], timeout=900)
-    if r.returncode != 0 or not os.path.exists(lib):
-        pytest.skip(f"sanitizer build of {target_dir} unavailable on this host")
+    # incremental (a no-op when the sanitizer build is current; build() tries it up front).  Called only
+    # once the runtime is known to exist, so any failure here is a build error in the host code: fail.
+    r = subprocess.run(["make", "-s", "-j", str(min(8, os.cpu_count() or 2)), "-C", target_dir, "asan"],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, f"sanitizer build of {target_dir} failed:\n{r.stdout[-2000:]}{r.stderr[-3000:]}"
+    assert os.path.exists(lib), lib
 
 
 def _run(env_extra, probe, tests):
@@ -42,10 +57,12 @@ def _run(env_extra, probe, tests):
 
 
 def test_c_oracle_under_asan_ubsan():
+    rts = gcc_runtimes()
+    if rts is None:
+        pytest.skip("gcc ASan / UBSan runtimes not installed on this host")
     lib = os.path.join(ROOT, "oracle", "build", "asan", "libd2d_oracle_asan.so")
     _build(os.path.join(ROOT, "oracle"), lib)
-    rt = " ".join(subprocess.run(["gcc", f"-print-file-name={n}"], capture_output=True, text=True).stdout.strip()
-                  for n in ("libasan.so", "libubsan.so"))
+    rt = " ".join(rts)
     probe = ("import ctypes, sys; sys.path.insert(0, '.'); from oracle import c_oracle; c_oracle.lib();"
              "maps = open('/proc/self/maps').read(); assert 'libd2d_oracle_asan.so' in maps;"
              "ctypes.CDLL(None).__asan_init; print('ASAN_MAPPED')")
@@ -53,12 +70,12 @@ def test_c_oracle_under_asan_ubsan():
 
 
 def test_abi_host_code_under_asan_ubsan():
+    rt = clang_runtime()
+    if rt is None:
+        pytest.skip("clang ASan runtime not found under /opt/rocm/lib/llvm")
     lib = os.path.join(ROOT, "d2d-ppo_amd", "build", "asan", "libd2dhip_asan.so")
     _build(os.path.join(ROOT, "d2d-ppo_amd"), lib)
-    rts = glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so")
-    if not rts:
-        pytest.skip("clang ASan runtime not found under /opt/rocm/lib/llvm")
     probe = ("import ctypes, sys; sys.path[:0] = ['.', 'd2d-ppo_amd']; import d2dhip; d2dhip.load();"
              "maps = open('/proc/self/maps').read(); assert 'libd2dhip_asan.so' in maps;"
              "ctypes.CDLL(None).__asan_init; print('ASAN_MAPPED')")
-    _run({"D2D_LIB_VARIANT": "asan", "LD_PRELOAD": rts[0]}, probe, ["tests/test_abi_cpu.py"])
+    _run({"D2D_LIB_VARIANT": "asan", "LD_PRELOAD": rt}, probe, ["tests/test_abi_cpu.py"])

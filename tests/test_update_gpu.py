@@ -364,23 +364,36 @@ def test_happo_chain_kernel_matches_torch_loop():
 
 
 def test_grads_on_large_rollout_vs_float64():
-    """iPPO's fused actor and critic gradients on a real 8,192-env x 200-slot rollout of the c3 config
-    (64 agents x 8 channels, 1.6 M samples per agent: 51,200 tiles, 50 workgroups per agent, 256 tiles
-    per wave -- the longest accumulation chain update_blocks allows at any batch) against float64
-    autograd, agents 0 and 1: every tensor within max(4x torch fp32's own error, 2e-5) of max|g|.
-    (tools/gpu/ppo_grads_full_batch.py runs the same comparison at the 65,536-env headline batch.)"""
+    """iPPO's fused actor and critic gradients on a real 2,048-env x 200-slot rollout of the c3 config
+    (64 agents x 8 channels, 409,600 samples per agent) against float64 autograd, EVERY agent.
+
+    Criterion, elementwise: |g_kernel - g64| <= envelope + max(2e-5, 4 x torch fp32's own excess) x max|g64|.
+    The envelope (tools/gpu/ppo_grads_full_batch.py _flip_envelope) is the largest change relu-mask flips
+    can make: env observations are small integers repeated over many samples, so a layer-1 pre-activation
+    within fp32 rounding of 0 (|pre| <= 2 (F + 2) u sum |w x|) may take either mask in ANY fp32 evaluation
+    and flips dW1 / db1 for every sample sharing it.  The round-3 all-agent run showed such outliers of up
+    to 5e-4 of max|g| in torch fp32 autograd itself (agent 27) as well as in the kernels (agents 22, 45, 59),
+    each on w1 / b1 only (profiles/r03k/ppo_full_2048_all.json); the envelope is computed, not fitted,
+    and is zero for every tensor but w1 / b1.  Everything outside it is held to the fp32 band.
+    (The 65,536-env headline batch runs the same comparison in tools/gpu/ppo_grads_full_batch.py.)"""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "gpu"))
     from ppo_grads_full_batch import grads_vs_float64
-    out = grads_vs_float64(8192, (0, 1), emulate=False)
+    out = grads_vs_float64(2048, range(64), emulate=False, envelope=True)
     checked = 0
-    for key, err in out.items():
-        if key.count("/") != 2 or "torch32" in key:
+    worst = (0.0, None)
+    for key, exc in out.items():
+        if not key.startswith("excess/"):
             continue
-        net, k, n = key.split("/")
-        band = out[f"{net}_torch32/{k}/{n}"]
-        print(f"  {key}: kernel {err:.2e}  torch fp32 {band:.2e}")
-        assert err <= max(4 * band, 2e-5), (key, err, band)
+        _, net, k, n = key.split("/")
+        band = max(out[f"excess32/{net}/{k}/{n}"], 0.0)
+        raw = out[f"{net}/{k}/{n}"]
+        if raw > 2e-5 or exc > 1e-5:
+            print(f"  {net}/{k}/{n}: |kernel - f64| {raw:.2e}, outside the flip envelope {exc:.2e}, "
+                  f"torch fp32 outside it {band:.2e}, ambiguous pairs {out[f'ambiguous_{net}/{k}']}")
+        worst = max(worst, (exc, key))
+        assert exc <= max(4 * band, 2e-5), (key, exc, band)
         checked += 1
-    assert checked == 16
+    print(f"  worst excess over the envelope: {worst}")
+    assert checked == 64 * 8

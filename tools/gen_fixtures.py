@@ -538,6 +538,20 @@ def _learner_env(kind, episode_length=20):
     return mod.ChannelSelectionEnv(**p), p
 
 
+def _tap_grads(out, tag, opt, net):
+    """Record the .grad of every parameter of `net` each time `opt` steps (before the step runs)."""
+    step = opt.step
+    count = [0]
+
+    def rec(*a, **kw):
+        for n, prm in net.named_parameters():
+            if prm.grad is not None:
+                out[f"grads/{tag}/step{count[0]}/{n}"] = prm.grad.detach().numpy().copy()
+        count[0] += 1
+        return step(*a, **kw)
+    opt.step = rec
+
+
 def gen_learner(only=None, episodes=2, suffix="", algos=("ippo", "d2d"), variants=None):
     import torch
     ippo = ref_module("algorithms.ippo")
@@ -604,6 +618,15 @@ def gen_learner(only=None, episodes=2, suffix="", algos=("ippo", "d2d"), variant
                 ro = tuple(ro)
             lr.create_rollouts = lambda num_episodes=4, _ro=ro: _ro
             lr.test = lambda num_episodes: (0.5, 1.0, 0, 0.0)
+            # the gradient every Adam step consumes (grads/<net>/step<j>/<param>): the final-weight check
+            # of tests/test_learner_gpu.py derives its Adam-aware bound from these reference gradients
+            taps = [(f"agent{i}/policy", ag.policy_optimizer, ag.policy_network) for i, ag in enumerate(lr.agents)]
+            if algo == "ippo":
+                taps += [(f"agent{i}/value", ag.value_optimizer, ag.value_network) for i, ag in enumerate(lr.agents)]
+            else:
+                taps.append(("critic", lr.value_optimizer, lr.value_network))
+            for tag, opt, net in taps:
+                _tap_grads(out, tag, opt, net)
             np.random.seed(21)  # D2D agent permutation stream (d2d_ppo.py:421-422)
             if algo == "ippo":
                 res = lr.train(1, n_epoch=2, num_episodes=episodes, test_freq=10 ** 9)

@@ -6,7 +6,7 @@ accumulated over sample chunks.  Prints max |kernel - f64| / max |g| per tensor,
 chunks (the fp32 band the kernels are held to).
 The kernels' accumulation chains are long here: at 65,536 envs 409,600 32-sample tiles per agent, at
 most 256 per wave since round 3 (update_blocks); tests/test_update_gpu.py runs the comparison at 8,192 envs.
-usage (GPU box): python3 tools/gpu/ppo_grads_full_batch.py [E] [K]"""
+usage (GPU box): python3 tools/gpu/ppo_grads_full_batch.py [E] [K] [reversed] [envelope]"""
 import json
 import os
 import sys
@@ -23,14 +23,38 @@ def split2(v):
     return h + (v.float() - h.float()).to(torch.bfloat16).to(v.dtype)
 
 
-def grads_vs_float64(E, agents, emulate=True, seed=11, reversed_fp32=False):
+U32 = 2.0 ** -24   # fp32 unit roundoff
+
+
+def _flip_envelope(x, pre, absum, F, env):
+    """Accumulate the relu-mask flip envelope of one float64 forward chunk.  A (sample, hidden) pair is
+    ambiguous when |pre| <= 2 (F + 2) u sum_j |w_j x_j| + |b|: within twice the standard fp32 dot-product
+    error bound (Higham gamma_K, K = F + 1 products plus the bias), so any fp32 evaluation of the
+    pre-activation -- the kernels' split-bf16 MFMA sums, torch's GEMM -- may land on either side of 0
+    and take the other relu mask.  A flipped mask at (s, h) moves dW1[h, :] by dA[s, h] x_s and db1[h]
+    by dA[s, h] (dA = dL/drelu(pre)), so |g_fp32 - g64| <= band + sum over ambiguous s of |dA| |x_s|
+    elementwise.  Returns a hook that adds the chunk's part once dA is known."""
+    amb = (pre.detach().abs() <= 2 * (F + 2) * U32 * absum)
+    env["n_amb"] = env.get("n_amb", 0) + int(amb.sum())
+
+    def hook(dA):
+        a = (dA.detach().abs() * amb)                 # [B][H]
+        env["w1"] = env.get("w1", 0) + a.t() @ x.detach().abs()
+        env["b1"] = env.get("b1", 0) + a.sum(0)
+    return hook
+
+
+def grads_vs_float64(E, agents, emulate=True, seed=11, reversed_fp32=False, envelope=False):
     """Relative errors {"<net>/<agent>/<param>": max |g - g64| / max |g64|} of the kernels ("actor",
     "critic"), of torch fp32 autograd ("actor_torch32", "critic_torch32") and, with emulate, of float64
     with one kernel rounding emulated ("actor_emu_dh": dH on the two-way split of the dW1 operand;
     "actor_emu_h": relu(H) on the two-way split in the logits); with reversed_fp32, torch fp32 autograd
     with the layer-1 inputs summed in reverse column order ("actor_torch32r": another, equally valid
     fp32 rounding) and the number of (sample, hidden) relu masks each fp32 forward gets wrong against
-    float64 ("mask_flips32/<k>", "mask_flips32r/<k>")."""
+    float64 ("mask_flips32/<k>", "mask_flips32r/<k>"); with envelope, the relu-mask flip envelope of
+    _flip_envelope for both nets' layer 1 and, per tensor, "excess/<net>/<k>/<n>" = max over elements of
+    (|g - g64| - envelope) / max |g64| for the kernels ("excess32/..." for torch fp32), and
+    "ambiguous_<net>/<k>" = the number of ambiguous (sample, hidden) pairs."""
     import bench
     from algorithms.ippo import iPPO
     from d2dhip.update import actor_grads, critic_grads
@@ -70,6 +94,7 @@ def grads_vs_float64(E, agents, emulate=True, seed=11, reversed_fp32=False):
         if reversed_fp32:
             runs += [(torch.float32, q32r, None, 3)]
         flips = [0, 0]
+        envs = {"actor": {}, "critic": {}}
         if emulate:
             runs += [(torch.float64, qe1, None, 1), (torch.float64, qe2, None, 2)]
         chunk = max(1, (1 << 21) // E)
@@ -91,9 +116,16 @@ def grads_vs_float64(E, agents, emulate=True, seed=11, reversed_fp32=False):
                     with torch.no_grad():
                         ref_pre = x.double() @ pp["w1"][k].double().t() + pp["b1"][k].double()
                         flips[emu == 3] += int(((pre > 0) != (ref_pre > 0)).sum())
+                if envelope and dt == torch.float64 and emu == 0:
+                    with torch.no_grad():
+                        xa = x.abs()
+                        ab = xa @ qa["w1"].detach().abs().t() + qa["b1"].detach().abs()
+                    hk = _flip_envelope(x, pre, ab, F, envs["actor"])
                 if emu == 1:  # dH on the kernel's two-way RNE bf16 split (the dW1 / db1 operand)
                     pre.register_hook(split2)
                 h = torch.relu(pre)
+                if envelope and dt == torch.float64 and emu == 0:
+                    h.register_hook(hk)
                 if emu == 2:  # relu(H) on the two-way split in the logits (before round 3's three-way split)
                     h = h + (split2(h) - h).detach()
                 probs = torch.softmax(h @ qa["w2"].t() + qa["b2"], -1)
@@ -103,7 +135,12 @@ def grads_vs_float64(E, agents, emulate=True, seed=11, reversed_fp32=False):
                 (-(surr.sum() / B) - 0.01 * dist.entropy().mean(-1).sum() / B).backward()
                 if qc is None:
                     continue
-                hv = torch.relu(x @ qc["w1"].t() + qc["b1"])
+                prev = x @ qc["w1"].t() + qc["b1"]
+                hv = torch.relu(prev)
+                if envelope and dt == torch.float64:
+                    with torch.no_grad():
+                        abv = x.abs() @ qc["w1"].detach().abs().t() + qc["b1"].detach().abs()
+                    hv.register_hook(_flip_envelope(x, prev, abv, F, envs["critic"]))
                 v = (hv @ qc["w2"].t() + qc["b2"])[:, 0]
                 (((v - ret) ** 2).sum() / B).backward()
         tags = [("actor_torch32", q32)] + ([("actor_emu_dh", qe1), ("actor_emu_h", qe2)] if emulate else [])
@@ -119,19 +156,34 @@ def grads_vs_float64(E, agents, emulate=True, seed=11, reversed_fp32=False):
             ref = qv[n].grad
             out[f"critic/{k}/{n}"] = float((gc[n][k] - ref).abs().max() / ref.abs().max())
             out[f"critic_torch32/{k}/{n}"] = float((qv32[n].grad.double() - ref).abs().max() / ref.abs().max())
+        if envelope:
+            for net, ref_p, got, p32 in (("actor", q, ga, q32), ("critic", qv, gc, qv32)):
+                e = envs[net]
+                out[f"ambiguous_{net}/{k}"] = e.get("n_amb", 0)
+                for n in ref_p:
+                    ref = ref_p[n].grad
+                    sc = ref.abs().max()
+                    env_n = e.get(n, 0)
+                    env_n = env_n if torch.is_tensor(env_n) else torch.zeros_like(ref)
+                    env_n = env_n.reshape(ref.shape)   # dA carries the loss's 1 / B already
+                    out[f"excess/{net}/{k}/{n}"] = float(((got[n][k] - ref).abs() - env_n).max() / sc)
+                    out[f"excess32/{net}/{k}/{n}"] = float(((p32[n].grad.double() - ref).abs() - env_n).max() / sc)
     return out
 
 
 if __name__ == "__main__":
     E = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     K = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    out = grads_vs_float64(E, range(K), reversed_fp32=len(sys.argv) > 3 and sys.argv[3] == "reversed")
+    out = grads_vs_float64(E, range(K), reversed_fp32="reversed" in sys.argv[3:], envelope="envelope" in sys.argv[3:])
     print(json.dumps(out), flush=True)
     summ = {}
     for kk, vv in out.items():
         if kk.count("/") == 2:
             tag, _, n = kk.split("/")
             summ.setdefault(f"{tag}/{n}", []).append(vv)
+        elif kk.count("/") == 3:
+            tag, net, _, n = kk.split("/")
+            summ.setdefault(f"{tag}/{net}/{n}", []).append(vv)
     res = {"E": E, "T": out["T"], "agents": K, "samples_per_agent": out["samples_per_agent"]}
     res.update({kk: {"max": max(vv), "median": float(np.median(vv))} for kk, vv in sorted(summ.items())})
     print(json.dumps(res), flush=True)

@@ -1,6 +1,8 @@
 // Probe: v_dot2c_f32_bf16 as an exact residual v - bf16 half (update_kernels.hip sub_bf16_lo/hi).
 // Prints mismatches against the plain fp32 subtraction for the inline-constant form the compiler
-// picks and for the constant held in a register.
+// picks and for the constant held in a register; then the register form on special
+// inputs: a finite value whose pair partner is +-inf or NaN (h.hi * 0 = NaN spreads into the finite
+// value's residual), and fp32 denormal / bf16-denormal values (whether the dot2 flushes them).
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
@@ -53,5 +55,30 @@ int main() {
     }
   }
   printf("mismatches: inline lo %d, literal hi %d, register lo %d, register hi %d (of %d each)\n", bad[0], bad[1], bad[2], bad[3], n);
+  // special inputs, register form only: [finite, partner] pairs
+  const float inf = __builtin_inff(), qnan = __builtin_nanf("");
+  const float specials[][2] = {{1.5f, inf}, {1.5f, -inf}, {1.5f, qnan}, {inf, 1.5f}, {qnan, 1.5f},
+                               {1e-39f, 1.0f}, {1.0f, 1e-39f}, {3e-39f, -2e-40f}, {1.17549435e-38f, 1.0f},
+                               {1.2e-38f * 1.001f, 2.5f}};
+  const int ns = sizeof(specials) / sizeof(specials[0]);
+  float* hs = new float[2 * 256]();
+  for (int i = 0; i < ns; ++i) { hs[2 * i] = specials[i][0]; hs[2 * i + 1] = specials[i][1]; }
+  hipMemcpy(dv, hs, 8 * 256, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k, dim3(1), dim3(256), 0, 0, dv, dout, 0x0000BF80u, 0xBF800000u, 256);
+  hipMemcpy(ho, dout, 16 * 256, hipMemcpyDeviceToHost);
+  for (int i = 0; i < ns; ++i) {
+    for (int j = 0; j < 2; ++j) {
+      const float x = hs[2 * i + j];
+      uint32_t u;
+      memcpy(&u, &x, 4);
+      const uint32_t r = u + 0x7FFFu + ((u >> 16) & 1u);
+      uint32_t hb = (u & 0x7F800000u) == 0x7F800000u ? u : (r & 0xFFFF0000u);
+      float hf;
+      memcpy(&hf, &hb, 4);
+      const float want = x - hf, got = ho[4 * i + 2 + j];
+      printf("special pair (%a, %a) half %d: v - bf16(v) want %a got %a%s\n", hs[2 * i], hs[2 * i + 1], j, want, got,
+             memcmp(&got, &want, 4) ? "  <- differs" : "");
+    }
+  }
   return (bad[0] + bad[1] + bad[2] + bad[3]) ? 1 : 0;
 }
