@@ -279,7 +279,11 @@ class D2DPPO(BatchedLearnerBase):
 
     # ------------------------------------------------ central critic on bf16 split GEMMs
     critic_split = True
-    CRITIC_SPLIT_MIN_DIM = 256  # below this state width the fp32 GEMMs are launch-bound anyway
+    # every state width: at configs[1]'s S = 117 and configs[4]'s 8 / 16 agents (S = 128 / 248) the fp32
+    # path's dW1 (K = the whole 819 K-sample batch, one output tile row) took 12.4-13.3 ms per 5-epoch
+    # iteration against 2.3-2.6 ms for the split-K bf16 path (profiles/r04/critic_small.log)
+    CRITIC_SPLIT_MIN_DIM = 0
+    CRITIC_F32_FWD_MAX_DIM = 768  # below this state width the forward's first layer is one fp32 GEMM
 
     def _critic_split_forward(self, ro):
         """Value(state) = linear2(relu(linear1(state))) (d2d_ppo.py:95-98) for all T*E states with the
@@ -302,12 +306,14 @@ class D2DPPO(BatchedLearnerBase):
             lib = _lib.require_gpu()
             st = ro.__dict__.get("states")
             if "state_seq" not in ro.__dict__ and st is not None and st.is_contiguous() and st.dim() == 3:
-                # straight from the slot-major rollout buffer [T][E][stride] (no env-major fp32 copy)
+                # straight from the slot-major rollout buffer [T][E][stride] (no env-major fp32 copy), rows
+                # padded with zero columns to a multiple of 8 (16-byte aligned GEMM rows: configs[1]'s S = 117)
                 T_, E_ = st.shape[0], st.shape[1]
-                xb = torch.empty((E_ * T_, S), dtype=torch.bfloat16, device=st.device)
+                S8 = -(-S // 8) * 8
+                xb = torch.empty((E_ * T_, S8), dtype=torch.bfloat16, device=st.device)
                 flag = torch.empty(1, dtype=torch.int32, device=st.device)
-                _lib.check(lib.d2d_states_to_bf16_exact(T_, E_, S, st.shape[2], st.data_ptr(), xb.data_ptr(),
-                                                        flag.data_ptr(), _lib.stream_ptr()), "d2d_states_to_bf16_exact")
+                _lib.check(lib.d2d_states_to_bf16_padded(T_, E_, S, st.shape[2], st.data_ptr(), xb.data_ptr(), S8,
+                                                         flag.data_ptr(), _lib.stream_ptr()), "d2d_states_to_bf16_padded")
             else:
                 sq = ro.state_seq.contiguous()
                 xb = torch.empty(sq.shape, dtype=torch.bfloat16, device=sq.device)
@@ -320,8 +326,20 @@ class D2DPPO(BatchedLearnerBase):
             ro.state_bf16 = xb
         l1, l2 = self.value_network.linear1, self.value_network.linear2
         H = l1.weight.shape[0]
+        if S < self.CRITIC_F32_FWD_MAX_DIM:
+            # narrow states: the first layer as one fp32 GEMM on the env-major fp32 states (4 S + 4 H bytes
+            # per sample) beats the split GEMM's [3H][B] fp32 output and its sum (2 S + 28 H bytes) below
+            # S = 12 H; the backward still runs on the bf16 operand (split-K dW1).  c2 (S = 117): critic
+            # forward 4.7 -> 2.8 ms per 5-epoch iteration (profiles/r04/critic_small*.log)
+            with torch.no_grad():
+                pre = torch.addmm(l1.bias[:, None], l1.weight, ro.state_seq.t())               # [H][B]
+                hid = torch.relu(pre)
+                v = torch.addmm(l2.bias[:, None], l2.weight, hid)[0]                           # [B]
+            return v, pre, hid
         with torch.no_grad():
             w = l1.weight
+            if xb.shape[1] > S:  # the operand's zero pad columns
+                w = torch.nn.functional.pad(w, (0, xb.shape[1] - S))
             wh = w.to(torch.bfloat16)
             r = w - wh.float()
             wm = r.to(torch.bfloat16)
@@ -360,7 +378,7 @@ class D2DPPO(BatchedLearnerBase):
             _lib.check(lib.d2d_critic_dpre_split(H, B, pre_c.data_ptr(), w2v.data_ptr(), dv_c.data_ptr(), dhm.data_ptr(),
                                                  part.data_ptr(), G, _lib.stream_ptr()), "d2d_critic_dpre_split")
             sums = part.sum(0)                                                              # [2H]: db1 | dW2
-            g = self._dw1_gemm(dhm, ro.state_bf16)                                          # [2H][S]
+            g = self._dw1_gemm(dhm, ro.state_bf16)[:, :l1.weight.shape[1]]                 # [2H][S]
             grads = {l1.weight: g[:H] + g[H:], l1.bias: sums[:H], l2.weight: sums[H:], l2.bias: g_b2}
             for prm, gr in grads.items():
                 prm.grad = gr.reshape(prm.shape).contiguous()

@@ -731,16 +731,19 @@ __global__ __launch_bounds__(256) void bf16_exact_kernel(int64_t n, const float*
 // The same conversion + check straight from the rollout's slot-major state buffer x [T][E][ld] into the
 // env-major operand out [E*T][S] (out row e*T + t <- x row t*E + e, its first S floats): the central
 // critic no longer needs an fp32 env-major copy of the states first.  One workgroup per output row.
+// out rows are out_ld wide: columns [S, out_ld) are written as zeros (a GEMM-aligned operand for state
+// widths such as configs[1]'s 117)
 template <bool VEC>
 __global__ __launch_bounds__(256) void states_bf16_kernel(int T, int E, int S, int64_t ld, const float* __restrict__ x,
-                                                          uint16_t* __restrict__ out, int32_t* __restrict__ inexact) {
+                                                          uint16_t* __restrict__ out, int64_t out_ld,
+                                                          int32_t* __restrict__ inexact) {
   const int64_t rows = (int64_t)T * E;
   uint32_t low = 0;
   for (int64_t r = blockIdx.x; r < rows; r += gridDim.x) {
     const int64_t e = r / T, t = r - e * T;
     const float* xr = x + (t * E + e) * ld;
-    uint16_t* orow = out + r * S;
-    if constexpr (VEC) {  // S % 4 == 0, ld % 4 == 0, 16-byte aligned x
+    uint16_t* orow = out + r * out_ld;
+    if constexpr (VEC) {  // S % 4 == 0, ld % 4 == 0, out_ld % 4 == 0, 16-byte aligned x
       for (int q = threadIdx.x; q < (S >> 2); q += blockDim.x) {
         const uint4 v = reinterpret_cast<const uint4*>(xr)[q];
         low |= (v.x | v.y | v.z | v.w) & 0xFFFFu;
@@ -753,14 +756,15 @@ __global__ __launch_bounds__(256) void states_bf16_kernel(int T, int E, int S, i
         orow[q] = (uint16_t)(v >> 16);
       }
     }
+    for (int64_t q = S + threadIdx.x; q < out_ld; q += blockDim.x) orow[q] = 0;
   }
   if (low) inexact[0] = 1;
 }
 
-extern "C" int d2d_states_to_bf16_exact(int32_t T, int32_t E, int32_t S, int64_t ld, const float* x, uint16_t* out,
-                                        int32_t* inexact, void* stream) {
-  if (T < 0 || E < 0 || S < 1 || ld < S || !inexact || ((int64_t)T * E > 0 && (!x || !out))) {
-    d2d_set_error("d2d_states_to_bf16_exact: bad arguments");
+extern "C" int d2d_states_to_bf16_padded(int32_t T, int32_t E, int32_t S, int64_t ld, const float* x, uint16_t* out,
+                                         int64_t out_ld, int32_t* inexact, void* stream) {
+  if (T < 0 || E < 0 || S < 1 || ld < S || out_ld < S || !inexact || ((int64_t)T * E > 0 && (!x || !out))) {
+    d2d_set_error("d2d_states_to_bf16: bad arguments");
     return D2D_EINVAL;
   }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -768,12 +772,19 @@ extern "C" int d2d_states_to_bf16_exact(int32_t T, int32_t E, int32_t S, int64_t
   const int64_t rows = (int64_t)T * E;
   if (rows == 0) return D2D_OK;
   const unsigned grid = (unsigned)(rows < 16384 ? rows : 16384);
-  const bool vec = (S % 4 == 0) && (ld % 4 == 0) && !(reinterpret_cast<uintptr_t>(x) & 15) &&
+  const bool vec = (S % 4 == 0) && (ld % 4 == 0) && (out_ld % 4 == 0) && !(reinterpret_cast<uintptr_t>(x) & 15) &&
                    !(reinterpret_cast<uintptr_t>(out) & 7);
-  if (vec) hipLaunchKernelGGL(states_bf16_kernel<true>, dim3(grid), dim3(256), 0, s, T, E, S, ld, x, out, inexact);
-  else hipLaunchKernelGGL(states_bf16_kernel<false>, dim3(grid), dim3(256), 0, s, T, E, S, ld, x, out, inexact);
+  if (vec)
+    hipLaunchKernelGGL(states_bf16_kernel<true>, dim3(grid), dim3(256), 0, s, T, E, S, ld, x, out, out_ld, inexact);
+  else
+    hipLaunchKernelGGL(states_bf16_kernel<false>, dim3(grid), dim3(256), 0, s, T, E, S, ld, x, out, out_ld, inexact);
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
+}
+
+extern "C" int d2d_states_to_bf16_exact(int32_t T, int32_t E, int32_t S, int64_t ld, const float* x, uint16_t* out,
+                                        int32_t* inexact, void* stream) {
+  return d2d_states_to_bf16_padded(T, E, S, ld, x, out, S, inexact, stream);
 }
 
 extern "C" int d2d_f32_to_bf16_exact(int64_t n, const float* x, uint16_t* out, int32_t* inexact, void* stream) {

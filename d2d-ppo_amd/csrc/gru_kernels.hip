@@ -118,6 +118,7 @@ struct GruArgs {
 
 enum { kGruBernoulli = 0, kGruCategorical = 1, kGruValue = 2 };
 constexpr int kGruPadTab = 63;  // padding-table steps of the policy kernel (history_len <= 64)
+constexpr int kFlushSteps = 64;  // BPTT steps per weight-gradient MFMA accumulation chain (coop_flush)
 
 // ------------------------------------------------------------------------------ policy kernel
 // Workgroup = agent k x a strided set of tiles; 8 waves (2 per SIMD), one 16-env tile per wave at a
@@ -500,6 +501,35 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       for (int U = 0; U < IT; ++U) cwi[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
+  // COOP: add the accumulators into the wave's running sums and restart them.  After every tile, and inside
+  // a window every kFlushSteps BPTT steps: one MFMA chain over a whole L = 256 window (64 L terms) measured
+  // 100x torch fp32's error against float64 at 256 agents (tests/test_gru_gpu.py::test_gru_grads_long_window);
+  // windows of <= kFlushSteps steps (xp_load's 64) flush exactly as before
+  auto coop_flush = [&]() {
+    if constexpr (COOP) {
+      float d[NVC];
+      int v = 0;
+#pragma unroll
+      for (int g3 = 0; g3 < 3; ++g3) {
+#pragma unroll
+        for (int U = 0; U < HT; ++U)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) d[v++] = cwh[g3][U][r];
+#pragma unroll
+        for (int U = 0; U < IT; ++U)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) d[v++] = cwi[g3][U][r];
+      }
+      rmw_block(gpart, lane, 0, d);
+#pragma unroll
+      for (int g3 = 0; g3 < 3; ++g3) {
+#pragma unroll
+        for (int U = 0; U < HT; ++U) cwh[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int U = 0; U < IT; ++U) cwi[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
   __syncthreads();
 
   // The front-padding steps of a training window (x = the bias input only, h0 = 0) give the same h_j
@@ -894,6 +924,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
             for (int U = 0; U < IT; ++U) cwi[g3][U] = mfma_bf16(ai, cat2(tx[U], tx[U]), cwi[g3][U]);
           }
         }
+        if (((L - 1 - j) % kFlushSteps) == kFlushSteps - 1 && j > 0) coop_flush();  // wave-uniform
       }
 #endif
     }
@@ -901,27 +932,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       __syncthreads();  // the regions' last readers are done before the next head phase
       // flush the tile's sums into the wave's running sums (one fp32 add per tile): MFMA accumulation of
       // every tile of the kernel into the same registers measured 2x the float64 band at 64 envs
-      float d[NVC];
-      int v = 0;
-#pragma unroll
-      for (int g3 = 0; g3 < 3; ++g3) {
-#pragma unroll
-        for (int U = 0; U < HT; ++U)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) d[v++] = cwh[g3][U][r];
-#pragma unroll
-        for (int U = 0; U < IT; ++U)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) d[v++] = cwi[g3][U][r];
-      }
-      rmw_block(gpart, lane, 0, d);
-#pragma unroll
-      for (int g3 = 0; g3 < 3; ++g3) {
-#pragma unroll
-        for (int U = 0; U < HT; ++U) cwh[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int U = 0; U < IT; ++U) cwi[g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
+      coop_flush();
     }
 
     // ---- the tile's weight-gradient GEMMs over the history, K = L steps x 16 samples, TBP hidden
@@ -990,6 +1001,33 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
           for (int U = 0; U < IT; ++U) dwi[p][g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
+      // the passes' sums into the wave's global sums, accumulators restarted: at the end of the window and,
+      // for windows longer than kFlushSteps steps, every kFlushSteps steps (see coop_flush)
+      auto hist_flush = [&]() {
+#pragma unroll
+        for (int p = 0; p < TBP; ++p) {
+          if (tb0 + p >= HT) break;
+#pragma unroll
+          for (int g3 = 0; g3 < 3; ++g3) {
+            const int T = g3 * HT + tb0 + p;
+            float dh_[4 * HT], di_[4 * IT];
+#pragma unroll
+            for (int U = 0; U < HT; ++U)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) dh_[4 * U + r] = dwh[p][g3][U][r];
+#pragma unroll
+            for (int U = 0; U < IT; ++U)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) di_[4 * U + r] = dwi[p][g3][U][r];
+            rmw_block(gpart, lane, T * HT * 4, dh_);
+            rmw_block(gpart, lane, WA::WI + T * IT * 4, di_);
+#pragma unroll
+            for (int U = 0; U < HT; ++U) dwh[p][g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int U = 0; U < IT; ++U) dwi[p][g3][U] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+      };
       WFr cur, nxt;
       load_fr(nxt, 0, tb0);
 #pragma unroll 1
@@ -1021,6 +1059,37 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
           for (int q = 0; q < 4; ++q) d[q] = __builtin_amdgcn_perm(fbits(xt[U][q]), fbits(xt[U][q]), 0x03020302u);
           bx[U] = __builtin_bit_cast(bf16x8, d);
         }
+        // fp32-row inputs that are not bf16-exact (the chsel env's 1/n ACK fractions): x is the exact sum of
+        // three truncation parts x_h + x_m + x_l; [x_h x_h] above leaves a_h x_m + a_m x_m ([x_m x_m]) and
+        // a_h x_l ([x_l 0]) to two more MFMAs (wave-uniform: the record's integers never take this branch).
+        // Without them dW_ih carried x's 2^-8 truncation coherently over every sample of a fractional
+        // ACK value: 1.5e-4 - 5.6e-4 of max|g| on the categorical GRU learner traces (tools/gpu/gru_learner_diag.py)
+        bool xfrac = false;
+        bf16x8 bxm[IT], bxl[IT];
+        if (!a.ov.u8) {
+          uint32_t low = 0;
+#pragma unroll
+          for (int U = 0; U < IT; ++U)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) low |= fbits(xt[U][q]) & 0xFFFFu;
+          xfrac = __builtin_amdgcn_ballot_w64(low != 0) != 0;
+          if (xfrac) {
+#pragma unroll
+            for (int U = 0; U < IT; ++U) {
+              u32x4v dm, dl;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const float rm = xt[U][q] - ffrom(fbits(xt[U][q]) & 0xFFFF0000u);  // x - x_h, exact
+                const uint32_t rb = fbits(rm) & 0xFFFF0000u;                       // x_m
+                const float rl = rm - ffrom(rb);                                  // x_l, exact in bf16
+                dm[q] = __builtin_amdgcn_perm(rb, rb, 0x03020302u);
+                dl[q] = fbits(rl) >> 16;
+              }
+              bxm[U] = __builtin_bit_cast(bf16x8, dm);
+              bxl[U] = __builtin_bit_cast(bf16x8, dl);
+            }
+          }
+        }
 #pragma unroll
         for (int p = 0; p < TBP; ++p) {
           if (tb0 + p >= HT) break;
@@ -1040,6 +1109,15 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
           for (int g3 = 0; g3 < 3; ++g3)
 #pragma unroll
             for (int U = 0; U < IT; ++U) dwi[p][g3][U] = mfma_bf16(ag[g3], bx[U], dwi[p][g3][U]);
+          if (xfrac) {
+#pragma unroll
+            for (int g3 = 0; g3 < 3; ++g3)
+#pragma unroll
+              for (int U = 0; U < IT; ++U) {
+                dwi[p][g3][U] = mfma_bf16(ag[g3], bxl[U], dwi[p][g3][U]);
+                dwi[p][g3][U] = mfma_bf16(ag[g3], bxm[U], dwi[p][g3][U]);
+              }
+          }
         }
 #else
 #pragma unroll
@@ -1061,26 +1139,9 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
               for (int s4 = 0; s4 < 4; ++s4) dwi[p][g3][U] = mfma4(cur.ai[p][g3][s4], xt[U][s4], dwi[p][g3][U]);
         }
 #endif
+        if ((j % kFlushSteps) == kFlushSteps - 1 && j + 1 < L) hist_flush();  // wave-uniform
       }
-#pragma unroll
-      for (int p = 0; p < TBP; ++p) {
-        if (tb0 + p >= HT) break;
-#pragma unroll
-        for (int g3 = 0; g3 < 3; ++g3) {
-          const int T = g3 * HT + tb0 + p;
-          float dh_[4 * HT], di_[4 * IT];
-#pragma unroll
-          for (int U = 0; U < HT; ++U)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dh_[4 * U + r] = dwh[p][g3][U][r];
-#pragma unroll
-          for (int U = 0; U < IT; ++U)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) di_[4 * U + r] = dwi[p][g3][U][r];
-          rmw_block(gpart, lane, T * HT * 4, dh_);
-          rmw_block(gpart, lane, WA::WI + T * IT * 4, di_);
-        }
-      }
+      hist_flush();
     }
   }
 

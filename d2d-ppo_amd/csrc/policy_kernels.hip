@@ -178,6 +178,12 @@ __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* 
   }
 }
 
+#ifndef D2D_POLICY_L2_F32
+// 1 (A/B): actor layer 2 on v_mfma_f32_16x16x4_f32 straight from relu(H^T) (an exact fmaf chain, 16 MFMAs
+// of 32 cycles per tile) instead of the three-way split of relu(H^T) (88 VALU per tile) and 6 bf16 MFMAs
+#define D2D_POLICY_L2_F32 0
+#endif
+
 // KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even);
 // U8: the inputs are the env kernel's compact obs record (D2D_OBS_U8)
 template <int KC, int HT, int KIND, bool CRITIC, int MODE, bool U8>
@@ -213,7 +219,12 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
   }
 
   // ---- weight fragments of agent k, split once per workgroup
-  Parts w1p[HT][KC], v1p[CRITIC ? HT : 1][KC], w2p[HT / 2];
+  Parts w1p[HT][KC], v1p[CRITIC ? HT : 1][KC];
+#if D2D_POLICY_L2_F32
+  float w2f[HT][4];  // A operand of step (t, r): row = action i, k-slot g <-> hidden 16t + 4g + r
+#else
+  Parts w2p[HT / 2];
+#endif
   float v2f[HT][4];
   f32x4 b2i;
   {
@@ -242,6 +253,15 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
         v2f[t][r] = (CRITIC && hid < H) ? a.v2[(size_t)k * H + hid] : 0.f;
       }
     }
+#if D2D_POLICY_L2_F32
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int hid = 16 * t + 4 * g + r;
+        w2f[t][r] = (i < A && hid < H) ? a.w2[((size_t)k * A + i) * H + hid] * kLog2e : 0.f;
+      }
+#else
 #pragma unroll
     for (int c2 = 0; c2 < HT / 2; ++c2) {
       // element j of lane group g <-> hidden 16 * (2 c2 + (j >> 2)) + 4 g + (j & 3): the
@@ -254,6 +274,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
       }
       w2p[c2] = split3(wv);
     }
+#endif
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int act = 4 * g + r;
@@ -365,6 +386,24 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
 
       // ---- actor layer 2 on the accumulators of tile pairs (split, full six terms)
       lg = b2i;
+#if D2D_POLICY_L2_F32 == 1
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lg = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[t][r], relu(ha[t][r]), lg, 0, 0, 0);
+#elif D2D_POLICY_L2_F32 == 2
+      {  // two independent accumulation chains (hidden tiles [0, HT/2) and [HT/2, HT)), summed once
+        f32x4 lh = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < HT / 2; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            lg = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[t][r], relu(ha[t][r]), lg, 0, 0, 0);
+            lh = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[HT / 2 + t][r], relu(ha[HT / 2 + t][r]), lh, 0, 0, 0);
+          }
+        lg += lh;
+      }
+#else
 #pragma unroll
       for (int c2 = 0; c2 < HT / 2; ++c2) {
         float hvals[8];
@@ -375,6 +414,7 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
         }
         lg = mfma_split(w2p[c2], split3(hvals), false, lg);
       }
+#endif
       // ---- critic layer 2 (64 -> 1) on VALU
       value = 0.f;
       if constexpr (CRITIC) {

@@ -61,7 +61,12 @@
 #define D2D_LOGITS_SPLIT3 1  // 0 (timing A/B only): relu(HT) on the two-way split in the logits
 #endif
 #ifndef D2D_SPLIT_DOT2
-#define D2D_SPLIT_DOT2 1  // 0 (timing A/B only): split residuals on v_perm + v_and + v_pk_add_f32
+// split residuals v - (bf16 half): 2 (default since round 4) a v_perm / v_and plus one scalar v_sub_f32;
+// 1: one v_dot2c_f32_bf16 (round 3; fewer VALU but each one issues at a higher price beside the MFMAs:
+// actor 1.85 -> 1.83 ms, critic 0.776 -> 0.747 ms per 26 M agent-samples with 2, profiles/r04/upd_ab_sub2.json);
+// 0 (A/B only): the subtraction left to the compiler, which pairs it into v_pk_add_f32.  All three are exact
+// (v - h is representable), so the gradients are bitwise the same
+#define D2D_SPLIT_DOT2 2
 #endif
 #ifndef D2D_DW2_PAIRED
 // 1 (A/B only): record-path actor dW2^T = relu(H)^T . dZ over both 16-sample halves at once, k-slots =
@@ -158,14 +163,25 @@ __device__ __forceinline__ uint32_t bf16_pair_neg1_hi() {
   asm("s_mov_b32 %0, 0xbf800000" : "=s"(c));
   return c;
 }
+// D2D_SPLIT_DOT2 == 2 (A/B): the residual as one v_perm / v_and plus one scalar v_sub_f32 (asm, so the
+// compiler cannot pair the subtractions into v_pk_add_f32)
+__device__ __forceinline__ float sub_f32_asm(float a, float b) {
+  float r;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ float sub_bf16_lo(float v, uint32_t h) {
-#if !D2D_SPLIT_DOT2
+#if D2D_SPLIT_DOT2 == 2
+  return sub_f32_asm(v, ffrom(bf16_lo_as_f32bits(h)));
+#elif !D2D_SPLIT_DOT2
   return v - ffrom(bf16_lo_as_f32bits(h));
 #endif
   return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, h), __builtin_bit_cast(bf16x2_t, bf16_pair_neg1_lo()), v, false);
 }
 __device__ __forceinline__ float sub_bf16_hi(float v, uint32_t h) {
-#if !D2D_SPLIT_DOT2
+#if D2D_SPLIT_DOT2 == 2
+  return sub_f32_asm(v, ffrom(h & 0xFFFF0000u));
+#elif !D2D_SPLIT_DOT2
   return v - ffrom(h & 0xFFFF0000u);
 #endif
   return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, h), __builtin_bit_cast(bf16x2_t, bf16_pair_neg1_hi()), v, false);

@@ -37,7 +37,7 @@ def refuse_ablation(what):
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 9
+ABI_VERSION = 10
 D2D_OBS_F32, D2D_OBS_U8 = 0, 1
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
@@ -125,6 +125,8 @@ _SIGS = {
     "d2d_f32_to_bf16_exact": (ctypes.c_int, [ctypes.c_int64, _p, _p, _p, _p]),
     "d2d_states_to_bf16_exact": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, _p, _p,
                                                 _p, _p]),
+    "d2d_states_to_bf16_padded": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, _p, _p,
+                                                  ctypes.c_int64, _p, _p]),
     "d2d_critic_dpre_blocks": (ctypes.c_int32, [ctypes.c_int64]),
     "d2d_critic_dpre_split": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, _p, _p, _p, _p, _p, ctypes.c_int32, _p]),
     "d2d_policy_mlp_step": (ctypes.c_int, [ctypes.POINTER(MlpDesc), _p, _p, ctypes.c_uint32, ctypes.c_int32, _p, _p,

@@ -43,10 +43,11 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 9  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
+#define D2D_ABI_VERSION 10  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
                               6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_states_to_bf16_exact,
                               d2d_critic_dpre_split; 8: d2d_gae_scan_moments, d2d_normalize_pair;
-                              9: d2d_gae_scan_moments without outputs, d2d_gae_scan_normalized */
+                              9: d2d_gae_scan_moments without outputs, d2d_gae_scan_normalized;
+                              10: d2d_states_to_bf16_padded */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -255,6 +256,10 @@ int d2d_f32_to_bf16_exact(int64_t n, const float* x, uint16_t* out, int32_t* ine
  * the env-major bf16 operand out [E*T][S] (row e*T + t), no fp32 env-major copy first (ABI v7). */
 int d2d_states_to_bf16_exact(int32_t T, int32_t E, int32_t S, int64_t ld, const float* x, uint16_t* out,
                              int32_t* inexact, void* stream);
+/* The same into rows of out_ld >= S bf16 (columns [S, out_ld) written as zeros): the GEMM-aligned operand
+ * [E*T][out_ld] of a state width that is not a multiple of 8 (configs[1]'s S = 117).  ABI v10. */
+int d2d_states_to_bf16_padded(int32_t T, int32_t E, int32_t S, int64_t ld, const float* x, uint16_t* out,
+                              int64_t out_ld, int32_t* inexact, void* stream);
 
 /* D2D central critic backward glue (algorithms/d2d_ppo.py:208-216 value_loss.backward() through
  * Value = linear2(relu(linear1(state)))), pre [H][B] (the first layer's pre-activations), w2 [H]

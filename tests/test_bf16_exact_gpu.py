@@ -77,3 +77,23 @@ def test_states_from_the_slot_major_buffer(T, E, S, ld):
                                             _lib.stream_ptr()), "d2d_states_to_bf16_exact")
     torch.cuda.synchronize()
     assert int(flag.item()) == 1
+
+
+@pytest.mark.parametrize("T,E,S,ld,out_ld", [(200, 64, 117, 117, 120), (7, 5, 23, 24, 24), (3, 2, 128, 132, 136),
+                                             (20, 33, 248, 248, 248)])
+def test_states_padded_rows(T, E, S, ld, out_ld):
+    """d2d_states_to_bf16_padded (ABI v10): rows of out_ld bf16, the states in [0, S) and zeros in [S, out_ld)
+    (the pad columns are overwritten whatever the buffer held)."""
+    g = torch.Generator(device="cuda").manual_seed(T + E + S)
+    x = torch.randint(-1, 20, (T, E, ld), device="cuda", generator=g).float()
+    ref = torch.zeros((E * T, out_ld), device="cuda")
+    ref[:, :S] = x[:, :, :S].transpose(0, 1).reshape(E * T, S)
+    out = torch.full((E * T, out_ld), 5.0, dtype=torch.bfloat16, device="cuda")
+    flag = torch.full((1,), 7, dtype=torch.int32, device="cuda")
+    lib = _lib.require_gpu()
+    _lib.check(lib.d2d_states_to_bf16_padded(T, E, S, ld, x.data_ptr(), out.data_ptr(), out_ld, flag.data_ptr(),
+                                             _lib.stream_ptr()), "d2d_states_to_bf16_padded")
+    torch.cuda.synchronize()
+    assert int(flag.item()) == 0 and torch.equal(out, ref.to(torch.bfloat16))
+    assert lib.d2d_states_to_bf16_padded(T, E, S, ld, x.data_ptr(), out.data_ptr(), S - 1, flag.data_ptr(),
+                                         _lib.stream_ptr()) == -1  # D2D_EINVAL

@@ -466,6 +466,9 @@ def test_gru_grads_long_window(kind, c, grad_input):
     xp_grads_check(kind, grad_input, c["E"], cfg=c)
 
 
+LAST = []  # the last xp_grads_check's (kernel, float64, fp32) gradients
+
+
 def xp_grads_check(kind, grad_input, E, check=True, cfg=None):
     """The body of test_gru_grads_at_xp_load_window at E envs; returns {tensor: (err64, band, max|g|)}
     (check=False: no assertions; tools/gpu/gru_coop_vs_history.py runs it at the bench's 256 envs)."""
@@ -530,6 +533,7 @@ def xp_grads_check(kind, grad_input, E, check=True, cfg=None):
     torch.cuda.synchronize()
     well = True
     errs = {}
+    LAST[:] = [got, r64, r32]  # for tools/gpu/gru_long_diag.py
     for name in r64:
         gk = got[name].double()
         scale = r64[name].abs().max().item()
@@ -547,7 +551,10 @@ def xp_grads_check(kind, grad_input, E, check=True, cfg=None):
             assert err64 <= 4 * band, (name, err64, band)
     if not check:
         return errs
-    s_ref = s64 if well else s32
-    torch.testing.assert_close(st.double()[:, 0], s_ref[:, 0], rtol=1e-5, atol=1e-4)
-    if kind is not None:
-        torch.testing.assert_close(st.double()[:, 1], s_ref[:, 1], rtol=1e-5, atol=1e-4)
+    # loss sums vs float64: 1e-5 relative, or within 4x torch fp32's own distance where a long window's
+    # fp32 rounding is larger (the sums over L = 256-step windows at 256 agents)
+    for col in ((0,) if kind is None else (0, 1)):
+        got_s, s64c, s32c = st.double()[:, col], s64[:, col], s32[:, col].double()
+        tol = torch.maximum(1e-5 * s64c.abs() + 1e-4, 4 * (s32c - s64c).abs())
+        assert bool(((got_s - s64c).abs() <= tol).all()), (col, ((got_s - s64c).abs() / tol).max().item())
+    del well

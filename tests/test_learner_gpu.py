@@ -446,20 +446,22 @@ def test_rollout_graph_bound_to_its_batch():
     assert ro.E == 4
 
 
-@pytest.mark.parametrize("case", ["comb12", "chsel16", "comb8", "comb16", "comb256"])
+@pytest.mark.parametrize("case", ["comb12", "chsel16", "comb8", "comb16", "comb256", "chsel16-splitfwd"])
 def test_d2d_central_critic_split_gemm_matches_fp32(case):
     """The central critic on bf16 split GEMMs (exact bf16 states x three-way split W1; dPre two-way
     split) == torch fp32 autograd of mse(Value(state), returns): values to 1e-5 relative,
     gradients to 2e-5 of their largest entry.  comb256: the configs[4] sweep's widest state
     (S = 15 N + 8 = 3,848 with deadlines 7); chsel16 / comb8 / comb16: the small widths the learners
     now also run on the split path -- configs[1] (S = 16 x 7 + 5 = 117, not a multiple of 8) and the
-    sweep's 8 / 16 agents (S = 128 / 248)."""
+    sweep's 8 / 16 agents (S = 128 / 248), whose forward runs as one fp32 GEMM below
+    CRITIC_F32_FWD_MAX_DIM (the "-splitfwd" case forces the split forward at S = 117)."""
     from algorithms.d2d_ppo import D2DPPO
     from envs.channel_selection_env import ChannelSelectionEnv
     from envs.combinatorial_env import CombinatorialEnv
     C = 8
     comb = case.startswith("comb")
-    N = int(case[4:] if comb else case[5:])
+    split_fwd = case.endswith("-splitfwd")
+    N = int((case[4:] if comb else case[5:]).split("-")[0])
     if comb:
         dl = np.array([7, 14] * (N // 2)) if N == 12 else np.full(N, 7)
         env = CombinatorialEnv(N, C, dl, np.full(N, 0.4), episode_length=20,
@@ -475,6 +477,8 @@ def test_d2d_central_critic_split_gemm_matches_fp32(case):
     torch.manual_seed(2)
     lr = D2DPPO(env, hidden_size=64, gamma=0.5, device="cuda", combinatorial=comb, early_stopping=False)
     lr.CRITIC_SPLIT_MIN_DIM = 0
+    if split_fwd:
+        lr.CRITIC_F32_FWD_MAX_DIM = 0
     ro = lr._rollout(64)
     crit = lr._critic_split_forward(ro)
     assert crit is not None

@@ -1,6 +1,6 @@
 """Multi-rank rehearsal of the data-parallel PRODUCT path on one GPU.
 
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+    [D2D_REHEARSE_N=64] python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29541 tools/gpu/rehearse_dp.py
 
 Both ranks share cuda:0 over gloo (a 1-GPU box cannot run RCCL between two ranks).  Each rank
@@ -26,9 +26,11 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-E, N, C, L = 96, 8, 8, 20
+# batch shape: 8 agents by default; D2D_REHEARSE_N=64 rehearses the benched 64 x 8 agent count
+E, N, C, L = (int(os.environ.get(f"D2D_REHEARSE_{k}", v)) for k, v in (("E", 96), ("N", 8), ("C", 8), ("L", 20)))
 ALGOS = ("ippo", "d2d", "ippo_gru", "d2d_gru")
-OUT = os.path.join(ROOT, "gpurun_out", "dp")
+# the ranks' tensors (hundreds of MB at 64 agents) go to a scratch directory outside gpurun_out/
+OUT = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"d2d_rehearse_dp_{os.environ.get('MASTER_PORT', '0')}")
 
 
 def make_env(n_envs):
@@ -84,6 +86,8 @@ def main():
     for algo in ALGOS:
         full = run(algo, E * ws)
         shards = [torch.load(os.path.join(OUT, f"{algo}_rank{r}.pt")) for r in range(ws)]
+        for r in range(ws):
+            os.remove(os.path.join(OUT, f"{algo}_rank{r}.pt"))
         d = {}
         for k in ("obs", "actions"):          # [T][E]...: env axis 1
             ok = torch.equal(torch.cat([s[k] for s in shards], 1), full[k])
@@ -114,7 +118,8 @@ def main():
                 d[k + "_over_lr"] = err / 3e-3
                 bad += [] if err <= 0.02 * 3e-3 else [f"{algo} {k} {err / 3e-3:.2e} lr"]
         rep[algo] = d
-    print(json.dumps({"rehearse_dp": rep, "world_size": ws, "envs_per_rank": E, "violations": bad}))
+    print(json.dumps({"rehearse_dp": rep, "world_size": ws, "envs_per_rank": E, "agents": N, "channels": C,
+                      "violations": bad}))
     return 1 if bad else 0
 
 
