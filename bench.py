@@ -487,6 +487,47 @@ def _env_rate(env, steps=40, bytes_per_agent_step=None):
     return rate, roof
 
 
+def _env_rate_graph(env, reps=5):
+    """The same env steps replayed as one captured HIP graph per episode (reset + episode_length x
+    (synthetic-action sampling + env kernel)), as the learners' training rollouts run: the device-side rate
+    of the small configurations, whose eager step loop is bound by Python and launch overhead.  The replays
+    advance the env kernel's Philox counters through the rng_offset word (fresh channel flips and arrivals
+    every replay); the synthetic actions repeat per replay."""
+    b = env.batch()
+    act = b.action_buffer()
+    L = env.episode_length
+
+    def episode():
+        b.reset(want_obs=True)
+        for _ in range(L):
+            b.sample_actions(0.1, out=act)
+            b.step(act, want_obs=True)
+
+    side = torch.cuda.Stream(device=b.device)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        episode()  # warm-up (allocations, kernel attributes)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    base = b.rng_step
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        episode()
+    delta = b.rng_step - base
+    b.rng_step = base
+    g.replay()  # first replay (graph upload) untimed
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for r in range(reps):
+        b.rng_off.fill_(delta * (r + 1))
+        g.replay()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    b.rng_off.zero_()
+    b.rng_step = base + delta * (reps + 1)
+    return b.E * L * reps / el
+
+
 def _d2d_iteration(env, n_epoch, combinatorial):
     """One D2D-PPO training iteration (d2d_ppo.py:405-448 loop body without test()): rollout of
     every env, returns, n_epoch epochs (critic values, GAE, chain over a random agent cycle,
@@ -536,8 +577,10 @@ def configs_leg(args, rank, world, local):
     env.shard(rank, world)
     # chsel B_as = 1 + 2D + 4(D + C + 1) + 2(C + 1)/N = 63.6 B at D = 7, C = 4, N = 16
     rate, roof = _env_rate(env, bytes_per_agent_step=1 + 2 * 7 + 4 * (7 + 4 + 1) + 2 * 5 / N)
+    rate_g = _env_rate_graph(env)
     it_s, fused, phases = _d2d_iteration(env, 5, combinatorial=False)
     out["c2"] = {"envs_per_gpu": 4096, "agents": N, "channels": 4, "env_steps_per_s": rate * world,
+                 "env_steps_per_s_graph": rate_g * world,
                  "env_kernel": roof, "d2d_iteration_s": it_s, "fused_update": fused, "phase_ms": phases,
                  "d2d_env_steps_per_s_end_to_end": 4096 * world * args.episode_length / it_s}
     del env
@@ -550,8 +593,10 @@ def configs_leg(args, rank, world, local):
         env.shard(rank, world)
         # comb B_as = 6D + 11C = 130 B at D = 7, C = 8 (fp32 obs rows)
         rate, roof = _env_rate(env, bytes_per_agent_step=6 * 7 + 11 * 8)
+        rate_g = _env_rate_graph(env)
         it_s, fused, phases = _d2d_iteration(env, 5, combinatorial=True)
         sweep.append({"agents": N, "env_steps_per_s": rate * world, "agent_steps_per_s": rate * world * N,
+                      "env_steps_per_s_graph": rate_g * world,
                       "env_kernel": roof, "d2d_iteration_s": it_s, "fused_update": fused, "phase_ms": phases})
         del env
         torch.cuda.empty_cache()

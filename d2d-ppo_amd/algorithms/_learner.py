@@ -127,10 +127,12 @@ class BatchedLearnerBase(DataParallelMixin):
 
     # ------------------------------------------------ behaviour policy slot
     def _fused_ok(self):
-        """The fused HIP policy kernel covers the MLP policies (H <= 64, A <= 16, F <= 64)."""
+        """The fused HIP policy kernel covers the MLP policies (A <= 16, F <= 64; H <= 128 with F + 1 <= 32 --
+        the learners' default hidden_size 128 on the reference envs -- else H <= 64)."""
         if getattr(self, "_fused", None) is None:
             p = self.policy
-            self._fused = (not self.useRNN and p.kind == "mlp" and p.H <= 64 and p.A <= 16 and p.F <= 64
+            hmax = 128 if p.F + 1 <= 32 else 64
+            self._fused = (not self.useRNN and p.kind == "mlp" and p.H <= hmax and p.A <= 16 and p.F <= 64
                            and os.environ.get("D2D_FUSED_POLICY", "1") != "0")
         return self._fused
 

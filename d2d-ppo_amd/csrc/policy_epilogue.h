@@ -77,6 +77,14 @@ __device__ __forceinline__ void load_obs_tile(float (&xf)[KS], const float* __re
 }
 
 
+// The Philox block policy_epilogue draws in sample mode for (env, agent k, action group ga) -- KIND 1 draws
+// group 0's block in every lane
+template <int KIND>
+__device__ __forceinline__ u32x4 policy_rng_block(const MlpArgs& a, int env, bool env_ok, int k, int ga, uint32_t rng) {
+  const uint32_t genv = (uint32_t)(a.env_base + (uint64_t)(env_ok ? env : 0));
+  return philox(genv, (uint32_t)k, rng, (kStreamPolicy << 24) | (KIND == 0 ? (uint32_t)ga : 0u), a.seed);
+}
+
 // Softmax over the A action logits of env i (action group ga holds actions 4ga..4ga+3 in lg),
 // sampling / forced / deterministic actions, log-prob and the stores (ippo.py:154-176).
 // HALF (A <= 8): each 32-lane half is its own env tile -- lanes 0-31 one tile, lanes 32-63 the
@@ -87,9 +95,13 @@ __device__ __forceinline__ void load_obs_tile(float (&xf)[KS], const float* __re
 // prefetch), or kModeRuntime (tested per launch from a.forced / a.deterministic).
 // PRE (forced mode): the forced mask / id was loaded ahead by the caller and arrives in `fpre`
 // (the split kernel's paired epilogue); otherwise the epilogue loads it itself.
-template <int KIND, bool CRITIC, bool HALF = false, int MODE = kModeRuntime, bool PRE = false, bool SIGMOID = false>
+// RNG (sample mode): the lane's Philox block drawn ahead by the caller and passed in `rpre` -- the split
+// kernel draws it before its tile MFMAs so that the ten dependent rounds (20 v_mad_u64_u32) fill the MFMA issue
+// gaps instead of running as a serial chain after them; the same counter and key, so the same words.
+template <int KIND, bool CRITIC, bool HALF = false, int MODE = kModeRuntime, bool PRE = false, bool SIGMOID = false,
+          bool RNG = false>
 __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, float value, int env, bool env_ok,
-                                                int k, int g, uint32_t rng, uint32_t fpre = 0) {
+                                                int k, int g, uint32_t rng, uint32_t fpre = 0, u32x4 rpre = {}) {
   const int N = a.N, A = a.A;
   constexpr bool critic = CRITIC;
   const int ga = HALF ? (g & 1) : g;
@@ -138,7 +150,7 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
 #pragma unroll
       for (int r = 0; r < 4; ++r) taken |= (uint32_t)(p[r] > 0.5f) << r;  // dist.probs > 0.5 (ippo.py:166)
     } else {
-      const u32x4 rr = philox(genv, (uint32_t)k, rng, (kStreamPolicy << 24) | (uint32_t)ga, a.seed);
+      const u32x4 rr = RNG ? rpre : philox(genv, (uint32_t)k, rng, (kStreamPolicy << 24) | (uint32_t)ga, a.seed);
 #pragma unroll
       for (int r = 0; r < 4; ++r) taken |= (uint32_t)((float)(pick(rr, r) >> 8) * (1.f / 16777216.f) < p[r]) << r;
     }
@@ -180,7 +192,7 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
       chosen = bi;
     } else {
       // prefix over lane groups: exclusive sum of psum for groups < g
-      const u32x4 rr = philox(genv, (uint32_t)k, rng, (kStreamPolicy << 24), a.seed);
+      const u32x4 rr = RNG ? rpre : philox(genv, (uint32_t)k, rng, (kStreamPolicy << 24), a.seed);
       const float u = (float)(rr.x >> 8) * (1.f / 16777216.f) * tot;
       const float s16 = uf(partner16(fu(psum), g));  // partner in pair (g ^ 1)
       const float pair = psum + s16;

@@ -178,6 +178,12 @@ __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* 
   }
 }
 
+#ifndef D2D_POLICY_RNG_EARLY
+#define D2D_POLICY_RNG_EARLY 1  // draw the paired epilogue's Philox block before the tile MFMAs (A/B: 0)
+#endif
+#ifndef D2D_POLICY_SGB
+#define D2D_POLICY_SGB 0  // A/B: scheduling-group hints interleaving the tile MFMAs with the VALU (incl. Philox)
+#endif
 #ifndef D2D_POLICY_L2_F32
 // 1 (A/B): actor layer 2 on v_mfma_f32_16x16x4_f32 straight from relu(H^T) (an exact fmaf chain, 16 MFMAs
 // of 32 cycles per tile) instead of the three-way split of relu(H^T) (88 VALU per tile) and 6 bf16 MFMAs
@@ -187,7 +193,9 @@ __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* 
 // KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even);
 // U8: the inputs are the env kernel's compact obs record (D2D_OBS_U8)
 template <int KC, int HT, int KIND, bool CRITIC, int MODE, bool U8>
-__global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpArgs a) {  // waves / SIMD
+// (H <= 64, F + 1 <= 32: 2 waves / SIMD; H in (64, 128] -- the learners' default hidden_size 128 -- or
+// F + 1 > 32: one wave / SIMD with the doubled weight fragments in registers)
+__global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_split_kernel(MlpArgs a) {
   static_assert(HT % 2 == 0, "layer 2 consumes hidden tiles in pairs");
   // Philox step of the launch, read once before the obs pipeline starts (the optional device
   // offset of graph replays; a load inside the epilogue would add a wait to every tile pair)
@@ -437,12 +445,28 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
     issue(tt + RING - 1);
     wait_vmem<(RING - 2) * KC * DPC>();  // tiles tt, tt + 1 have landed
     __builtin_amdgcn_sched_barrier(0);        // no LDS read of the slots moves above the wait
+    const int env0 = wave_env0 + tt * 16 + i, env1 = env0 + 16;
+    // the paired epilogue's Philox block, drawn here: inside the scheduling region of the tiles' MFMAs (the
+    // barrier below would otherwise keep it behind them as a serial chain of ten dependent rounds)
+    u32x4 rpre = {};
+    if constexpr (MODE == kModeSample && D2D_POLICY_RNG_EARLY) {
+      if (A <= 8) {
+        const int envc = g < 2 ? env0 : env1;
+        rpre = policy_rng_block<KIND>(a, envc, envc < a.E, k, g & 1, rng);
+      }
+    }
     f32x4 lg0, lg1;
     float v0, v1;
     tile(tt, lg0, v0);
     tile(tt + 1, lg1, v1);
+#if D2D_POLICY_SGB
+#pragma unroll
+    for (int q = 0; q < 36; ++q) {  // 2 MFMAs, then 8 VALU (72 MFMAs, ~300 VALU in the region)
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
+    }
+#endif
     __builtin_amdgcn_sched_barrier(0);        // the slots are read before the next DMA reuses them
-    const int env0 = wave_env0 + tt * 16 + i, env1 = env0 + 16;
     if (A <= 8) {
       // one epilogue for both tiles: lanes 0-31 keep tile tt (action groups 0, 1), lanes 32-63
       // take tile tt + 1's lanes 0-31 (permlane32_swap: vdst upper half <- src lower half)
@@ -452,8 +476,8 @@ __global__ __launch_bounds__(256, KC == 1 ? 2 : 1) void policy_split_kernel(MlpA
       const int envc = g < 2 ? env0 : env1;
       const int pair = tt >> 1;  // wave-uniform
       const uint32_t fpre = ((pair < 4 ? fpk[0] : fpk[1]) >> (8 * (pair & 3))) & 0xFFu;
-      policy_epilogue<KIND, CRITIC, true, MODE, MODE == kModeForced>(a, lgc, g < 2 ? v0 : v1, envc, envc < a.E, k,
-                                                                      g, rng, fpre);
+      policy_epilogue<KIND, CRITIC, true, MODE, MODE == kModeForced, false, MODE == kModeSample && D2D_POLICY_RNG_EARLY>(
+          a, lgc, g < 2 ? v0 : v1, envc, envc < a.E, k, g, rng, fpre, rpre);
     } else {
       policy_epilogue<KIND, CRITIC, false, MODE>(a, lg0, v0, env0, env0 < a.E, k, g, rng);
       policy_epilogue<KIND, CRITIC, false, MODE>(a, lg1, v1, env1, env1 < a.E, k, g, rng);
@@ -517,8 +541,13 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const void* obs, const
   }
   if (d->kind != 0 && d->kind != 1) { d2d_set_error("kind must be 0 (Bernoulli) or 1 (Categorical)"); return D2D_EINVAL; }
   if (d->n_out < 1 || d->n_out > 16) { d2d_set_error("n_out=%d outside [1,16]", d->n_out); return D2D_EUNSUPPORTED; }
-  if (d->hidden < 1 || d->hidden > 64) { d2d_set_error("hidden=%d outside [1,64]", d->hidden); return D2D_EUNSUPPORTED; }
   if (d->obs_dim < 1 || d->obs_dim > 64) { d2d_set_error("obs_dim=%d outside [1,64]", d->obs_dim); return D2D_EUNSUPPORTED; }
+  // hidden <= 128 with one input chunk (F + 1 <= 32), else <= 64
+  const int hmax = d->obs_dim + 1 <= 32 ? 128 : 64;
+  if (d->hidden < 1 || d->hidden > hmax) {
+    d2d_set_error("hidden=%d outside [1,%d] (obs_dim %d)", d->hidden, hmax, d->obs_dim);
+    return D2D_EUNSUPPORTED;
+  }
   if (d->kind == 0 && d->n_out > 32) { d2d_set_error("too many channels"); return D2D_EUNSUPPORTED; }
   if (d->v1 && (!d->c1 || !d->v2 || !d->c2)) { d2d_set_error("critic needs v1, c1, v2, c2"); return D2D_EINVAL; }
   MlpArgs a;
@@ -541,9 +570,12 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const void* obs, const
   if (g_policy_f32_mfma || a.F + 1 > 64) {
     if (a.rec) { d2d_set_error("the fp32-MFMA policy kernel reads fp32 obs only"); return D2D_EUNSUPPORTED; }
     const int ks = (a.F + 3) / 4;
-    if (ks <= 8) return ht <= 2 ? launch_policy_f32<8, 2>(a, s) : launch_policy_f32<8, 4>(a, s);
+    if (ks <= 8) return ht <= 2 ? launch_policy_f32<8, 2>(a, s) : ht <= 4 ? launch_policy_f32<8, 4>(a, s)
+                                                                      : launch_policy_f32<8, 8>(a, s);
     return ht <= 2 ? launch_policy_f32<16, 2>(a, s) : launch_policy_f32<16, 4>(a, s);
   }
-  if (a.F + 1 <= 32) return ht <= 2 ? launch_policy_split<1, 2>(a, s) : launch_policy_split<1, 4>(a, s);
+  if (a.F + 1 <= 32)
+    return ht <= 2 ? launch_policy_split<1, 2>(a, s) : ht <= 4 ? launch_policy_split<1, 4>(a, s)
+                                                               : launch_policy_split<1, 8>(a, s);
   return ht <= 2 ? launch_policy_split<2, 2>(a, s) : launch_policy_split<2, 4>(a, s);
 }

@@ -419,7 +419,7 @@ __device__ __forceinline__ void lds_row(float (&v)[8], const float (*xw)[XS], in
 // v_mfma_f32_16x16x4_f32 (an exact fmaf chain) straight from the accumulator registers; the
 // weight gradients dW1, dW2 on two-way RNE splits of their per-tile operands.
 template <int KC, int HT, int KIND, bool PAIR, bool U8, int AFIX = 0>
-__global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_actor_grad_kernel(UpdArgs a) {
+__global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? D2D_UPD_WAVES : 1) void ppo_actor_grad_kernel(UpdArgs a) {
   constexpr int QT = 2 * KC;  // input tiles of 16 in dW1
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, i = lane & 15;
@@ -944,7 +944,7 @@ __device__ __forceinline__ void load_critic_in(CriticIn<KC, U8>& in, const UpdAr
 }
 
 template <int KC, int HT, bool U8>
-__global__ __launch_bounds__(256, KC == 1 ? D2D_UPD_WAVES : 1) void ppo_critic_grad_kernel(UpdArgs a) {
+__global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? D2D_UPD_WAVES : 1) void ppo_critic_grad_kernel(UpdArgs a) {
   constexpr int QT = 2 * KC;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4, i = lane & 15;
@@ -1302,7 +1302,12 @@ static int check_update(const d2d_mlp_desc* d, int T, const void* obs, const voi
     return D2D_EINVAL;
   }
   if (T < 0 || d->n_envs < 0 || d->n_agents < 0) { d2d_set_error("negative size"); return D2D_EINVAL; }
-  if (d->hidden < 1 || d->hidden > 64) { d2d_set_error("hidden=%d outside [1,64]", d->hidden); return D2D_EUNSUPPORTED; }
+  // hidden <= 128 with one input chunk (F + 1 <= 32: the learners' default hidden_size 128), else <= 64
+  const int hmax = d->obs_dim + 1 <= 32 ? 128 : 64;
+  if (d->hidden < 1 || d->hidden > hmax) {
+    d2d_set_error("hidden=%d outside [1,%d] (obs_dim %d)", d->hidden, hmax, d->obs_dim);
+    return D2D_EUNSUPPORTED;
+  }
   if (d->obs_dim < 1 || d->obs_dim + 1 > 64) { d2d_set_error("obs_dim=%d outside [1,63]", d->obs_dim); return D2D_EUNSUPPORTED; }
   if (!critic && (d->n_out < 1 || d->n_out > 16)) { d2d_set_error("n_out=%d outside [1,16]", d->n_out); return D2D_EUNSUPPORTED; }
   if (!critic && d->kind != 0 && d->kind != 1) { d2d_set_error("kind must be 0 or 1"); return D2D_EINVAL; }
@@ -1394,7 +1399,7 @@ extern "C" int d2d_ppo_actor_grad(const d2d_mlp_desc* d, int32_t T, const void* 
   }
   const int ht = (a.H + 15) / 16;
   if (a.F + 1 <= 32) {
-    if (ht <= 2) launch_actor<1, 2>(a, s); else launch_actor<1, 4>(a, s);
+    if (ht <= 2) launch_actor<1, 2>(a, s); else if (ht <= 4) launch_actor<1, 4>(a, s); else launch_actor<1, 8>(a, s);
   } else {
     if (ht <= 2) launch_actor<2, 2>(a, s); else launch_actor<2, 4>(a, s);
   }
@@ -1427,7 +1432,7 @@ extern "C" int d2d_ppo_critic_grad(const d2d_mlp_desc* d, int32_t T, const void*
   }
   const int ht = (a.H + 15) / 16;
   if (a.F + 1 <= 32) {
-    if (ht <= 2) launch_critic<1, 2>(a, s); else launch_critic<1, 4>(a, s);
+    if (ht <= 2) launch_critic<1, 2>(a, s); else if (ht <= 4) launch_critic<1, 4>(a, s); else launch_critic<1, 8>(a, s);
   } else {
     if (ht <= 2) launch_critic<2, 2>(a, s); else launch_critic<2, 4>(a, s);
   }

@@ -288,7 +288,10 @@ int d2d_happo_chain(int32_t n_agents, int32_t T, int32_t E, const float* adv, co
  * kind 1: softmax -> Categorical over A = C+1 ids, actions = uint8 [E][N].
  * obs [E][N][F] (the env kernel's layout); logp, value [N][E].  forced != NULL
  * evaluates the given actions instead of sampling; deterministic = argmax / p > 0.5.
- * Sampling uses Philox stream 3 at (env_base + env, agent, rng_step). */
+ * Sampling uses Philox stream 3 at (env_base + env, agent, rng_step).
+ * Shapes: obs_dim <= 64, n_out <= 16, hidden <= 64, or hidden <= 128 when obs_dim + 1 <= 32 (the
+ * learners' default hidden_size 128 on the reference envs; one wave per SIMD there), else D2D_EUNSUPPORTED;
+ * the update kernels below take the same hidden limits with obs_dim + 1 <= 64. */
 typedef struct d2d_mlp_desc {
     int32_t n_agents, n_envs, obs_dim, hidden, n_out, kind;
     const float *w1, *b1, *w2, *b2;

@@ -314,8 +314,11 @@ def window_groups(obs, ep, L, padded):
     return groups
 
 
-def head(q, h, kind):
-    y = torch.relu(torch.baddbmm(q["b1"].unsqueeze(1), h, q["w1"].transpose(1, 2)))
+def head(q, h, kind, flip=None):
+    """The RNN head; flip (bool [N][B][H]) inverts the relu mask of those (sample, unit) pairs (their
+    pre-activations are within fp32 rounding of 0, so y ~ 0 either way and only the gradient's mask changes)."""
+    pre = torch.baddbmm(q["b1"].unsqueeze(1), h, q["w1"].transpose(1, 2))
+    y = torch.relu(pre) if flip is None else pre * ((pre > 0) ^ flip).to(pre.dtype)
     z = torch.baddbmm(q["b2"].unsqueeze(1), y, q["w2"].transpose(1, 2))
     return torch.sigmoid(z) if kind == "sigmoid" else torch.softmax(z, -1) if kind == "softmax" else z[..., 0]
 
@@ -496,13 +499,24 @@ def xp_grads_check(kind, grad_input, E, check=True, cfg=None):
         logp_old = (lp + (torch.rand(N, T, E, generator=g).to(dev) * 0.6 - 0.3)).float()
         W = torch.randn(N, T, E, generator=g).to(dev)
 
-    def ref(dtype):
+    amb = []  # per slot chunk: the head's ambiguous relu pairs (float64 pass)
+
+    def ref(dtype, flips=None):
         q = {k: v.to(dev, dtype).clone().requires_grad_() for k, v in p.items()}
         stats = torch.zeros(N, 2, dtype=torch.float64, device=dev)
         x = xall.to(dtype).view(N, T, E, L, F)
-        for t0 in range(0, T, 25):
+        for ci, t0 in enumerate(range(0, T, 25)):
             sl = slice(t0, t0 + 25)
-            o = head(q, gru_window(x[:, sl].reshape(N, -1, L, F), q["w_ih"], q["w_hh"], q["b_ih"], q["b_hh"]), kind)
+            hL = gru_window(x[:, sl].reshape(N, -1, L, F), q["w_ih"], q["w_hh"], q["b_ih"], q["b_hh"])
+            if dtype == torch.float64 and flips is None:
+                # relu pairs of the head's first layer within twice the fp32 dot-product error bound of 0
+                # (K = H products + bias): any fp32 evaluation may take the other mask there (the MLP
+                # update's relu-flip envelope, tools/gpu/ppo_grads_full_batch.py)
+                with torch.no_grad():
+                    pre = torch.baddbmm(q["b1"].unsqueeze(1), hL, q["w1"].transpose(1, 2))
+                    ab = torch.baddbmm(q["b1"].abs().unsqueeze(1), hL.abs(), q["w1"].abs().transpose(1, 2))
+                    amb.append(pre.abs() <= 2 * (H + 2) * 2.0 ** -24 * ab)
+            o = head(q, hL, kind, None if flips is None else flips[ci])
             o = o.reshape((N, 25, E) + o.shape[2:])
             if kind is None:
                 sq = ((o - W[:, sl].to(dtype)) ** 2).reshape(N, -1)
@@ -522,6 +536,30 @@ def xp_grads_check(kind, grad_input, E, check=True, cfg=None):
 
     r64, s64 = ref(torch.float64)
     r32, s32 = ref(torch.float32)
+    n_amb = int(sum(int(m.sum()) for m in amb))
+    # A kernel whose fp32 forward took the other side of an ambiguous head relu matches the float64 gradients
+    # with that mask flipped.  The backward is linear in the masks given the forward, so with Delta_i = the
+    # float64 gradients with agent k's i-th ambiguous head unit flipped (for every sample where it is ambiguous)
+    # minus r64, the candidates of agent k are r64 + sum_{i in S} Delta_i over the subsets S of its (at most
+    # four) ambiguous units; each agent is held to its nearest candidate, one subset for all eight tensors.
+    units = [set() for _ in range(N)]
+    for m in amb:
+        for k, u in torch.nonzero(m.any(1)).tolist():
+            units[k].add(u)
+    units = [sorted(u) for u in units]
+    n_cls = min(4, max((len(u) for u in units), default=0))
+    deltas = []
+    for idx in range(n_cls):
+        sel = torch.zeros(N, 1, H, dtype=torch.bool, device=dev)
+        for k in range(N):
+            if idx < len(units[k]):
+                sel[k, 0, units[k][idx]] = True
+        rf = ref(torch.float64, flips=[m & sel for m in amb])[0]
+        deltas.append({n: rf[n] - r64[n] for n in r64})
+    subsets = [tuple(i for i in range(n_cls) if (b >> i) & 1) for b in range(1 << n_cls)]
+    if n_amb:
+        print(f"  {n_amb} ambiguous head relu pairs over {sum(1 for u in units if u)} agents, up to "
+              f"{max(len(u) for u in units)} units per agent ({n_cls} searched)")
     pd = {k: v.to(dev).contiguous() for k, v in p.items()}
     W_te = W.permute(1, 2, 0).contiguous()
     xin = obs if grad_input == "f32" else to_record(obs.cpu())
@@ -534,10 +572,16 @@ def xp_grads_check(kind, grad_input, E, check=True, cfg=None):
     well = True
     errs = {}
     LAST[:] = [got, r64, r32]  # for tools/gpu/gru_long_diag.py
+    # per agent: the error of every candidate (subset S), scored over all tensors in units of their max|g|
+    cand = {n: torch.stack([(got[n].double() - r64[n] - sum((deltas[i][n] for i in S), torch.zeros_like(r64[n])))
+                            .abs().reshape(N, -1).amax(1) for S in subsets]) for n in r64}      # [subsets][N]
+    score = torch.stack([cand[n] / r64[n].abs().max() for n in r64]).amax(0)                 # [subsets][N]
+    best = score.argmin(0)                                                                      # [N]
+    if n_cls:
+        print(f"  agents matched with flipped head masks: {int((best > 0).sum())}")
     for name in r64:
-        gk = got[name].double()
         scale = r64[name].abs().max().item()
-        err64 = (gk - r64[name]).abs().max().item()
+        err64 = cand[name].gather(0, best[None])[0].max().item()
         band = (r32[name] - r64[name]).abs().max().item()
         errs[name] = (err64, band, scale)
         print(f"  {name}: max|g| {scale:.3e}  |kernel-f64| {err64:.2e}  |torchf32-f64| {band:.2e}")

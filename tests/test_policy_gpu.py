@@ -58,7 +58,9 @@ def torch_ref(actor, crit, obs):
 
 CASES = [("comb", 30, 64, 8, None), ("comb", 30, 64, 8, [23, 30, 23, 30, 23, 30, 30]), ("comb", 46, 64, 16, None),
          ("comb", 10, 20, 3, None), ("chsel", 12, 16, 5, None), ("chsel", 24, 64, 16, [24, 20, 24, 21, 24, 24, 24]),
-         ("chsel", 8, 40, 2, None), ("comb", 63, 32, 8, None), ("comb", 64, 64, 8, None), ("chsel", 31, 48, 9, None)]
+         ("chsel", 8, 40, 2, None), ("comb", 63, 32, 8, None), ("comb", 64, 64, 8, None), ("chsel", 31, 48, 9, None),
+         # the learners' default hidden_size 128 (ippo.py:225, d2d_ppo.py:222) and the modules' default 100
+         ("comb", 30, 128, 8, None), ("chsel", 12, 128, 5, None), ("comb", 23, 100, 8, [23, 20, 23, 23, 23, 23, 23])]
 
 
 @pytest.mark.parametrize("frac", [False, True])

@@ -124,6 +124,10 @@ CASES = [
     # configs[4] (xp_n_agents sweep) shapes bench.py times: 128 / 256 agents, C = 8, D = 7 -> F = 23
     ("comb", 128, 2, 72, 23, 64, 8, None, False),
     ("comb", 256, 2, 40, 23, 64, 8, None, False),
+    # the learners' default hidden_size 128 (ippo.py:225) and the modules' default 100: 8 hidden tiles
+    ("comb", 4, 3, 100, 30, 128, 8, None, False),
+    ("chsel", 3, 2, 70, 12, 128, 5, None, True),
+    ("comb", 3, 2, 45, 23, 100, 8, [23, 20, 23], False),
 ]
 
 
@@ -228,9 +232,10 @@ def test_update_deterministic_and_large():
     assert_grads(g1, r64, r32, None, F, conditioned(probs))
 
 
-def test_update_rejects_bad_shapes():
+@pytest.mark.parametrize("F,H", [(70, 16), (30, 129), (40, 128)])  # F + 1 > 64; H > 128; H > 64 with F + 1 > 32
+def test_update_rejects_bad_shapes(F, H):
     from d2dhip.update import actor_grads
-    N, T, E, F, H, A = 2, 1, 8, 70, 16, 4   # F + 1 > 64
+    N, T, E, A = 2, 1, 8, 4
     net = {"w1": torch.zeros(N, H, F, device="cuda"), "b1": torch.zeros(N, H, device="cuda"),
            "w2": torch.zeros(N, A, H, device="cuda"), "b2": torch.zeros(N, A, device="cuda")}
     obs = torch.zeros(T, E, N, F, device="cuda")
@@ -240,7 +245,7 @@ def test_update_rejects_bad_shapes():
         actor_grads(net, obs, acts, lo, lo, "comb")
 
 
-def _learner_pair(cls, kind, seed=0, E=96, N=6):
+def _learner_pair(cls, kind, seed=0, E=96, N=6, H=64):
     """Two identical learners (same init, same rollout) on a small batched env.  kind "c5": the
     xp_n_agents sweep env of configs[4] (N agents, 8 channels, deadlines 7, lambda 1/14, switch 0.8)."""
     import copy
@@ -271,7 +276,7 @@ def _learner_pair(cls, kind, seed=0, E=96, N=6):
     for _ in range(2):
         torch.manual_seed(seed)
         env = make_env()
-        kw = dict(hidden_size=64, gamma=0.6, policy_lr=3e-3, value_lr=1e-3, device="cuda", useRNN=False,
+        kw = dict(hidden_size=H, gamma=0.6, policy_lr=3e-3, value_lr=1e-3, device="cuda", useRNN=False,
                   combinatorial=kind in ("comb", "c5"))
         lr = cls(env, beta_entropy=0.05, **kw) if cls.__name__ == "D2DPPO" else cls(env, **kw)
         out.append(lr)
@@ -280,9 +285,10 @@ def _learner_pair(cls, kind, seed=0, E=96, N=6):
     return out, ro, copy
 
 
-@pytest.mark.parametrize("kind,algo,N", [("comb", "ippo", 6), ("chsel", "ippo", 6), ("comb", "d2d", 6),
-                                         ("chsel", "d2d", 6), ("c5", "d2d", 128), ("c5", "d2d", 256)])
-def test_fused_epoch_matches_torch_epoch(kind, algo, N):
+@pytest.mark.parametrize("kind,algo,N,H", [("comb", "ippo", 6, 64), ("chsel", "ippo", 6, 64), ("comb", "d2d", 6, 64),
+                                           ("chsel", "d2d", 6, 64), ("c5", "d2d", 128, 64), ("c5", "d2d", 256, 64),
+                                           ("comb", "ippo", 6, 128), ("chsel", "d2d", 6, 128)])
+def test_fused_epoch_matches_torch_epoch(kind, algo, N, H):
     """One learner epoch on the fused kernels == the torch agent-stacked epoch (same rollout, same
     permutation): losses 1e-5; post-Adam weights within 2% of the learning rate.  Adam's first
     steps are lr * g / (|g| + 1e-8): sign-like, so elements whose gradient is ~1e-8 move by a
@@ -290,7 +296,7 @@ def test_fused_epoch_matches_torch_epoch(kind, algo, N):
     from algorithms.d2d_ppo import D2DPPO
     from algorithms.ippo import iPPO
     cls = iPPO if algo == "ippo" else D2DPPO
-    (fused, ref), ro, copy = _learner_pair(cls, kind, E=96 if N <= 64 else 32, N=N)
+    (fused, ref), ro, copy = _learner_pair(cls, kind, E=96 if N <= 64 else 32, N=N, H=H)
     assert fused._fused_update_ok()
     if N > 64:  # the central critic's bf16-split GEMM path (S = 15 N + 8) is the one bench.py times
         assert ro.state_seq.shape[1] == 15 * N + 8 and fused._critic_split_forward(ro) is not None
