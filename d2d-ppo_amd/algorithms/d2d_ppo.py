@@ -373,13 +373,17 @@ class D2DPPO(BatchedLearnerBase):
             B = pre.shape[1]
             G = int(lib.d2d_critic_dpre_blocks(B))
             pre_c, w2v, dv_c = pre.contiguous(), l2.weight.detach().reshape(-1).contiguous(), dv.contiguous()
-            dhm = torch.empty((2 * H, B), dtype=torch.bfloat16, device=pre.device)
+            # dPre on a three-way RNE split (ABI v10): the two-way split's 2^-17 per product let near-zero dW1
+            # elements take the other sign than fp32 autograd's, which Adam's first step turns into 2 lr moves
+            # (the hidden-128 D2D reference trace's epoch-2 value loss, learner_d2d_mlp_comb_h128)
+            dhm = torch.empty((3 * H, B), dtype=torch.bfloat16, device=pre.device)
             part = torch.empty((G, 2 * H), dtype=torch.float32, device=pre.device)
-            _lib.check(lib.d2d_critic_dpre_split(H, B, pre_c.data_ptr(), w2v.data_ptr(), dv_c.data_ptr(), dhm.data_ptr(),
-                                                 part.data_ptr(), G, _lib.stream_ptr()), "d2d_critic_dpre_split")
+            _lib.check(lib.d2d_critic_dpre_split3(H, B, pre_c.data_ptr(), w2v.data_ptr(), dv_c.data_ptr(), dhm.data_ptr(),
+                                                  part.data_ptr(), G, _lib.stream_ptr()), "d2d_critic_dpre_split3")
             sums = part.sum(0)                                                              # [2H]: db1 | dW2
-            g = self._dw1_gemm(dhm, ro.state_bf16)[:, :l1.weight.shape[1]]                 # [2H][S]
-            grads = {l1.weight: g[:H] + g[H:], l1.bias: sums[:H], l2.weight: sums[H:], l2.bias: g_b2}
+            g = self._dw1_gemm(dhm, ro.state_bf16)[:, :l1.weight.shape[1]]                 # [3H][S]
+            grads = {l1.weight: (g[2 * H:] + g[H:2 * H]) + g[:H], l1.bias: sums[:H], l2.weight: sums[H:],
+                     l2.bias: g_b2}
             for prm, gr in grads.items():
                 prm.grad = gr.reshape(prm.shape).contiguous()
         return value_loss

@@ -176,6 +176,17 @@ __device__ __forceinline__ uint32_t arrival_value(const EnvArgs& a, const d2d_ag
   return (uint64_t)r.x < ag.arrival_thr ? 1u : 0u;
 }
 
+// one 16-byte record word, streaming (non-temporal) when nt (D2D_OPT_NT_STORES): the record is written once
+// and read by the next slot's consumers only, so it need not displace the env state from L2 / MALL
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_rec(uint4* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d, bool nt) {
+  const v4u32 v = {a, b, c, d};
+  if (nt)
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u32*>(p));
+  else
+    *reinterpret_cast<v4u32*>(p) = v;
+}
+
 // ------------------------------------------------------ LDS -> HBM flushing
 // Copy `count` floats from LDS to a contiguous global range with float4 stores
 // when both ends allow it (every obs/state row group of a block is contiguous).
@@ -525,8 +536,9 @@ __global__ __launch_bounds__(kMaxAgents) __attribute__((amdgpu_waves_per_eu(D2D_
           word |= (q == (F >> 2)) ? (1u << (8 * (F & 3))) : 0u;
           v[q] = word;
         }
-        dst[0] = make_uint4(v[0], v[1], v[2], v[3]);
-        dst[1] = make_uint4(v[4], v[5], v[6], v[7]);
+        const bool nt = a.flags & 1u;
+        st_rec(dst, v[0], v[1], v[2], v[3], nt);
+        st_rec(dst + 1, v[4], v[5], v[6], v[7], nt);
         built = true;
       }
     }

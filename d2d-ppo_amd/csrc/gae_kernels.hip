@@ -815,6 +815,10 @@ extern "C" int d2d_f32_to_bf16_exact(int64_t n, const float* x, uint16_t* out, i
 // One pass over pre instead of ~8 torch elementwise kernels over [H][B].  Block g owns samples
 // [g chunk, (g + 1) chunk); its sums are reduced in a fixed order (wave shuffles, then the 4 waves
 // in order): deterministic, no atomics.
+// PARTS = 2 (ABI v7) or 3 (ABI v10: dhm [3H][B], rows 2H + h = RNE(dpre - hb - mb): dW1 = sum of the three
+// parts' GEMMs is then accurate to ~2^-24 per product term, torch fp32's level, where the two-way split's
+// 2^-17 let near-zero dW1 elements take the other sign and Adam's first step move them by 2 lr)
+template <int PARTS>
 __global__ __launch_bounds__(256) void critic_dpre_kernel(int H, int64_t B, int64_t chunk, const float* __restrict__ pre,
                                                           const float* __restrict__ w2, const float* __restrict__ dv,
                                                           uint16_t* __restrict__ dhm, float* __restrict__ partial) {
@@ -829,9 +833,11 @@ __global__ __launch_bounds__(256) void critic_dpre_kernel(int H, int64_t B, int6
       const float p = pre[(int64_t)h * B + b], d = dv[b];
       const float dp = p > 0.f ? m * d : 0.f;
       const __bf16 hb = (__bf16)dp;  // v_cvt_pk_bf16_f32: round to nearest even, like torch's .to(bfloat16)
-      const __bf16 mb = (__bf16)(dp - (float)hb);
+      const float r1 = dp - (float)hb;  // exact
+      const __bf16 mb = (__bf16)r1;
       dhm[(int64_t)h * B + b] = __builtin_bit_cast(uint16_t, hb);
       dhm[(int64_t)(H + h) * B + b] = __builtin_bit_cast(uint16_t, mb);
+      if constexpr (PARTS == 3) dhm[(int64_t)(2 * H + h) * B + b] = __builtin_bit_cast(uint16_t, (__bf16)(r1 - (float)mb));
       s_db += dp;
       s_gw += fmaxf(p, 0.f) * d;
     }
@@ -866,8 +872,21 @@ extern "C" int d2d_critic_dpre_split(int32_t H, int64_t B, const float* pre, con
     return D2D_EINVAL;
   }
   const int64_t chunk = (B + G - 1) / G;
-  hipLaunchKernelGGL(critic_dpre_kernel, dim3((unsigned)G), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), H, B,
-                     chunk, pre, w2, dv, dhm, partial);
+  hipLaunchKernelGGL(critic_dpre_kernel<2>, dim3((unsigned)G), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), H,
+                     B, chunk, pre, w2, dv, dhm, partial);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
+extern "C" int d2d_critic_dpre_split3(int32_t H, int64_t B, const float* pre, const float* w2, const float* dv,
+                                      uint16_t* dhm, float* partial, int32_t G, void* stream) {
+  if (H < 1 || B < 0 || G != d2d_critic_dpre_blocks(B) || !pre || !w2 || !dv || !dhm || !partial) {
+    d2d_set_error("d2d_critic_dpre_split3: bad arguments (G must be d2d_critic_dpre_blocks(B))");
+    return D2D_EINVAL;
+  }
+  const int64_t chunk = (B + G - 1) / G;
+  hipLaunchKernelGGL(critic_dpre_kernel<3>, dim3((unsigned)G), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), H,
+                     B, chunk, pre, w2, dv, dhm, partial);
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
 }

@@ -179,10 +179,11 @@ __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* 
 }
 
 #ifndef D2D_POLICY_RNG_EARLY
-#define D2D_POLICY_RNG_EARLY 1  // draw the paired epilogue's Philox block before the tile MFMAs (A/B: 0)
-#endif
-#ifndef D2D_POLICY_SGB
-#define D2D_POLICY_SGB 0  // A/B: scheduling-group hints interleaving the tile MFMAs with the VALU (incl. Philox)
+// 1 (A/B): draw the paired epilogue's Philox block before the tile MFMAs instead of in the epilogue.  The
+// scheduler then issues the ten dependent rounds as one chain ahead of the MFMAs rather than in their gaps,
+// and the partner wave already hides the chain: 233.7 / 229.6 vs 232.7 / 227.5 us per 65,536-env slot
+// (r04i, two boxes' runs each) -- no gain, off
+#define D2D_POLICY_RNG_EARLY 0
 #endif
 #ifndef D2D_POLICY_L2_F32
 // 1 (A/B): actor layer 2 on v_mfma_f32_16x16x4_f32 straight from relu(H^T) (an exact fmaf chain, 16 MFMAs
@@ -459,13 +460,6 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
     float v0, v1;
     tile(tt, lg0, v0);
     tile(tt + 1, lg1, v1);
-#if D2D_POLICY_SGB
-#pragma unroll
-    for (int q = 0; q < 36; ++q) {  // 2 MFMAs, then 8 VALU (72 MFMAs, ~300 VALU in the region)
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x002, 8, 0);
-    }
-#endif
     __builtin_amdgcn_sched_barrier(0);        // the slots are read before the next DMA reuses them
     if (A <= 8) {
       // one epilogue for both tiles: lanes 0-31 keep tile tt (action groups 0, 1), lanes 32-63

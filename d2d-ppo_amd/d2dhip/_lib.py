@@ -129,6 +129,7 @@ _SIGS = {
                                                   ctypes.c_int64, _p, _p]),
     "d2d_critic_dpre_blocks": (ctypes.c_int32, [ctypes.c_int64]),
     "d2d_critic_dpre_split": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, _p, _p, _p, _p, _p, ctypes.c_int32, _p]),
+    "d2d_critic_dpre_split3": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, _p, _p, _p, _p, _p, ctypes.c_int32, _p]),
     "d2d_policy_mlp_step": (ctypes.c_int, [ctypes.POINTER(MlpDesc), _p, _p, ctypes.c_uint32, ctypes.c_int32, _p, _p,
                                             _p, _p]),
     "d2d_ppo_workspace": (ctypes.c_int64, [ctypes.c_int32] * 6),

@@ -47,7 +47,7 @@ extern "C" {
                               6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_states_to_bf16_exact,
                               d2d_critic_dpre_split; 8: d2d_gae_scan_moments, d2d_normalize_pair;
                               9: d2d_gae_scan_moments without outputs, d2d_gae_scan_normalized;
-                              10: d2d_states_to_bf16_padded */
+                              10: d2d_states_to_bf16_padded, d2d_critic_dpre_split3 */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -270,6 +270,10 @@ int d2d_states_to_bf16_padded(int32_t T, int32_t E, int32_t S, int64_t ld, const
 int32_t d2d_critic_dpre_blocks(int64_t B);
 int d2d_critic_dpre_split(int32_t H, int64_t B, const float* pre, const float* w2, const float* dv, uint16_t* dhm,
                           float* partial, int32_t G, void* stream);
+/* The same with a three-way RNE split, dhm [3H][B] (rows 2H + h: RNE(dpre - rows h - rows H + h)): the dW1
+ * GEMM over the three parts is accurate to ~2^-24 per product term (torch fp32's level).  ABI v10. */
+int d2d_critic_dpre_split3(int32_t H, int64_t B, const float* pre, const float* w2, const float* dv, uint16_t* dhm,
+                           float* partial, int32_t G, void* stream);
 
 /* D2D-PPO's sequential agent update chain (algorithms/d2d_ppo.py:405-433): for the agent
  * permutation perm[0..N), M[perm[j]][b] = adv[b] * prod_{l<j} exp(logp_new[perm[l]][b] -

@@ -200,6 +200,10 @@ def test_learner_matches_reference(name, E):
         # every reference GRU shape (incl. hidden 64 / 16-step windows and the 46-input 6 x 16-channel
         # env) rolls out and trains on the HIP GRU kernels, not the torch fallback
         assert lr._gru_ok() and lr._fused_update_ok()
+    else:
+        # every MLP trace -- incl. the learners' default hidden_size 128 (learner_*_h128) -- runs on the fused
+        # HIP policy and update kernels
+        assert lr._fused_ok() and lr._fused_update_ok()
 
     # --- one training iteration on the same rollout
     lr._rollout = lambda num_episodes, teacher=None, _ro=ro: _ro

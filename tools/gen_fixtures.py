@@ -496,6 +496,14 @@ DRIVER_VARIANTS = {
 }
 
 
+# The learners' default hidden_size 128 (ippo.py:225, d2d_ppo.py:222: what a user gets without the drivers'
+# explicit 64), MLP policies, on the kernels' 8-hidden-tile path (gen_learner_defaults)
+DEFAULT_VARIANTS = {
+    "mlp_comb_h128": ("comb", False, True, 4, 128, 20, ("ippo", "d2d"), 2),
+    "mlp_cat_h128": ("chsel", False, False, 3, 128, 20, ("ippo", "d2d"), 2),
+}
+
+
 def _learner_env(kind, episode_length=20):
     if kind == "comb_xpload":
         # xp_load.py:60-75 on setup_8_channels at load 1/2, homogeneous obs (14 + 2 * 8 = 30 inputs)
@@ -660,6 +668,11 @@ def gen_learner4():
     gen_learner(only=["mlp_comb", "rnn_cat", "mlp_d2denv"], episodes=4, suffix="_ep4")
 
 
+def gen_learner_defaults():
+    """MLP traces at the learners' default hidden_size 128 (DEFAULT_VARIANTS)."""
+    gen_learner(only=[], variants=DEFAULT_VARIANTS)
+
+
 def gen_learner_drivers():
     """GRU traces at the reference drivers' own network shapes (DRIVER_VARIANTS): hidden 64 with a
     16-step window, and the 6 x 16-channel env with 46 inputs."""
@@ -712,7 +725,7 @@ if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
     table = {"data": gen_data, "env": gen_env, "d2denv": gen_d2denv, "gae": gen_gae, "learner": gen_learner,
              "baselines": gen_baselines, "evaltest": gen_evaltest, "learner4": gen_learner4,
-             "learner_drivers": gen_learner_drivers}
+             "learner_drivers": gen_learner_drivers, "learner_defaults": gen_learner_defaults}
     # `learner <variant> ...` regenerates only the named learner variants
     which = sys.argv[1:2] if sys.argv[1:2] == ["learner"] else sys.argv[1:]
     for w in which or list(table):

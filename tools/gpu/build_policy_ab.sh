@@ -15,13 +15,13 @@ for n in pl2f pl2f2; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib/libd2dhip_$n.so build/env_kernels.o \
     build/gae_kernels.o build/abl/policy_kernels_$n.o build/update_kernels.o build/gru_kernels.o build/abi.o
 done
-# r04 scheduling A/B: prng0 = Philox drawn in the epilogue (round 3), psgb = early draw + scheduling-group hints
-for spec in "prng0=-DD2D_POLICY_RNG_EARLY=0" "psgb=-DD2D_POLICY_SGB=1"; do
+# r04 scheduling A/B: prng1 = Philox drawn before the tile MFMAs (D2D_POLICY_RNG_EARLY=1)
+for spec in "prng1=-DD2D_POLICY_RNG_EARLY=1"; do
   n=${spec%%=*}
   /opt/rocm/bin/hipcc $F ${spec#*=} -c csrc/policy_kernels.hip -o build/abl/policy_kernels_$n.o &
 done
 wait
-for n in prng0 psgb; do
+for n in prng1; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o lib/libd2dhip_$n.so build/env_kernels.o \
     build/gae_kernels.o build/abl/policy_kernels_$n.o build/update_kernels.o build/gru_kernels.o build/abi.o
 done
