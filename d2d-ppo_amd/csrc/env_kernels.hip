@@ -1153,6 +1153,7 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
 }  // namespace
 
 extern int g_policy_f32_mfma;  // policy_kernels.hip
+extern int g_policy_critic_split;  // policy_kernels.hip
 extern std::atomic<int> g_gru_grad_history;  // gru_kernels.hip
 
 extern "C" int d2d_set_option(int32_t option, int32_t value) {
@@ -1166,6 +1167,10 @@ extern "C" int d2d_set_option(int32_t option, int32_t value) {
   }
   if (option == D2D_OPT_POLICY_F32_MFMA) {
     g_policy_f32_mfma = value ? 1 : 0;
+    return D2D_OK;
+  }
+  if (option == D2D_OPT_POLICY_CRITIC_SPLIT) {
+    g_policy_critic_split = value ? 1 : 0;
     return D2D_OK;
   }
   d2d_set_error("unknown option %d", option);

@@ -26,7 +26,9 @@ struct MlpArgs {
 };
 
 constexpr uint32_t kStreamPolicy = 3;
-enum { kModeSample = 0, kModeDeterministic = 1, kModeForced = 2, kModeRuntime = -1 };
+// kModeValue: the split kernel's value-only instantiation (the iPPO critic as its own launch beside the actor:
+// policy_kernels.hip, D2D_POLICY_CRITIC_SPLIT)
+enum { kModeSample = 0, kModeDeterministic = 1, kModeForced = 2, kModeValue = 3, kModeRuntime = -1 };
 // The epilogue takes logits pre-multiplied by log2(e) (folded into W2, b2 by the split kernel) so
 // the softmax exponentials are bare v_exp_f32 (exp2, 1 ulp); the relative rounding of the scaled
 // logits is ~2^-24, i.e. a log-prob error ~|logit| * 1e-7.

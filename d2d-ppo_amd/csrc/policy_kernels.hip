@@ -19,7 +19,9 @@
 // layer is a per-lane dot product + 2 cross-group shuffles.  fp32 MFMA is an
 // exact k-ordered fmaf chain, so results match the torch fp32 reference to
 // ~1e-6 (parity tests use 1e-5).
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 #include "policy_epilogue.h"
 
@@ -227,8 +229,10 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
     }
   }
 
-  // ---- weight fragments of agent k, split once per workgroup
-  Parts w1p[HT][KC], v1p[CRITIC ? HT : 1][KC];
+  // ---- weight fragments of agent k, split once per workgroup (kModeValue: the critic's only)
+  constexpr bool ACTOR = MODE != kModeValue;
+  static_assert(ACTOR || CRITIC, "the value-only instantiation needs the critic");
+  Parts w1p[ACTOR ? HT : 1][KC], v1p[CRITIC ? HT : 1][KC];
 #if D2D_POLICY_L2_F32
   float w2f[HT][4];  // A operand of step (t, r): row = action i, k-slot g <-> hidden 16t + 4g + r
 #else
@@ -253,7 +257,7 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
           if constexpr (CRITIC)
             vv[j] = !hok ? 0.f : col < F ? V1[(size_t)hrow * F + col] : col == F ? a.c1[(size_t)k * H + hrow] : 0.f;
         }
-        w1p[t][c] = split3(wv);
+        if constexpr (ACTOR) w1p[t][c] = split3(wv);
         if constexpr (CRITIC) v1p[t][c] = split3(vv);
       }
 #pragma unroll
@@ -272,7 +276,7 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
       }
 #else
 #pragma unroll
-    for (int c2 = 0; c2 < HT / 2; ++c2) {
+    for (int c2 = 0; c2 < (ACTOR ? HT / 2 : 0); ++c2) {
       // element j of lane group g <-> hidden 16 * (2 c2 + (j >> 2)) + 4 g + (j & 3): the
       // accumulator registers of layer-1 tiles 2 c2 and 2 c2 + 1
       float wv[8];
@@ -363,10 +367,12 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
       for (int t = 0; t < HT; ++t) {
 #pragma unroll
         for (int c = 0; c < KC; ++c) {
-          const f32x4 za = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ha[t];
-          ha[t] = mfma_bf16(w1p[t][c].l, xh[c], za);
-          ha[t] = mfma_bf16(w1p[t][c].m, xh[c], ha[t]);
-          ha[t] = mfma_bf16(w1p[t][c].h, xh[c], ha[t]);
+          if constexpr (ACTOR) {
+            const f32x4 za = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ha[t];
+            ha[t] = mfma_bf16(w1p[t][c].l, xh[c], za);
+            ha[t] = mfma_bf16(w1p[t][c].m, xh[c], ha[t]);
+            ha[t] = mfma_bf16(w1p[t][c].h, xh[c], ha[t]);
+          }
           if constexpr (CRITIC) {
             const f32x4 zv = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : hv[t];
             hv[t] = mfma_bf16(v1p[t][c].l, xh[c], zv);
@@ -381,9 +387,11 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
           const Parts xp = split3(xc[c]);
 #pragma unroll
           for (int t = 0; t < HT; ++t) {
-            ha[t] = mfma_bf16(w1p[t][c].h, xp.l, ha[t]);
-            ha[t] = mfma_bf16(w1p[t][c].m, xp.m, ha[t]);
-            ha[t] = mfma_bf16(w1p[t][c].h, xp.m, ha[t]);
+            if constexpr (ACTOR) {
+              ha[t] = mfma_bf16(w1p[t][c].h, xp.l, ha[t]);
+              ha[t] = mfma_bf16(w1p[t][c].m, xp.m, ha[t]);
+              ha[t] = mfma_bf16(w1p[t][c].h, xp.m, ha[t]);
+            }
             if constexpr (CRITIC) {
               hv[t] = mfma_bf16(v1p[t][c].h, xp.l, hv[t]);
               hv[t] = mfma_bf16(v1p[t][c].m, xp.m, hv[t]);
@@ -414,7 +422,7 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
       }
 #else
 #pragma unroll
-      for (int c2 = 0; c2 < HT / 2; ++c2) {
+      for (int c2 = 0; c2 < (ACTOR ? HT / 2 : 0); ++c2) {
         float hvals[8];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -461,6 +469,13 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
     tile(tt, lg0, v0);
     tile(tt + 1, lg1, v1);
     __builtin_amdgcn_sched_barrier(0);        // the slots are read before the next DMA reuses them
+    if constexpr (!ACTOR) {
+      // value only: lane group 0 stores tile tt's values, group 1 tile tt + 1's (every lane of a row
+      // holds its env's value after the group sum)
+      const int envv = g == 0 ? env0 : env1;
+      if (g < 2 && envv < a.E) a.value_out[(size_t)k * a.E + envv] = g == 0 ? v0 : v1;
+      continue;
+    }
     if (A <= 8) {
       // one epilogue for both tiles: lanes 0-31 keep tile tt (action groups 0, 1), lanes 32-63
       // take tile tt + 1's lanes 0-31 (permlane32_swap: vdst upper half <- src lower half)
@@ -485,6 +500,12 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
 using namespace d2d;
 
 int g_policy_f32_mfma = 0;  // d2d_set_option(D2D_OPT_POLICY_F32_MFMA, 1): fp32-MFMA kernel
+#ifndef D2D_POLICY_CRITIC_SPLIT
+// the iPPO critic's weight fragments (48 + 16 registers at H = 64) hold the fused actor + critic kernel at two
+// waves per SIMD (224 VGPRs; the actor alone: 137); 1 = the value as a separate value-only launch
+#define D2D_POLICY_CRITIC_SPLIT 0
+#endif
+int g_policy_critic_split = D2D_POLICY_CRITIC_SPLIT;  // d2d_set_option(D2D_OPT_POLICY_CRITIC_SPLIT, v)
 
 template <int KS, int HT>
 static int launch_policy_f32(const MlpArgs& a, hipStream_t s) {
@@ -500,29 +521,78 @@ static int launch_policy_f32(const MlpArgs& a, hipStream_t s) {
   return D2D_OK;
 }
 
+
+// Workgroups of kernel K resident on the device at once (its occupancy x the CU count), queried once
+template <auto K>
+static int resident_blocks() {
+  static int n = 0;
+  if (!n) {
+    int per = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, K, 256, 0) != hipSuccess) per = 2;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    n = std::max(1, per * cus);
+  }
+  return n;
+}
+static int g_policy_sizing = -1;  // (A/B) D2D_POLICY_SIZING=r: r resident rounds (0: the 256-envs-per-wave rule only)
+
+// envs per wave for one resident round of K (every wave's per-agent weight split amortised over all of its
+// tiles, no partial last round); the forced mode keeps <= 256 (its forced bytes are preloaded per wave)
+template <auto K>
+static MlpArgs one_round(MlpArgs x) {
+  if (g_policy_sizing < 0) {
+    const char* e = getenv("D2D_POLICY_SIZING");
+    g_policy_sizing = e ? atoi(e) : 1;
+  }
+  if (x.forced || g_policy_sizing <= 0) return x;
+  const int64_t per_agent = std::max<int64_t>(1, (int64_t)resident_blocks<K>() * g_policy_sizing / x.N);
+  int64_t epw = ((int64_t)x.E + 4 * per_agent - 1) / (4 * per_agent);
+  epw = (epw + 31) / 32 * 32;
+  x.envs_per_wave = (int)std::max<int64_t>(x.envs_per_wave, epw);
+  return x;
+}
+template <auto K>
+static void launch_one(const MlpArgs& a, hipStream_t s) {
+  const MlpArgs x = one_round<K>(a);
+  const dim3 grid(x.N, (x.E + 4 * x.envs_per_wave - 1) / (4 * x.envs_per_wave));
+  hipLaunchKernelGGL(K, grid, dim3(256), 0, s, x);
+}
+
 template <int KC, int HT, int KIND, bool CRITIC, bool U8>
-static void launch_split_fmt(const MlpArgs& a, dim3 grid, hipStream_t s) {
-  if (a.forced) hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeForced, U8>), grid, dim3(256), 0, s, a);
-  else if (a.deterministic)
-    hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeDeterministic, U8>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((policy_split_kernel<KC, HT, KIND, CRITIC, kModeSample, U8>), grid, dim3(256), 0, s, a);
+static void launch_split_fmt(const MlpArgs& a, hipStream_t s) {
+  if (a.forced) launch_one<policy_split_kernel<KC, HT, KIND, CRITIC, kModeForced, U8>>(a, s);
+  else if (a.deterministic) launch_one<policy_split_kernel<KC, HT, KIND, CRITIC, kModeDeterministic, U8>>(a, s);
+  else launch_one<policy_split_kernel<KC, HT, KIND, CRITIC, kModeSample, U8>>(a, s);
+}
+
+template <int KC, int HT, int KIND, bool CRITIC, bool U8>
+static void launch_split_mode(const MlpArgs& a, hipStream_t s) {
+  if (CRITIC && g_policy_critic_split) {
+    // the actor (actions, log-probs) and the critic value as two launches of the same arithmetic, each at its
+    // own occupancy (actor 137 VGPRs, value-only 119, fused 224 at H = 64)
+    MlpArgs av = a;
+    av.v1 = av.c1 = av.v2 = av.c2 = nullptr;
+    launch_split_fmt<KC, HT, KIND, false, U8>(av, s);
+    launch_one<policy_split_kernel<KC, HT, KIND, true, kModeValue, U8>>(a, s);
+    return;
+  }
+  launch_split_fmt<KC, HT, KIND, CRITIC, U8>(a, s);
 }
 
 template <int KC, int HT, int KIND, bool CRITIC>
-static void launch_split_mode(const MlpArgs& a, dim3 grid, hipStream_t s) {
-  if (a.rec) launch_split_fmt<KC, HT, KIND, CRITIC, true>(a, grid, s);
-  else launch_split_fmt<KC, HT, KIND, CRITIC, false>(a, grid, s);
+static void launch_split_kind(const MlpArgs& a, hipStream_t s) {
+  if (a.rec) launch_split_mode<KC, HT, KIND, CRITIC, true>(a, s);
+  else launch_split_mode<KC, HT, KIND, CRITIC, false>(a, s);
 }
 
 template <int KC, int HT>
 static int launch_policy_split(const MlpArgs& a, hipStream_t s) {
-  const int envs_per_block = 4 * a.envs_per_wave;  // 4 waves
-  dim3 grid(a.N, (a.E + envs_per_block - 1) / envs_per_block);
   const bool critic = a.v1 != nullptr;
-  if (a.kind == 0 && critic) launch_split_mode<KC, HT, 0, true>(a, grid, s);
-  else if (a.kind == 0) launch_split_mode<KC, HT, 0, false>(a, grid, s);
-  else if (critic) launch_split_mode<KC, HT, 1, true>(a, grid, s);
-  else launch_split_mode<KC, HT, 1, false>(a, grid, s);
+  if (a.kind == 0 && critic) launch_split_kind<KC, HT, 0, true>(a, s);
+  else if (a.kind == 0) launch_split_kind<KC, HT, 0, false>(a, s);
+  else if (critic) launch_split_kind<KC, HT, 1, true>(a, s);
+  else launch_split_kind<KC, HT, 1, false>(a, s);
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
 }

@@ -42,6 +42,7 @@ D2D_OBS_F32, D2D_OBS_U8 = 0, 1
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
 D2D_OPT_GRU_GRAD_HISTORY = 3  # 1: d2d_gru_grad through the global row history even where the LDS path applies
+D2D_OPT_POLICY_CRITIC_SPLIT = 4  # 1: the iPPO critic value as its own launch beside the actor (bitwise the same)
 
 _p = ctypes.c_void_p
 

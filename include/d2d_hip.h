@@ -389,8 +389,11 @@ int d2d_gru_grad(const d2d_gru_desc* desc, int32_t T, const void* obs, const voi
  *   global row history also where the cooperative LDS path applies (ABI 9; A/B timing and tests).  It
  *   selects the workspace layout: set it before the d2d_gru_grad_workspace query that sizes the buffer
  *   (d2d_gru_grad re-checks the size against its own snapshot of the option and returns D2D_EINVAL
- *   for a buffer sized under the other setting). */
-enum { D2D_OPT_NT_STORES = 1, D2D_OPT_POLICY_F32_MFMA = 2, D2D_OPT_GRU_GRAD_HISTORY = 3 };
+ *   for a buffer sized under the other setting).
+ * D2D_OPT_POLICY_CRITIC_SPLIT: d2d_policy_mlp_step with a critic runs the actor and the critic value as two
+ *   launches of the split kernel (1) or as one fused launch (0); the same arithmetic either way (bitwise
+ *   identical actions, log-probs and values).  Default: policy_kernels.hip's D2D_POLICY_CRITIC_SPLIT. */
+enum { D2D_OPT_NT_STORES = 1, D2D_OPT_POLICY_F32_MFMA = 2, D2D_OPT_GRU_GRAD_HISTORY = 3, D2D_OPT_POLICY_CRITIC_SPLIT = 4 };
 int d2d_set_option(int32_t option, int32_t value);
 
 const char* d2d_last_error(void);

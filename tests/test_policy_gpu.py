@@ -175,3 +175,36 @@ def test_forced_full_waves_equal_sampled_logp(kind, F, H, A, in_dims):
         ref_lp = Categorical(probs=probs, validate_args=False).log_prob(acts.t().long())
     well = ((probs > 1e-3) & (probs < 1 - 1e-3)).all(-1)
     torch.testing.assert_close(lp2[well], ref_lp[well], rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("kind,F,H,A", [("comb", 30, 64, 8), ("chsel", 12, 64, 5)])
+def test_one_round_waves_and_critic_split(kind, F, H, A):
+    """Sampling and deterministic launches size every wave to one resident round (64 agents x 32,845 envs: about
+    1,000 envs per wave, a ragged tail); forced launches keep 256 envs per wave.  The sampled log-probs equal the
+    forced evaluation's bit for bit, values match torch (1e-5), and the actor + value-only launches
+    (D2D_OPT_POLICY_CRITIC_SPLIT) reproduce the fused kernel's actions, log-probs and values bit for bit."""
+    from d2dhip import _lib
+    from d2dhip.policy import policy_mlp_step
+    lib = _lib.require_gpu()
+    N, E = 64, 32768 + 77
+    actor, crit, obs = make(kind, N, E, F, H, A, seed=11)
+    acts, lp, val = policy_mlp_step(actor, obs, kind, crit, rng_step=4, seed=5)
+    acts2, lp2, val2 = policy_mlp_step(actor, obs, kind, crit, forced=acts)
+    assert torch.equal(acts2, acts)
+    torch.testing.assert_close(lp2, lp, rtol=0, atol=0)
+    torch.testing.assert_close(val2, val, rtol=0, atol=0)
+    _, v = torch_ref(actor, crit, obs)
+    torch.testing.assert_close(val, v, rtol=0, atol=1e-5)
+    try:
+        lib.d2d_set_option(_lib.D2D_OPT_POLICY_CRITIC_SPLIT, 1)
+        acts3, lp3, val3 = policy_mlp_step(actor, obs, kind, crit, rng_step=4, seed=5)
+        acts_d3, lp_d3, val_d3 = policy_mlp_step(actor, obs, kind, crit, deterministic=True)
+    finally:
+        lib.d2d_set_option(_lib.D2D_OPT_POLICY_CRITIC_SPLIT, 0)
+    assert torch.equal(acts3, acts)
+    torch.testing.assert_close(lp3, lp, rtol=0, atol=0)
+    torch.testing.assert_close(val3, val, rtol=0, atol=0)
+    acts_d, lp_d, val_d = policy_mlp_step(actor, obs, kind, crit, deterministic=True)
+    assert torch.equal(acts_d3, acts_d)
+    torch.testing.assert_close(lp_d3, lp_d, rtol=0, atol=0)
+    torch.testing.assert_close(val_d3, val_d, rtol=0, atol=0)
