@@ -213,22 +213,6 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
   const int tiles = a.envs_per_wave / 16;
   const int wave_env0 = (by * (blockDim.x >> 6) + wave) * a.envs_per_wave;
 
-  // ---- forced mode with the paired epilogue (A <= 8: one forced byte per cell): every forced
-  // byte this lane's epilogues will read, loaded before the weight split so their latency hides
-  // under it.  A load inside the tile loop would be waited for with vmcnt(0) and drain the obs
-  // DMA ring every tile pair.  Pair p of lane (g, i) is env wave_env0 + 32 p + 16 (g >> 1) + i,
-  // byte p & 3 of word p >> 2 (envs_per_wave <= 256: at most 8 pairs).
-  // Branch-free: all eight loads are issued (clamped to cell 0), and packed after the split.
-  uint32_t fpk[2] = {0u, 0u}, fv[8];
-  if constexpr (MODE == kModeForced) {
-    const unsigned char* fb = reinterpret_cast<const unsigned char*>(a.forced);
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int env = wave_env0 + 32 * p + 16 * (g >> 1) + i;
-      fv[p] = fb[(A <= 8 && 2 * p < tiles && env < a.E) ? (size_t)env * N + k : 0];
-    }
-  }
-
   // ---- weight fragments of agent k, split once per workgroup (kModeValue: the critic's only)
   constexpr bool ACTOR = MODE != kModeValue;
   static_assert(ACTOR || CRITIC, "the value-only instantiation needs the critic");
@@ -295,19 +279,23 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
     }
   }
   const float c2 = CRITIC ? a.c2[k] : 0.f;
-  if constexpr (MODE == kModeForced) {
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int env = wave_env0 + 32 * p + 16 * (g >> 1) + i;
-      fpk[p >> 2] |= (2 * p < tiles && env < a.E ? fv[p] : 0u) << (8 * (p & 3));
-    }
-  }
 
   // Two obs register sets alternate (loop unrolled by two), so each tile's loads are issued two
   // tiles ahead of their use without a register copy that would wait on them early.
   constexpr int RING = ring_tiles<KC, U8>();
   constexpr int DPC = chunk_dwords<U8>();
   __shared__ float ring[4][RING][KC][DPC][64];
+  // forced mode: the forced-action words of each tile travel through the same DMA ring (one more
+  // buffer_load_dword ... lds per tile: lane i of group 0 brings the dword holding env i's byte), so no
+  // register load inside the tile loop drains the ring with vmcnt(0) and a wave can run any number of
+  // tiles (one resident round).  Paired epilogue (A <= 8, one byte per cell) only; otherwise the DMA is
+  // aimed outside the buffer (no traffic) and the epilogue loads its masks itself.
+  constexpr int FD = MODE == kModeForced ? 1 : 0;
+  __shared__ uint32_t fring[4][FD ? RING : 1][64];
+  const int64_t fbytes = MODE == kModeForced ? ((int64_t)a.E * N * a.mask_bytes + 3) / 4 * 4 : 0;
+  const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<void*>(MODE == kModeForced ? a.forced : (const void*)a.act_out), 0,
+      fbytes > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)fbytes, 0x00020000);
   // row bytes: F floats, or the record's 32 KC bytes
   const int RB = U8 ? 32 * KC : 4 * F;
   const uint8_t* wbase = (U8 ? a.rec : reinterpret_cast<const uint8_t*>(a.obs)) + ((size_t)wave_env0 * N + k) * RB;
@@ -335,6 +323,13 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rsrc, (__attribute__((address_space(3))) void*)&ring[wave][t % RING][c][j][0], 4,
             vo + (U8 ? 32 * c + 4 * j : 4 * (32 * c + j)), 0, 0, 0);
+    if constexpr (FD) {
+      const int env = wave_env0 + t * 16 + i;
+      const uint32_t fo = (t < tiles && g == 0 && A <= 8 && env < a.E) ? (uint32_t)(((size_t)env * N + k) & ~(size_t)3)
+                                                                       : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(frsrc, (__attribute__((address_space(3))) void*)&fring[wave][t % RING][0],
+                                               4, fo, 0, 0, 0);
+    }
   };
   // layers 1-2 of one tile -> (pre-scaled) logits lg and critic value
   auto tile = [&](int tt, f32x4& lg, float& value) {
@@ -452,9 +447,17 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
   for (int tt = 0; tt < tiles; tt += 2) {
     issue(tt + RING - 2);
     issue(tt + RING - 1);
-    wait_vmem<(RING - 2) * KC * DPC>();  // tiles tt, tt + 1 have landed
+    wait_vmem<(RING - 2) * (KC * DPC + FD)>();  // tiles tt, tt + 1 have landed
     __builtin_amdgcn_sched_barrier(0);        // no LDS read of the slots moves above the wait
     const int env0 = wave_env0 + tt * 16 + i, env1 = env0 + 16;
+    // forced byte of this lane's paired-epilogue cell (env0 for groups 0-1, env1 for 2-3), read before the
+    // slots are released
+    uint32_t fpre = 0;
+    if constexpr (FD) {
+      const int envc = g < 2 ? env0 : env1;
+      const uint32_t w = fring[wave][(g < 2 ? tt : tt + 1) % RING][i];
+      fpre = (w >> (8 * (uint32_t)(((size_t)(envc < a.E ? envc : 0) * N + k) & 3))) & 0xFFu;
+    }
     // the paired epilogue's Philox block, drawn here: inside the scheduling region of the tiles' MFMAs (the
     // barrier below would otherwise keep it behind them as a serial chain of ten dependent rounds)
     u32x4 rpre = {};
@@ -483,8 +486,6 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
 #pragma unroll
       for (int r = 0; r < 4; ++r) lgc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(lg0[r]), fu(lg1[r]), false, false)[0]);
       const int envc = g < 2 ? env0 : env1;
-      const int pair = tt >> 1;  // wave-uniform
-      const uint32_t fpre = ((pair < 4 ? fpk[0] : fpk[1]) >> (8 * (pair & 3))) & 0xFFu;
       policy_epilogue<KIND, CRITIC, true, MODE, MODE == kModeForced, false, MODE == kModeSample && D2D_POLICY_RNG_EARLY>(
           a, lgc, g < 2 ? v0 : v1, envc, envc < a.E, k, g, rng, fpre, rpre);
     } else {
@@ -538,14 +539,14 @@ static int resident_blocks() {
 static int g_policy_sizing = -1;  // (A/B) D2D_POLICY_SIZING=r: r resident rounds (0: the 256-envs-per-wave rule only)
 
 // envs per wave for one resident round of K (every wave's per-agent weight split amortised over all of its
-// tiles, no partial last round); the forced mode keeps <= 256 (its forced bytes are preloaded per wave)
+// tiles, no partial last round)
 template <auto K>
 static MlpArgs one_round(MlpArgs x) {
   if (g_policy_sizing < 0) {
     const char* e = getenv("D2D_POLICY_SIZING");
     g_policy_sizing = e ? atoi(e) : 1;
   }
-  if (x.forced || g_policy_sizing <= 0) return x;
+  if (g_policy_sizing <= 0) return x;
   const int64_t per_agent = std::max<int64_t>(1, (int64_t)resident_blocks<K>() * g_policy_sizing / x.N);
   int64_t epw = ((int64_t)x.E + 4 * per_agent - 1) / (4 * per_agent);
   epw = (epw + 31) / 32 * 32;

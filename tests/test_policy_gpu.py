@@ -154,9 +154,10 @@ def test_sampling_uses_philox_stream3(kind, F, H, A, in_dims):
 
 @pytest.mark.parametrize("kind,F,H,A,in_dims", [CASES[0], CASES[4], CASES[3]])
 def test_forced_full_waves_equal_sampled_logp(kind, F, H, A, in_dims):
-    """Batches large enough for 256 envs per wave (8 epilogue pairs, the forced bytes preloaded
-    per wave) with a ragged tail: the forced evaluation of sampled actions reproduces their
-    log-probs bit for bit (the D2D first-epoch identity), and matches torch (1e-5, well-conditioned)."""
+    """Batches large enough for many tiles per wave (one resident round: the forced bytes travel through the
+    obs DMA ring, several hundred tile pairs per wave) with a ragged tail: the forced evaluation of sampled actions
+    reproduces their log-probs bit for bit (the D2D first-epoch identity), and matches torch (1e-5,
+    well-conditioned)."""
     from torch.distributions import Bernoulli, Categorical
     from d2dhip.policy import policy_mlp_step
     from d2dhip.envbatch import pack_masks_torch
