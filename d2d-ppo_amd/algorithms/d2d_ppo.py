@@ -355,9 +355,9 @@ class D2DPPO(BatchedLearnerBase):
 
     def _critic_split_backward(self, ro, crit):
         """Gradients of mse(V, returns) into the critic's .grad (what value_loss.backward() leaves,
-        d2d_ppo.py:208-216): dW1 = dPreᵀ X on a two-way RNE bf16 split of dPre (≤ 2^-17 relative per
-        product term, as in the fused update kernels) against the exact bf16 states; dPre's split and the
-        db1 / dW2 sums come from one HIP pass (d2d_critic_dpre_split), dW1 from a split-K batched GEMM."""
+        d2d_ppo.py:208-216): dW1 = dPreᵀ X on a three-way RNE bf16 split of dPre (~2^-24 relative per
+        product term, torch fp32's level) against the exact bf16 states; dPre's split and the db1 / dW2 sums
+        come from one HIP pass (d2d_critic_dpre_split3), dW1 from a split-K batched GEMM."""
         v, pre, _ = crit
         l1, l2 = self.value_network.linear1, self.value_network.linear2
         H = l1.weight.shape[0]
@@ -366,8 +366,8 @@ class D2DPPO(BatchedLearnerBase):
             value_loss = (d * d).mean()
             dv = d * (2.0 / d.numel())                                                  # [B]
             g_b2 = dv.sum().reshape(1)
-            # dpre = [pre > 0] w2^T dv as its two-way RNE bf16 split [2H][B], db1 = sum_b dpre and
-            # dW2 = sum_b relu(pre) dv, in one HIP pass over pre (d2d_critic_dpre_split)
+            # dpre = [pre > 0] w2^T dv as its RNE bf16 split parts [pH][B], db1 = sum_b dpre and
+            # dW2 = sum_b relu(pre) dv, in one HIP pass over pre
             from d2dhip import _lib
             lib = _lib.require_gpu()
             B = pre.shape[1]
@@ -390,7 +390,7 @@ class D2DPPO(BatchedLearnerBase):
 
     @staticmethod
     def _dw1_gemm(dhm, xb):
-        """[2H][B] x [B][S] -> fp32 [2H][S] with K = B (the whole sample batch): as one GEMM its output is
+        """[pH][B] x [B][S] -> fp32 [pH][S] (p split parts) with K = B (the whole sample batch): as one GEMM its output is
         a single row of tiles, so for large B the K range is split into nc chunks of a batched GEMM
         (hipBLASLt strided batches, [nc][2H][S] partials) summed afterwards."""
         B = dhm.shape[1]
