@@ -120,6 +120,7 @@ enum { kGruBernoulli = 0, kGruCategorical = 1, kGruValue = 2 };
 constexpr int kGruPadTab = 63;  // padding-table steps of the policy kernel (history_len <= 64)
 constexpr int kFlushSteps = 64;  // BPTT steps per weight-gradient MFMA accumulation chain (coop_flush)
 
+
 // ------------------------------------------------------------------------------ policy kernel
 // Workgroup = agent k x a strided set of tiles; 8 waves (2 per SIMD), one 16-env tile per wave at a
 // time.  LDS: the agent's input and recurrent images (fp32, swizzled; 72 KB at H = 64, F < 32).
@@ -411,10 +412,12 @@ __device__ __forceinline__ bf16x8 whh_dh_frag(const bf16x8* whh_b, int T, int t,
 // SPLIT (default): the forward and the BPTT recompute on the policy kernel's split step
 // (gru_preact_split: the 74 KB split W_hh image in LDS, the split W_ih image from L2); the scratch is
 // then 2 HW rows per wave (the step's gradient rows leave it in three passes), 155 KB in all.
-template <int HT, int IT, int KIND, bool SPLIT, bool COOP = false>
+// LONGW (COOP): windows longer than kFlushSteps steps, the cooperative accumulators flushed every kFlushSteps
+template <int HT, int IT, int KIND, bool SPLIT, bool COOP = false, bool LONGW = false>
 __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   constexpr int HW = 16 * HT, R3 = 3 * HW, RT = R3 + 4, SROWS = 2 * HW;
   static_assert(!COOP || (HT == 4 && SPLIT && D2D_GRU_DH_BF16), "COOP: H in (32, 64], the split step, bf16 dh");
+  static_assert(COOP || !LONGW, "LONGW: the cooperative path");
   using SP = GruSplit<HT, IT>;
   using CR = CoopRegion<IT>;
   __shared__ __attribute__((aligned(16))) unsigned char whh_raw[SPLIT ? 16 * SP::WHH : 4 * R3 * HW];
@@ -924,7 +927,12 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
             for (int U = 0; U < IT; ++U) cwi[g3][U] = mfma_bf16(ai, cat2(tx[U], tx[U]), cwi[g3][U]);
           }
         }
-        if (((L - 1 - j) % kFlushSteps) == kFlushSteps - 1 && j > 0) coop_flush();  // wave-uniform
+        // windows longer than kFlushSteps (LONGW instantiations only: the conditional flush inside the step
+        // loop cost the xp_load update, L = 64, ~8 % -- 1,097 vs 1,187 ms per 5-epoch GRU D2D-PPO iteration,
+        // profiles/r04/gru_flush_ab.log -- as a nest of 64-step chunks it broke the row-history instantiation's
+        // code generation, so the loop stays one loop)
+        if constexpr (LONGW)
+          if (((L - 1 - j) % kFlushSteps) == kFlushSteps - 1 && j > 0) coop_flush();  // wave-uniform
       }
 #endif
     }
@@ -1500,6 +1508,14 @@ extern "C" int64_t d2d_gru_grad_workspace(const d2d_gru_desc* d, int32_t T) {
 template <int HT, int IT>
 static void launch_grad_kind(const GruArgs& a, dim3 grid, hipStream_t s, bool coop) {
   if constexpr (HT == 4 && IT <= 3 && kGradSplit && D2D_GRU_DH_BF16) {
+    if (coop && a.L > kFlushSteps) {
+      if (a.kind == kGruBernoulli)
+        hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruBernoulli, true, true, true>), grid, dim3(256), 0, s, a);
+      else if (a.kind == kGruCategorical)
+        hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruCategorical, true, true, true>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruValue, true, true, true>), grid, dim3(256), 0, s, a);
+      return;
+    }
     if (coop) {
       if (a.kind == kGruBernoulli)
         hipLaunchKernelGGL((gru_grad_kernel<HT, IT, kGruBernoulli, true, true>), grid, dim3(256), 0, s, a);

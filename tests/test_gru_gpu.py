@@ -352,13 +352,16 @@ def test_gru_policy_at_xp_load_window(mode, policy_impl):
 # (gru_kernels.hip kGruPadTab), so the padding steps run inside every window, and L = 256 > the 200-slot
 # episode makes every rollout window start at the episode start.
 LONG = [dict(N=128, F=23, H=64, A=8, L=128, ep=200, T=200, E=4),
-        dict(N=256, F=23, H=64, A=8, L=256, ep=200, T=200, E=4)]
+        dict(N=256, F=23, H=64, A=8, L=256, ep=200, T=200, E=2)]  # (E = 2: the float64 reference takes minutes)
 
 
 @pytest.mark.parametrize("c", LONG, ids=lambda c: f"N{c['N']}-L{c['L']}")
 @pytest.mark.parametrize("mode", ["sampled", "deterministic", "forced_padded"])
 def test_gru_policy_long_window(mode, c, policy_impl):
-    """As test_gru_policy_at_xp_load_window, at history_len = n_agents = 128 / 256 (xp_n_agents)."""
+    """As test_gru_policy_at_xp_load_window, at history_len = n_agents = 128 / 256 (xp_n_agents); the fp32-MFMA
+    A/B kernel at 128 only (the float64 reference of the 256-step windows is the suite's slowest part)."""
+    if policy_impl == "f32" and c["L"] > 128:
+        pytest.skip("fp32-MFMA A/B kernel: covered at L = 128")
     xp_policy_check(mode, c)
 
 
@@ -465,7 +468,10 @@ def test_gru_grads_large_batch_record(kind):
 @pytest.mark.parametrize("kind", ["sigmoid", None])
 def test_gru_grads_long_window(kind, c, grad_input):
     """gru_grad_kernel at history_len = n_agents = 128 / 256 (xp_n_agents.py:98-112): all eight gradient
-    tensors vs float64 autograd over the padded training windows, the band rule of the xp_load test."""
+    tensors vs float64 autograd over the padded training windows, the band rule of the xp_load test.  At 256
+    the product input only (the compact record, cooperative path): the float64 reference there is minutes."""
+    if c["L"] > 128 and grad_input != "record":
+        pytest.skip("L = 256: the record (product) path; the fp32-row and row-history kernels are covered at 128")
     xp_grads_check(kind, grad_input, c["E"], cfg=c)
 
 

@@ -2,7 +2,7 @@
 # usage (GPU box): bash tools/gpu/run_r04z_final.sh
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 9
 O="$R/gpurun_out/r04z_final"; mkdir -p "$O"
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -v --timeout 200 --timeout-method thread -p no:cacheprovider \
+timeout -k 10 1000 python3 -u -m pytest tests -m gpu -v --durations=40 --timeout 300 --timeout-method thread -p no:cacheprovider \
   > "$O/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed" "$O/pytest_gpu.log" | tail -2
 [ $rc -eq 0 ] || exit $rc
