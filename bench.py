@@ -784,7 +784,8 @@ def gru_leg(args, rank, world, local):
                            "mfma_pipe_busy_frac_static": pol_pipe, "mfma_pmc": pmc_mfma("d2d::gru_policy_kernel"),
                            "bound": "mfma"},
            "update": {"envs_per_gpu": E2, "slots": ro.T, "agent_samples": samples,
-                      "kernel": f"d2d::gru_grad_kernel<4, {it_}, 0, true, {'true' if it_ <= 3 else 'false'}>",
+                      "kernel": (f"d2d::gru_grad_kernel<4, {it_}, 0, true, true, {'true' if L > 64 else 'false'}>" if it_ <= 3
+                                 else f"d2d::gru_grad_kernel<4, {it_}, 0, true, false, false>"),
                       "weight_gradients": "cooperative LDS exchange" if it_ <= 3 else "per-wave global row history",
                       "ms": grad_ms,
                       "agent_samples_per_s": samples * world / (grad_ms / 1e3), "flop": grad_flop,
