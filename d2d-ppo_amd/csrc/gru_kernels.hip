@@ -1329,42 +1329,42 @@ using namespace d2d;
 extern int g_policy_f32_mfma;  // policy_kernels.hip (D2D_OPT_POLICY_F32_MFMA)
 
 template <int HT, int IT, int KIND, bool SPLIT>
-static void launch_policy_split(const GruArgs& a, dim3 grid, hipStream_t s) {
+static void launch_policy_split(const GruArgs& a, dim3 grid, int threads, hipStream_t s) {
   if (KIND == kGruValue || a.ep.forced == nullptr) {
     if (KIND != kGruValue && a.ep.deterministic)
-      hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeDeterministic, SPLIT>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeDeterministic, SPLIT>), grid, dim3(threads), 0, s, a);
     else
-      hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeSample, SPLIT>), grid, dim3(512), 0, s, a);
+      hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeSample, SPLIT>), grid, dim3(threads), 0, s, a);
   } else {
-    hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeForced, SPLIT>), grid, dim3(512), 0, s, a);
+    hipLaunchKernelGGL((gru_policy_kernel<HT, IT, KIND, kModeForced, SPLIT>), grid, dim3(threads), 0, s, a);
   }
 }
 
 // the split kernel where its images fit LDS (IT <= 2: F < 32); the fp32-MFMA kernel otherwise or
 // when D2D_OPT_POLICY_F32_MFMA asks for it (A/B timing and tests)
 template <int HT, int IT, int KIND>
-static void launch_policy_mode(const GruArgs& a, dim3 grid, hipStream_t s) {
+static void launch_policy_mode(const GruArgs& a, dim3 grid, int threads, hipStream_t s) {
   if constexpr (IT <= 2) {
     if (!g_policy_f32_mfma) {
-      launch_policy_split<HT, IT, KIND, true>(a, grid, s);
+      launch_policy_split<HT, IT, KIND, true>(a, grid, threads, s);
       return;
     }
   }
-  launch_policy_split<HT, IT, KIND, false>(a, grid, s);
+  launch_policy_split<HT, IT, KIND, false>(a, grid, threads, s);
 }
 
 template <int HT, int IT>
-static void launch_policy_kind(const GruArgs& a, dim3 grid, hipStream_t s) {
-  if (a.kind == kGruBernoulli) launch_policy_mode<HT, IT, kGruBernoulli>(a, grid, s);
-  else if (a.kind == kGruCategorical) launch_policy_mode<HT, IT, kGruCategorical>(a, grid, s);
-  else launch_policy_mode<HT, IT, kGruValue>(a, grid, s);
+static void launch_policy_kind(const GruArgs& a, dim3 grid, int threads, hipStream_t s) {
+  if (a.kind == kGruBernoulli) launch_policy_mode<HT, IT, kGruBernoulli>(a, grid, threads, s);
+  else if (a.kind == kGruCategorical) launch_policy_mode<HT, IT, kGruCategorical>(a, grid, threads, s);
+  else launch_policy_mode<HT, IT, kGruValue>(a, grid, threads, s);
 }
 
 template <int HT>
-static void launch_policy_it(const GruArgs& a, dim3 grid, hipStream_t s) {
-  if (a.F + 1 <= 16) launch_policy_kind<HT, 1>(a, grid, s);
-  else if (a.F + 1 <= 32) launch_policy_kind<HT, 2>(a, grid, s);
-  else launch_policy_kind<HT, 4>(a, grid, s);  // (the swizzled fp32 images need 16 / 32 / 64 columns)
+static void launch_policy_it(const GruArgs& a, dim3 grid, int threads, hipStream_t s) {
+  if (a.F + 1 <= 16) launch_policy_kind<HT, 1>(a, grid, threads, s);
+  else if (a.F + 1 <= 32) launch_policy_kind<HT, 2>(a, grid, threads, s);
+  else launch_policy_kind<HT, 4>(a, grid, threads, s);  // (the swizzled fp32 images need 16 / 32 / 64 columns)
 }
 
 static int check_gru_desc(const d2d_gru_desc* d, const void* obs) {
@@ -1429,13 +1429,21 @@ extern "C" int d2d_policy_gru(const d2d_gru_desc* d, int32_t T, const void* obs,
   if (a.N == 0 || a.E == 0 || n_slots == 0) return D2D_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int64_t tiles = (int64_t)n_slots * a.env_tiles;
-  // about 2 workgroups of 8 waves per CU over the whole grid, at least one tile per wave
-  const int gy = (int)std::max<int64_t>(1, std::min<int64_t>((512 + a.N - 1) / a.N, (tiles + 7) / 8));
+  // about 2 workgroups of 8 waves per CU over the whole grid, at least one tile per wave.  A batch too small
+  // to give every CU a workgroup (the xp_load rollout: 64 agents x 16 tiles) takes 4-wave workgroups instead
+  // (the LDS images allow one workgroup per CU either way): one wave per SIMD on twice as many CUs, so each
+  // window step's MFMAs no longer share a SIMD's pipe with a second wave's
+  int threads = 512;
+  int gy = (int)std::max<int64_t>(1, std::min<int64_t>((512 + a.N - 1) / a.N, (tiles + 7) / 8));
+  if ((int64_t)a.N * gy < 256 && tiles > 4) {
+    threads = 256;
+    gy = (int)std::max<int64_t>(1, std::min<int64_t>((256 + a.N - 1) / a.N, (tiles + 3) / 4));
+  }
   dim3 grid(a.N, gy);
   const int ht = (a.H + 15) / 16;
-  if (ht <= 1) launch_policy_it<1>(a, grid, s);
-  else if (ht <= 2) launch_policy_it<2>(a, grid, s);
-  else launch_policy_it<4>(a, grid, s);
+  if (ht <= 1) launch_policy_it<1>(a, grid, threads, s);
+  else if (ht <= 2) launch_policy_it<2>(a, grid, threads, s);
+  else launch_policy_it<4>(a, grid, threads, s);
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
 }
