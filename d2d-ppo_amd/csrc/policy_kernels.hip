@@ -550,7 +550,10 @@ static MlpArgs one_round(MlpArgs x) {
   const int64_t per_agent = std::max<int64_t>(1, (int64_t)resident_blocks<K>() * g_policy_sizing / x.N);
   int64_t epw = ((int64_t)x.E + 4 * per_agent - 1) / (4 * per_agent);
   epw = (epw + 31) / 32 * 32;
-  x.envs_per_wave = (int)std::max<int64_t>(x.envs_per_wave, epw);
+  // a wave's row offsets are 32-bit buffer offsets from its first row: epw * N row bytes stay below 2 GiB
+  const int64_t rb = x.rec ? 32 * ((x.F + 1 + 31) / 32) : 4 * (int64_t)x.F;
+  const int64_t cap = std::max<int64_t>(32, ((int64_t)0x7FF00000 / ((int64_t)x.N * rb)) / 32 * 32);
+  x.envs_per_wave = (int)std::max<int64_t>(x.envs_per_wave, std::min(epw, cap));
   return x;
 }
 template <auto K>
@@ -629,6 +632,12 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const void* obs, const
   if (rc) return rc;
   a.forced = forced; a.act_out = actions; a.logp_out = logp; a.value_out = value;
   a.mask_bytes = d->n_out <= 8 ? 1 : d->n_out <= 16 ? 2 : 4;
+  if (forced && (int64_t)d->n_envs * d->n_agents * a.mask_bytes > 0x7FFFFFFF) {
+    // the forced words travel through a buffer descriptor with 32-bit offsets (the DMA ring)
+    d2d_set_error("d2d_policy_mlp_step: forced buffer of %lld bytes exceeds 2 GiB",
+                  (long long)d->n_envs * d->n_agents * a.mask_bytes);
+    return D2D_EUNSUPPORTED;
+  }
   if (a.E == 0 || a.N == 0) return D2D_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int ht = (a.H + 15) / 16;
