@@ -526,28 +526,31 @@ static int launch_policy_f32(const MlpArgs& a, hipStream_t s) {
 // Workgroups of kernel K resident on the device at once (its occupancy x the CU count), queried once
 template <auto K>
 static int resident_blocks() {
-  static int n = 0;
-  if (!n) {
+  static const int n = [] {  // (a function-local static: initialised once, thread-safe)
     int per = 0, dev = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, K, 256, 0) != hipSuccess) per = 2;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
-    n = std::max(1, per * cus);
-  }
+    return std::max(1, per * cus);
+  }();
   return n;
 }
-static int g_policy_sizing = -1;  // (A/B) D2D_POLICY_SIZING=r: r resident rounds (0: the 256-envs-per-wave rule only)
+// (A/B) D2D_POLICY_SIZING=r: r resident rounds (0: the 256-envs-per-wave rule only); read once per process
+static int policy_sizing() {
+  static const int r = [] {
+    const char* e = getenv("D2D_POLICY_SIZING");
+    return e ? atoi(e) : 1;
+  }();
+  return r;
+}
 
 // envs per wave for one resident round of K (every wave's per-agent weight split amortised over all of its
 // tiles, no partial last round)
 template <auto K>
 static MlpArgs one_round(MlpArgs x) {
-  if (g_policy_sizing < 0) {
-    const char* e = getenv("D2D_POLICY_SIZING");
-    g_policy_sizing = e ? atoi(e) : 1;
-  }
-  if (g_policy_sizing <= 0) return x;
-  const int64_t per_agent = std::max<int64_t>(1, (int64_t)resident_blocks<K>() * g_policy_sizing / x.N);
+  const int rounds = policy_sizing();
+  if (rounds <= 0) return x;
+  const int64_t per_agent = std::max<int64_t>(1, (int64_t)resident_blocks<K>() * rounds / x.N);
   int64_t epw = ((int64_t)x.E + 4 * per_agent - 1) / (4 * per_agent);
   epw = (epw + 31) / 32 * 32;
   // a wave's row offsets are 32-bit buffer offsets from its first row: epw * N row bytes stay below 2 GiB
