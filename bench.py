@@ -30,7 +30,11 @@ More legs are reported in the same JSON line (they do not change `value`):
             (agent sweep 8..256 x 8 channels, 4,096 envs/GPU, D2D-PPO): env-step rates and
             one D2D-PPO training iteration each;
   d2denv  : the single-channel D2DEnv (envs/env.py): 64 agents with ring
-            neighbourhoods, env-step rate, its kernel's HBM fraction, one iPPO iteration.
+            neighbourhoods, env-step rate, its kernel's HBM fraction, one iPPO iteration;
+  gru     : xp_load.py's learner (D2D-PPO, GRU, history_len 64): policy slot, BPTT update, iteration;
+  gru_c5  : configs[4] as xp_n_agents.py writes its learner (GRU, history_len = n_agents = 64/128/256).
+The line ends with the metric's second half (ppo_updates_per_s, train_s_per_iteration,
+train_env_steps_per_s_end_to_end) so that a truncated record still shows it.
 """
 import argparse
 import json
@@ -802,6 +806,66 @@ def gru_leg(args, rank, world, local):
     return out
 
 
+def gru_c5_leg(args, rank, world, local):
+    """configs[4] as xp_n_agents.py writes its learner (xp_n_agents.py:98-112): D2D-PPO with GRU policies,
+    hidden 64, gamma 0.4, history_len = n_agents, on the c5 env (N agents x 8 channels, deadlines 7, switch 0.8,
+    lambda 1/14 aperiodic) at --gru-c5-envs envs per GPU.  Per N: one 200-slot training rollout (GRU window
+    kernel per slot + env kernel), one D2D-PPO epoch (central critic, GAE, the forced log-prob pass over the
+    padded training windows, the chain, the GRU BPTT update of all N actors, Adam) and one whole iteration
+    with n_epoch = 1; iteration_s = rollout + GAE + 5 epochs is the n_epoch = 5 iteration (xp_n_agents.py:110)
+    assembled from the measured parts (an epoch's cost does not depend on the epoch index after the first)."""
+    from algorithms.d2d_ppo import D2DPPO
+    from envs.combinatorial_env import CombinatorialEnv
+    dev = f"cuda:{local}"
+    E = args.gru_c5_envs
+    sweep = []
+    for N in [int(x) for x in args.gru_c5_agents.split(",") if x]:
+        p5 = dict(n_agents=N, n_channels=8, deadlines=np.full(N, 7), lbdas=np.full(N, 1 / 14), period=None,
+                  arrival_probs=None, offsets=None, episode_length=args.episode_length, traffic_model="aperiodic",
+                  periodic_devices=[], channel_switch=np.ones((N, 8)) * 0.8)
+        env = CombinatorialEnv(**p5, n_envs=E, device=dev, seed=60 + N)
+        env.shard(rank, world)
+        torch.manual_seed(7)
+        np.random.seed(7)
+        lr = D2DPPO(env, hidden_size=64, gamma=0.4, policy_lr=3e-4, value_lr=1e-3, beta_entropy=0.01, device=dev,
+                    useRNN=True, combinatorial=True, history_len=N, early_stopping=False)
+        gru_ok = bool(lr._gru_ok())
+        # warm-up: one rollout and one epoch (kernel loads, hipBLASLt heuristics, allocator growth)
+        ro = lr._rollout(E)
+        lr._update_epoch(ro, lr._update_state(ro))
+        torch.cuda.synchronize()
+        barrier(world)
+        t0 = time.perf_counter()
+        ro = lr._rollout(E)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        upd = lr._update_state(ro)
+        lr._update_epoch(ro, upd)     # epoch 1 (its forced log-prob pass included: no first-epoch shortcut on GRU)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        lr._update_epoch(ro, upd)     # epoch 2
+        torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        barrier(world)
+        roll = max_over_ranks(t1 - t0, world)
+        ep1 = max_over_ranks(t2 - t1, world)
+        ep = max_over_ranks(t3 - t2, world)
+        samples = ro.T * E * world * N
+        sweep.append({"agents": N, "history_len": N, "envs_per_gpu": E, "gru_kernels": gru_ok,
+                      "rollout_s": roll, "rollout_env_steps_per_s": E * world * ro.T / roll,
+                      "epoch_s": ep, "first_epoch_s": ep1, "agent_samples_per_epoch": samples,
+                      "update_agent_samples_per_s": samples / ep,
+                      "iteration_s": roll + ep1 + 4 * ep,
+                      "iteration_env_steps_per_s_end_to_end": E * world * ro.T / (roll + ep1 + 4 * ep)})
+        del lr, env, ro, upd
+        torch.cuda.empty_cache()
+    return {"config": "xp_n_agents.py learner: D2D-PPO, GRU H=64, history_len = n_agents, gamma 0.4, "
+                      "beta_entropy 0.01 (xp_n_agents.py:98-112), n_epoch = 5",
+            "what": "per N: measured rollout (200 slots), first and second epoch; iteration_s = rollout + first epoch "
+                    "+ 4 x second epoch (the n_epoch = 5 iteration from its measured parts)",
+            "sweep": sweep}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -811,7 +875,9 @@ def main():
     ap.add_argument("--episode-length", type=int, default=200)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
-    ap.add_argument("--legs", default="env,rollout,ppo,train,configs,d2denv,gru")
+    ap.add_argument("--legs", default="env,rollout,ppo,train,configs,d2denv,gru,gru_c5")
+    ap.add_argument("--gru-c5-envs", type=int, default=4096, help="envs per GPU of the c5 GRU leg")
+    ap.add_argument("--gru-c5-agents", default="64,128,256", help="agent counts of the c5 GRU leg")
     ap.add_argument("--gru-envs", type=int, default=256, help="envs per GPU in the GRU update / iteration")
     ap.add_argument("--rollout-steps", type=int, default=60)
     ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
@@ -934,6 +1000,7 @@ def main():
     configs = configs_leg(args, rank, world, local) if "configs" in legs else None
     d2denv = d2denv_leg(args, rank, world, local) if "d2denv" in legs else None
     gru_res = gru_leg(args, rank, world, local) if "gru" in legs else None
+    gru_c5 = gru_c5_leg(args, rank, world, local) if "gru_c5" in legs else None
 
     if rank == 0:
         res = {
@@ -979,8 +1046,23 @@ def main():
             res["d2denv"] = d2denv
         if gru_res is not None:
             res["gru"] = gru_res
+        if gru_c5 is not None:
+            res["gru_c5"] = gru_c5
         if cpu is not None:
             res["cpu_baseline"] = cpu
+        # the metric's second half at the END of the line (the driver's record keeps the line's tail): PPO
+        # updates/s at the --ppo-envs batch and at the headline batch, the whole training iteration
+        if ppo is not None:
+            res["ppo_updates_per_s"] = ppo["updates_per_s"]
+            res["ppo_updates_per_s_batch"] = ppo["batch"]
+        if train is not None:
+            res["ppo_updates_per_s_headline_batch"] = train["ppo_updates_per_s"]
+            res["train_s_per_iteration"] = train["s_per_iteration"]
+            res["train_env_steps_per_s_end_to_end"] = train["env_steps_per_s_end_to_end"]
+            res["train_phase_ms"] = train["phase_ms"]
+        if gru_c5 is not None:
+            res["c5_gru_summary"] = [{k: r[k] for k in ("agents", "rollout_s", "epoch_s", "iteration_s")}
+                                     for r in gru_c5["sweep"]]
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

@@ -286,11 +286,13 @@ class D2DPPO(BatchedLearnerBase):
     CRITIC_F32_FWD_MAX_DIM = 768  # below this state width the forward's first layer is one fp32 GEMM
 
     def _critic_split_forward(self, ro):
-        """Value(state) = linear2(relu(linear1(state))) (d2d_ppo.py:95-98) for all T*E states with the
-        first layer as ONE bf16 GEMM with fp32 output: the states are small integers (buffer counts,
-        channel bits, ACKs) and so exact in bf16, and W1 is split three ways (h + m + l, exact), so
-        the product is fp32-accurate at the bf16 matrix rate.  Returns (values [B], pre-activation [H][B],
-        hidden [H][B]) or None when the fp32 torch path applies (small states or non-integer states)."""
+        """Value(state) = linear2(relu(linear1(state))) (d2d_ppo.py:95-98) for all T*E states.  At
+        S >= CRITIC_F32_FWD_MAX_DIM the first layer is ONE bf16 GEMM with fp32 output: the states are small
+        integers (buffer counts, channel bits, ACKs) and so exact in bf16, and W1 is split three ways (h + m + l,
+        exact), so the product is fp32-accurate at the bf16 matrix rate; below it the first layer is one fp32
+        addmm on the fp32 states (the backward uses the bf16 operand either way).  Returns (values [B],
+        pre-activation [H][B], hidden [H][B]) or None when the torch path applies (split off, S below
+        CRITIC_SPLIT_MIN_DIM, or states that are not bf16-exact)."""
         S = ro.state_dim if "state_dim" in ro.__dict__ else ro.state_seq.shape[1]
         if not self.critic_split or S < self.CRITIC_SPLIT_MIN_DIM:
             return None
@@ -392,7 +394,7 @@ class D2DPPO(BatchedLearnerBase):
     def _dw1_gemm(dhm, xb):
         """[pH][B] x [B][S] -> fp32 [pH][S] (p split parts) with K = B (the whole sample batch): as one GEMM its output is
         a single row of tiles, so for large B the K range is split into nc chunks of a batched GEMM
-        (hipBLASLt strided batches, [nc][2H][S] partials) summed afterwards."""
+        (hipBLASLt strided batches, [nc][pH][S] partials: p = 3 for the three-way dPre split) summed afterwards."""
         B = dhm.shape[1]
         nc = next((c for c in (64, 50, 40, 32, 25, 20, 16, 10, 8, 5, 4, 2) if B % c == 0 and B // c >= 4096), 1)
         if nc == 1:

@@ -956,13 +956,17 @@ namespace {
 
 // streaming (non-temporal) stores for the obs/state flush: d2d_set_option(D2D_OPT_NT_STORES, v),
 // initial value from the environment variable D2D_NT_STORES
-int g_nt_stores = -1;
+// (a relaxed atomic: d2d_set_option may run on another host thread; -1 = not yet read from the environment)
+std::atomic<int> g_nt_stores{-1};
 uint32_t store_flags() {
-  if (g_nt_stores < 0) {
+  int v = g_nt_stores.load(std::memory_order_relaxed);
+  if (v < 0) {
     const char* e = getenv("D2D_NT_STORES");
-    g_nt_stores = (e && e[0] == '1') ? 1 : 0;
+    int expect = -1;
+    g_nt_stores.compare_exchange_strong(expect, (e && e[0] == '1') ? 1 : 0, std::memory_order_relaxed);
+    v = g_nt_stores.load(std::memory_order_relaxed);
   }
-  return (uint32_t)g_nt_stores;
+  return (uint32_t)v;
 }
 
 int buffer_words(int D) { return D <= 4 ? 1 : D <= 8 ? 2 : D <= 12 ? 3 : D <= 16 ? 4 : 8; }
@@ -1152,9 +1156,10 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
 
 }  // namespace
 
-extern int g_policy_f32_mfma;  // policy_kernels.hip
-extern int g_policy_critic_split;  // policy_kernels.hip
+extern std::atomic<int> g_policy_f32_mfma;  // policy_kernels.hip
+extern std::atomic<int> g_policy_critic_split;  // policy_kernels.hip
 extern std::atomic<int> g_gru_grad_history;  // gru_kernels.hip
+extern std::atomic<int> g_critic_grad_rows;  // update_kernels.hip
 
 extern "C" int d2d_set_option(int32_t option, int32_t value) {
   if (option == D2D_OPT_GRU_GRAD_HISTORY) {
@@ -1162,15 +1167,19 @@ extern "C" int d2d_set_option(int32_t option, int32_t value) {
     return D2D_OK;
   }
   if (option == D2D_OPT_NT_STORES) {
-    g_nt_stores = value ? 1 : 0;
+    g_nt_stores.store(value ? 1 : 0, std::memory_order_relaxed);
+    return D2D_OK;
+  }
+  if (option == D2D_OPT_CRITIC_GRAD_ROWS) {
+    g_critic_grad_rows.store(value ? 1 : 0, std::memory_order_relaxed);
     return D2D_OK;
   }
   if (option == D2D_OPT_POLICY_F32_MFMA) {
-    g_policy_f32_mfma = value ? 1 : 0;
+    g_policy_f32_mfma.store(value ? 1 : 0, std::memory_order_relaxed);
     return D2D_OK;
   }
   if (option == D2D_OPT_POLICY_CRITIC_SPLIT) {
-    g_policy_critic_split = value ? 1 : 0;
+    g_policy_critic_split.store(value ? 1 : 0, std::memory_order_relaxed);
     return D2D_OK;
   }
   d2d_set_error("unknown option %d", option);

@@ -1326,7 +1326,7 @@ __global__ void gru_reduce_kernel(const float* __restrict__ partial, int G, int 
 
 using namespace d2d;
 
-extern int g_policy_f32_mfma;  // policy_kernels.hip (D2D_OPT_POLICY_F32_MFMA)
+extern std::atomic<int> g_policy_f32_mfma;  // policy_kernels.hip (D2D_OPT_POLICY_F32_MFMA)
 
 template <int HT, int IT, int KIND, bool SPLIT>
 static void launch_policy_split(const GruArgs& a, dim3 grid, int threads, hipStream_t s) {
@@ -1345,7 +1345,7 @@ static void launch_policy_split(const GruArgs& a, dim3 grid, int threads, hipStr
 template <int HT, int IT, int KIND>
 static void launch_policy_mode(const GruArgs& a, dim3 grid, int threads, hipStream_t s) {
   if constexpr (IT <= 2) {
-    if (!g_policy_f32_mfma) {
+    if (!g_policy_f32_mfma.load(std::memory_order_relaxed)) {
       launch_policy_split<HT, IT, KIND, true>(a, grid, threads, s);
       return;
     }

@@ -19,6 +19,7 @@
 // layer is a per-lane dot product + 2 cross-group shuffles.  fp32 MFMA is an
 // exact k-ordered fmaf chain, so results match the torch fp32 reference to
 // ~1e-6 (parity tests use 1e-5).
+#include <atomic>
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -500,13 +501,14 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_spli
 
 using namespace d2d;
 
-int g_policy_f32_mfma = 0;  // d2d_set_option(D2D_OPT_POLICY_F32_MFMA, 1): fp32-MFMA kernel
+// option words set by d2d_set_option from any host thread: relaxed atomics, read once per call
+std::atomic<int> g_policy_f32_mfma{0};  // d2d_set_option(D2D_OPT_POLICY_F32_MFMA, 1): fp32-MFMA kernel
 #ifndef D2D_POLICY_CRITIC_SPLIT
 // the iPPO critic's weight fragments (48 + 16 registers at H = 64) hold the fused actor + critic kernel at two
 // waves per SIMD (224 VGPRs; the actor alone: 137); 1 = the value as a separate value-only launch
 #define D2D_POLICY_CRITIC_SPLIT 0
 #endif
-int g_policy_critic_split = D2D_POLICY_CRITIC_SPLIT;  // d2d_set_option(D2D_OPT_POLICY_CRITIC_SPLIT, v)
+std::atomic<int> g_policy_critic_split{D2D_POLICY_CRITIC_SPLIT};  // d2d_set_option(D2D_OPT_POLICY_CRITIC_SPLIT, v)
 
 template <int KS, int HT>
 static int launch_policy_f32(const MlpArgs& a, hipStream_t s) {
@@ -574,32 +576,35 @@ static void launch_split_fmt(const MlpArgs& a, hipStream_t s) {
 }
 
 template <int KC, int HT, int KIND, bool CRITIC, bool U8>
-static void launch_split_mode(const MlpArgs& a, hipStream_t s) {
-  if (CRITIC && g_policy_critic_split) {
+static void launch_split_mode(const MlpArgs& a, hipStream_t s, bool critic_split) {
+  if (CRITIC && critic_split) {
     // the actor (actions, log-probs) and the critic value as two launches of the same arithmetic, each at its
     // own occupancy (actor 137 VGPRs, value-only 119, fused 224 at H = 64)
     MlpArgs av = a;
     av.v1 = av.c1 = av.v2 = av.c2 = nullptr;
     launch_split_fmt<KC, HT, KIND, false, U8>(av, s);
-    launch_one<policy_split_kernel<KC, HT, KIND, true, kModeValue, U8>>(a, s);
+    // the value-only launch stores nothing but the value: skipped when the caller passes value = NULL
+    // (the fused kernel guards the same store with a.value_out)
+    if (a.value_out) launch_one<policy_split_kernel<KC, HT, KIND, true, kModeValue, U8>>(a, s);
     return;
   }
   launch_split_fmt<KC, HT, KIND, CRITIC, U8>(a, s);
 }
 
 template <int KC, int HT, int KIND, bool CRITIC>
-static void launch_split_kind(const MlpArgs& a, hipStream_t s) {
-  if (a.rec) launch_split_mode<KC, HT, KIND, CRITIC, true>(a, s);
-  else launch_split_mode<KC, HT, KIND, CRITIC, false>(a, s);
+static void launch_split_kind(const MlpArgs& a, hipStream_t s, bool critic_split) {
+  if (a.rec) launch_split_mode<KC, HT, KIND, CRITIC, true>(a, s, critic_split);
+  else launch_split_mode<KC, HT, KIND, CRITIC, false>(a, s, critic_split);
 }
 
 template <int KC, int HT>
 static int launch_policy_split(const MlpArgs& a, hipStream_t s) {
   const bool critic = a.v1 != nullptr;
-  if (a.kind == 0 && critic) launch_split_kind<KC, HT, 0, true>(a, s);
-  else if (a.kind == 0) launch_split_kind<KC, HT, 0, false>(a, s);
-  else if (critic) launch_split_kind<KC, HT, 1, true>(a, s);
-  else launch_split_kind<KC, HT, 1, false>(a, s);
+  const bool cs = g_policy_critic_split.load(std::memory_order_relaxed) != 0;  // one snapshot per call
+  if (a.kind == 0 && critic) launch_split_kind<KC, HT, 0, true>(a, s, cs);
+  else if (a.kind == 0) launch_split_kind<KC, HT, 0, false>(a, s, cs);
+  else if (critic) launch_split_kind<KC, HT, 1, true>(a, s, cs);
+  else launch_split_kind<KC, HT, 1, false>(a, s, cs);
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
 }
@@ -644,7 +649,7 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const void* obs, const
   if (a.E == 0 || a.N == 0) return D2D_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int ht = (a.H + 15) / 16;
-  if (g_policy_f32_mfma || a.F + 1 > 64) {
+  if (g_policy_f32_mfma.load(std::memory_order_relaxed) || a.F + 1 > 64) {
     if (a.rec) { d2d_set_error("the fp32-MFMA policy kernel reads fp32 obs only"); return D2D_EUNSUPPORTED; }
     const int ks = (a.F + 3) / 4;
     if (ks <= 8) return ht <= 2 ? launch_policy_f32<8, 2>(a, s) : ht <= 4 ? launch_policy_f32<8, 4>(a, s)

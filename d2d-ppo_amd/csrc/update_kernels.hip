@@ -35,6 +35,7 @@
 // are summed in fixed order through LDS and written as one partial per (workgroup, agent);
 // update_reduce_kernel sums the partials in fixed order.  No atomics: bitwise reproducible.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <type_traits>
 
@@ -1243,6 +1244,423 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? D2D_UPD_WAVES : 1) void
   }
 }
 
+
+// -------------------------------------------------- critic gradients, hidden on rows (round 5, default)
+// The same Value(x) = V2 relu(V1 x + c1) + c2 and loss as ppo_critic_grad_kernel above, arranged so that the
+// per-(sample, hidden) work is one relu, one fma and a u16 mask per element (the sample-on-rows kernel above:
+// 11 VALU per MFMA, VALU-issue bound, profiles/pmc_mfma.json):
+//   * HVT = V1 . X^T (lane (g, i): hidden 16 t + 4 g + r of sample i -- the actor's forward orientation); the
+//     64 -> 1 head is a per-lane fma over the lane's 4 HT hidden units and a sum over the four lane groups (two
+//     permlane swaps) instead of 16-lane row sums of every (sample, tile);
+//   * dV1[h][j] = v2[h] G[h][j],  G[h][j] = sum_s M[s][h] dv_s x_s[j],  M = relu'(hv) in {0, 1}: the A operand
+//     (row = hidden, k = samples) is M times the bf16 parts (dv_h, dv_m) of dv's two-way RNE split -- M . dv_h
+//     is dv_h or 0, exact -- built with one v_pk_min_u16 per sample pair and one v_pk_mul_lo_u16 per part; the B
+//     operand (k = samples, column = input) is x itself, bf16-exact (the record; exact fp32 tiles), read
+//     sample-on-k from the tile's bf16 LDS image with ds_read_b64_tr_b16 (no product, no split per (sample,
+//     input));
+//   * M reaches the A layout (hidden on lanes) through LDS: relu(HVT)'s bf16 high halves (nonzero exactly when
+//     relu(h) >= 2^-133, the actor's relu-mask edge) written [sample][hidden] and read back transposed;
+//   * dv2[h] = sum_s dv_s relu(h_s) = sum_j V1ext[h][j] G[h][j] (relu(h_s) = M[s][h] (V1ext x_s)[h], V1ext = [V1 | c1]
+//     against x_s's bias column): from the workgroup's G partial once, no per-sample work (D2D_CRITIC_DV2_G; 0
+//     keeps per-sample fmas and Kahan sums for A/B).
+// Precision: forward as above (exact three-way V1 split, exact x); dv on a two-way RNE split (2^-17 relative per
+// term, as the sample-on-rows kernel's (dv x) split); x exact.  Fractional inputs (fp32 rows that are not
+// bf16-exact: the chsel env's 1/n ACKs) take the deferred body: x's residual parts in the forward, and
+// (dv_h + dv_m) x_h + dv_h x_m on x's two-way RNE split in dV1.
+#ifndef D2D_CRITIC_DV2_G
+#define D2D_CRITIC_DV2_G 1
+#endif
+template <int KC, bool U8>
+struct CriticInT {
+  XRows<KC, U8> x;
+  float R[2];  // returns of samples i and 16 + i
+};
+
+template <int KC, bool U8>
+__device__ __forceinline__ void load_critic_in_t(CriticInT<KC, U8>& in, const UpdArgs& a, TileCur c, int k, int g,
+                                                 int i) {
+  load_rows<KC, U8>(in.x, a, c.t, c.e0, k, g, i);
+  const __amdgpu_buffer_rsrc_t rw = sample_rsrc(a.weight, a.w_st, a.w_ext, c.t, c.e0, k);
+#pragma unroll
+  for (int s = 0; s < 2; ++s) in.R[s] = ld_sample(rw, a.w_st, 16 * s + i);
+}
+
+// v_pk_min_u16 / v_pk_mul_lo_u16 (asm: the compiler turns the packed forms into per-half compares + selects)
+__device__ __forceinline__ uint32_t pk_min1_u16(uint32_t x) {
+  uint32_t m;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(x), "s"(0x00010001u));
+  return m;
+}
+__device__ __forceinline__ uint32_t pk_mul_lo_u16(uint32_t a, uint32_t b) {
+  uint32_t o;
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(o) : "v"(a), "v"(b));
+  return o;
+}
+
+#ifndef D2D_CRITIC_T_WAVES
+// waves per SIMD the hidden-on-rows critic is register-budgeted for (KC = 1, H <= 64, the record: 168 VGPRs, no
+// spills; fp32 rows keep D2D_UPD_WAVES: their deferred fractional-input body would spill at 168)
+#define D2D_CRITIC_T_WAVES 3
+#endif
+template <int KC, int HT, bool U8>
+__global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? (U8 ? D2D_CRITIC_T_WAVES : D2D_UPD_WAVES) : 1) void ppo_critic_grad_t_kernel(UpdArgs a) {
+  constexpr int QT = 2 * KC;
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4, i = lane & 15;
+  int k, by;
+  xcd_block(k, by);  // k = agent, by = sample-chunk group
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int H = a.H, F = a.F;
+  typedef __attribute__((address_space(3))) v4i16* lds_v4i16;
+
+  Parts v1p[HT][KC];
+  float v2r[HT][4];  // V2 of hidden 16 t + 4 g + r: the rows of this lane's HVT accumulators
+  {
+    const float* V1 = a.w1 + (size_t)k * H * F;
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      const int hrow = 16 * t + i;
+      const bool hok = hrow < H;
+#pragma unroll
+      for (int c = 0; c < KC; ++c) {
+        float wv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int col = 32 * c + 8 * g + j;
+          wv[j] = !hok ? 0.f : col < F ? V1[(size_t)hrow * F + col] : col == F ? a.b1[(size_t)k * H + hrow] : 0.f;
+        }
+        v1p[t][c] = split3(wv);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int hid = 16 * t + 4 * g + r;
+        v2r[t][r] = hid < H ? a.w2[(size_t)k * H + hid] : 0.f;
+      }
+    }
+  }
+  const float c2 = a.b2[k];
+
+  f32x4 dv1[HT][QT];
+#pragma unroll
+  for (int t = 0; t < HT; ++t)
+#pragma unroll
+    for (int q = 0; q < QT; ++q) dv1[t][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  KahanSum dc2, loss_acc;
+#if !D2D_CRITIC_DV2_G
+  KahanSum dv2k[HT][4];
+#endif
+
+  // per-wave LDS: the tile's inputs as bf16 high parts (exact on the tiles the main body runs) and, for the
+  // deferred fractional tiles of fp32 rows, as fp32; relu(HVT)'s high halves [half][t2][sample][hidden]; dv's
+  // two bf16 parts [part][half][sample].  The cross-wave reduction buffer (after the tile loop) aliases the
+  // relu image.
+  constexpr int XS = 32 * KC + 4;    // fp32 row stride = 4 mod 16 floats: sample-on-k reads hit 64 banks
+  constexpr int XS16 = 32 * KC + 4;  // bf16 rows of 8-byte multiples, 8 banks apart per 4 rows
+  __shared__ __attribute__((aligned(16))) uint16_t xs16[4][32][XS16];
+  constexpr int X32B = U8 ? 16 : 4 * 32 * XS * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char xs32_raw[X32B];
+  constexpr int NV = HT * QT * 4 + 2 + (D2D_CRITIC_DV2_G ? 0 : HT * 4);
+  constexpr int MIMGB = 4 * 2 * HT * 256 * 2;
+  constexpr int RAWB = MIMGB > NV * 64 * 4 ? MIMGB : NV * 64 * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char raw[RAWB];
+  __shared__ __attribute__((aligned(16))) uint16_t dvimg[4][64];
+  float* red = reinterpret_cast<float*>(raw);
+  uint16_t* mimg = reinterpret_cast<uint16_t*>(raw) + wave * 2 * HT * 256;
+  uint16_t(*xw16)[XS16] = xs16[wave];
+  float(*xw)[XS] = reinterpret_cast<float(*)[XS]>(xs32_raw + (U8 ? 0 : wave * 32 * XS * 4));
+  uint16_t* dvw = dvimg[wave];
+
+  const int stride = a.G * 4;
+  const int tile0 = by * 4 + wave;
+  int e0 = 0;
+  float R[2];
+  bf16x8 xh[2][KC];
+  uint32_t sm[KC][2];
+  record_signs<KC, U8>(sm, a, k, g);
+  // inputs: bias column, zeros past it; bf16 high parts to registers (forward B operand) and LDS (dV1 B
+  // operand); F32: the fp32 image too (the deferred pass).  Returns whether every input is bf16-exact.
+  auto stage = [&](const CriticInT<KC, U8>& src, TileCur c, auto f32img) -> bool {
+    constexpr bool F32 = decltype(f32img)::value;
+    e0 = c.e0;
+    R[0] = src.R[0];
+    R[1] = src.R[1];
+    uint32_t low = 0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int cc = 0; cc < KC; ++cc) {
+        float xr[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int col = 32 * cc + 8 * g + j;
+          // the record carries the bias input at column F and zeros past it
+          xr[j] = U8 ? src.x.at(s, cc, j, sm) : col < F ? src.x.at(s, cc, j, sm) : col == F ? 1.f : 0.f;
+          low |= fbits(xr[j]) & 0xFFFFu;
+        }
+        xh[s][cc] = hi_frag(xr);
+        const u32x4v hv = __builtin_bit_cast(u32x4v, xh[s][cc]);
+        *reinterpret_cast<uint2*>(&xw16[16 * s + i][32 * cc + 8 * g]) = make_uint2(hv[0], hv[1]);
+        *reinterpret_cast<uint2*>(&xw16[16 * s + i][32 * cc + 8 * g + 4]) = make_uint2(hv[2], hv[3]);
+        if constexpr (F32 && !U8) {
+          *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * cc + 8 * g]) = f32x4{xr[0], xr[1], xr[2], xr[3]};
+          *reinterpret_cast<f32x4*>(&xw[16 * s + i][32 * cc + 8 * g + 4]) = f32x4{xr[4], xr[5], xr[6], xr[7]};
+        }
+      }
+    // the record's integers in [-128, 255] are bf16-exact
+    return U8 || __builtin_amdgcn_ballot_w64(low != 0) == 0;
+  };
+  {
+    auto body = [&](auto xe) {
+      constexpr bool XE = decltype(xe)::value;
+      float dvv[2];  // dL/dv of samples i and 16 + i
+      float tdc = 0.f, tls = 0.f;
+#if !D2D_CRITIC_DV2_G
+      float tv2[HT][4];
+#pragma unroll
+      for (int t2 = 0; t2 < HT; ++t2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) tv2[t2][r] = 0.f;
+#endif
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        // HVT = V1 . X^T (hidden 16 t2 + 4 g + r on rows, sample 16 s + i on lanes)
+        // (part-outer, tile-inner: HT independent accumulation chains interleave)
+        f32x4 hv[HT];
+#pragma unroll
+        for (int t2 = 0; t2 < HT; ++t2) hv[t2] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < KC; ++c) {
+#pragma unroll
+          for (int t2 = 0; t2 < HT; ++t2) hv[t2] = mfma_bf16(v1p[t2][c].l, xh[s][c], hv[t2]);
+#pragma unroll
+          for (int t2 = 0; t2 < HT; ++t2) hv[t2] = mfma_bf16(v1p[t2][c].m, xh[s][c], hv[t2]);
+#pragma unroll
+          for (int t2 = 0; t2 < HT; ++t2) hv[t2] = mfma_bf16(v1p[t2][c].h, xh[s][c], hv[t2]);
+        }
+        if constexpr (!XE) {
+#pragma unroll
+          for (int c = 0; c < KC; ++c) {
+            float xv[8];
+            lds_row(xv, xw, 16 * s + i, 32 * c + 8 * g);
+            const Parts xp = split3(xv);
+#pragma unroll
+            for (int t2 = 0; t2 < HT; ++t2) {
+              hv[t2] = mfma_bf16(v1p[t2][c].h, xp.l, hv[t2]);
+              hv[t2] = mfma_bf16(v1p[t2][c].m, xp.m, hv[t2]);
+              hv[t2] = mfma_bf16(v1p[t2][c].h, xp.m, hv[t2]);
+            }
+          }
+        }
+        // value of sample 16 s + i: the lane's 4 HT hidden units, then the four lane groups; relu(HVT)'s high
+        // halves to the image [half s][t2][sample i][hidden 4 g .. 4 g + 3]
+        // (four partial sums: the fma chain's dependent latency, not its issue, bounded the one-sum form)
+        float pv4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t2 = 0; t2 < HT; ++t2) {
+          float hr[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            hr[r] = relu(hv[t2][r]);
+            pv4[r] = fmaf(hr[r], v2r[t2][r], pv4[r]);
+          }
+          *reinterpret_cast<uint2*>(mimg + (s * HT + t2) * 256 + i * 16 + 4 * g) =
+              make_uint2(pack_hi(hr[0], hr[1]), pack_hi(hr[2], hr[3]));
+#if !D2D_CRITIC_DV2_G
+#pragma unroll
+          for (int r = 0; r < 4; ++r) hv[t2][r] = hr[r];
+#endif
+        }
+        const float pv = (pv4[0] + pv4[1]) + (pv4[2] + pv4[3]);
+#if D2D_UPD_ABLATE == 4  // timing ablation: no cross-lane value reduction
+        const float v = pv + c2;
+#else
+        const float v = group_sum(pv) + c2;
+#endif
+        const bool ok = e0 + 16 * s + i < a.E;
+        // the four lane groups hold the same sample: all accumulate, the partial keeps group 0's sums
+        const float d = ok ? v - R[s] : 0.f;
+        dvv[s] = 2.f * a.scale * d;
+        tls = fmaf(d, d, tls);
+        tdc += dvv[s];
+#if !D2D_CRITIC_DV2_G
+#pragma unroll
+        for (int t2 = 0; t2 < HT; ++t2)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tv2[t2][r] = fmaf(dvv[s], hv[t2][r], tv2[t2][r]);
+#endif
+      }
+      // dv's two-way RNE split, shared through LDS: [part][half][sample] (every lane group writes the same value)
+      {
+        const uint32_t dh = rne2(dvv[0], dvv[1]);
+        const uint32_t dm = rne2(sub_bf16_lo(dvv[0], dh), sub_bf16_hi(dvv[1], dh));
+        dvw[i] = (uint16_t)dh;
+        dvw[16 + i] = (uint16_t)(dh >> 16);
+        dvw[32 + i] = (uint16_t)dm;
+        dvw[48 + i] = (uint16_t)(dm >> 16);
+      }
+      lds_order();
+      // A operand k-slots of lane group g: samples 4 g .. 4 g + 3 of half 0, then of half 1
+      const uint2 h0 = *reinterpret_cast<const uint2*>(dvw + 4 * g), h1 = *reinterpret_cast<const uint2*>(dvw + 16 + 4 * g);
+      const uint2 m0 = *reinterpret_cast<const uint2*>(dvw + 32 + 4 * g), m1 = *reinterpret_cast<const uint2*>(dvw + 48 + 4 * g);
+      const uint32_t DH[4] = {h0.x, h0.y, h1.x, h1.y}, DM[4] = {m0.x, m0.y, m1.x, m1.y};
+      // B operands: x sample-on-k (column 16 q + i), the same k-slot order
+      bf16x8 bx[QT], bxm[QT];
+#pragma unroll
+      for (int q = 0; q < QT; ++q) {
+        if constexpr (XE) {
+          const v4i16 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(&xw16[4 * g + (i >> 2)][16 * q + 4 * (i & 3)]));
+          const v4i16 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(&xw16[16 + 4 * g + (i >> 2)][16 * q + 4 * (i & 3)]));
+          bx[q] = cat_tr(x0, x1);
+          bxm[q] = bx[q];
+        } else {
+          float x0[4], x1[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            x0[r] = xw[4 * g + r][16 * q + i];
+            x1[r] = xw[16 + 4 * g + r][16 * q + i];
+          }
+          const Parts2x4 p0 = split2_4(x0), p1 = split2_4(x1);
+          bx[q] = cat(p0.h, p1.h);
+          bxm[q] = cat(p0.m, p1.m);
+        }
+      }
+#pragma unroll
+      for (int t2 = 0; t2 < HT; ++t2) {
+        // relu(HVT)'s high halves of hidden 16 t2 + i, samples 4 g .. 4 g + 3 of each half (lane 4 q' + p of a
+        // 16-lane group addresses row 4 g + q', columns 4 p .. 4 p + 3 of the [sample][hidden] image)
+        const v4i16 t0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(mimg + (0 * HT + t2) * 256 + (4 * g + (i >> 2)) * 16 + 4 * (i & 3)));
+        const v4i16 t1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(mimg + (1 * HT + t2) * 256 + (4 * g + (i >> 2)) * 16 + 4 * (i & 3)));
+        const uint2 w0 = __builtin_bit_cast(uint2, t0), w1 = __builtin_bit_cast(uint2, t1);
+        const uint32_t W[4] = {w0.x, w0.y, w1.x, w1.y};
+        uint32_t ah[4], am[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const uint32_t m01 = pk_min1_u16(W[p]);  // relu'(h) of the two samples, 0 / 1 per half
+          ah[p] = pk_mul_lo_u16(m01, DH[p]);
+          am[p] = pk_mul_lo_u16(m01, DM[p]);
+        }
+        const bf16x8 Ah = as_frag(ah), Am = as_frag(am);
+        // (part-outer: the QT accumulators' chains interleave)
+        if constexpr (!XE) {
+#pragma unroll
+          for (int q = 0; q < QT; ++q) dv1[t2][q] = mfma_bf16(Ah, bxm[q], dv1[t2][q]);  // dv_h x_m
+        }
+#pragma unroll
+        for (int q = 0; q < QT; ++q) dv1[t2][q] = mfma_bf16(Am, bx[q], dv1[t2][q]);     // dv_m x_h
+#if D2D_UPD_ABLATE != 5  // timing ablation 5: no dV1 products
+#pragma unroll
+        for (int q = 0; q < QT; ++q) dv1[t2][q] = mfma_bf16(Ah, bx[q], dv1[t2][q]);     // dv_h x_h
+#endif
+      }
+      dc2.add(tdc);
+      loss_acc.add(tls);
+#if !D2D_CRITIC_DV2_G
+#pragma unroll
+      for (int t2 = 0; t2 < HT; ++t2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dv2k[t2][r].add(tv2[t2][r]);
+#endif
+    };
+    CriticInT<KC, U8> in;
+    bool deferred = false;
+    const TileStride ts(a, stride);
+    TileCur cur_t = tile_at(a, tile0);
+    if (tile0 < a.n_tiles) load_critic_in_t<KC, U8>(in, a, cur_t, k, g, i);
+    while (cur_t.tile < a.n_tiles) {
+      const bool x_exact = stage(in, cur_t, std::false_type{});
+      const TileCur nxt = ts.next(cur_t);
+      if (nxt.tile < a.n_tiles) load_critic_in_t<KC, U8>(in, a, nxt, k, g, i);
+      lds_order();
+      if (x_exact)
+        body(std::true_type{});
+      else
+        deferred = true;
+      lds_order();
+      cur_t = nxt;
+    }
+    if constexpr (!U8) {
+      if (deferred) {
+        for (TileCur c = tile_at(a, tile0); c.tile < a.n_tiles; c = ts.next(c)) {
+          load_critic_in_t<KC, U8>(in, a, c, k, g, i);
+          const bool x_exact = stage(in, c, std::true_type{});
+          lds_order();
+          if (!x_exact) body(std::false_type{});
+          lds_order();
+        }
+      }
+    }
+    (void)deferred;
+  }
+
+  float acc[NV];
+  {
+    int n = 0;
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int q = 0; q < QT; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[n++] = dv1[t][q][r];
+    acc[n++] = dc2.value();
+    acc[n++] = loss_acc.value();
+#if !D2D_CRITIC_DV2_G
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[n++] = dv2k[t][r].value();
+#endif
+  }
+  __syncthreads();  // every wave is past its last read of the relu image the reduction buffer aliases
+  reduce_waves<NV>(acc, red, wave, lane);
+  if (wave != 0) return;
+  float* out = a.partial + ((size_t)by * a.N + k) * a.P;
+  const int OB1 = H * F, OW2 = OB1 + H, OB2 = OW2 + H, OST = OB2 + 1;
+  const float* V1 = a.w1 + (size_t)k * H * F;
+  float dv2p[HT][4];
+  int n = 0;
+#pragma unroll
+  for (int t = 0; t < HT; ++t) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dv2p[t][r] = 0.f;
+#pragma unroll
+    for (int q = 0; q < QT; ++q)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int hid = 16 * t + 4 * g + r, col = 16 * q + i;
+        const float G = acc[n++];
+        if (hid < H) {
+          if (col < F) out[hid * F + col] = G * v2r[t][r];
+          else if (col == F) out[OB1 + hid] = G * v2r[t][r];
+#if D2D_CRITIC_DV2_G
+          const float w = col < F ? V1[(size_t)hid * F + col] : col == F ? a.b1[(size_t)k * H + hid] : 0.f;
+          dv2p[t][r] = fmaf(w, G, dv2p[t][r]);
+#endif
+        }
+      }
+  }
+  const float dcs = row_sum16(acc[n]);
+  const float ls = row_sum16(acc[n + 1]);
+#if !D2D_CRITIC_DV2_G
+#pragma unroll
+  for (int t = 0; t < HT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dv2p[t][r] = acc[n + 2 + 4 * t + r];
+#endif
+#pragma unroll
+  for (int t = 0; t < HT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = row_sum16(dv2p[t][r]);
+      const int hid = 16 * t + 4 * g + r;
+      if (i == 0 && hid < H) out[OW2 + hid] = v;
+    }
+  if (lane == 0) {
+    out[OB2] = dcs;
+    out[OST] = ls;
+    out[OST + 1] = 0.f;
+  }
+}
+
 // Fixed-order sum of the G workgroup partials of every (agent, parameter) -> gradient tensors.
 __global__ void update_reduce_kernel(const float* __restrict__ partial, int G, int N, int P, int H, int F, int A,
                                      float* gw1, float* gb1, float* gw2, float* gb2, float* stats) {
@@ -1270,27 +1688,55 @@ static int64_t tensor_extent(const int64_t (&st)[3], int T, int E, int N) {
   return 1 + (int64_t)(T - 1) * st[0] + (int64_t)(E - 1) * st[1] + (int64_t)(N - 1) * st[2];
 }
 
-// Workgroups per agent: about 4 per CU over the whole grid, at least one tile per wave, and at most
-// kMaxWaveTiles tiles per wave.  A wave sums its tiles' weight gradients in MFMA accumulators, an
-// fp32 chain whose rounding error grows with its length: at the 65,536-env batch 16 workgroups per
-// agent left 6,400 tiles per wave and dW2 at 4x torch fp32's error against float64
-// (tools/gpu/ppo_grads_full_batch.py); the G partials are summed by update_reduce_kernel (G x N x P
-// floats, 0.26 GB at that batch).
+// Workgroups per agent: whole rounds of the kernel's resident workgroups (its occupancy x the CU count: a
+// partial last round leaves CUs idle -- the hidden-on-rows critic at 3 workgroups per CU over a 4-per-CU grid ran
+// a second round one third full), at least one tile per wave, and at most kMaxWaveTiles tiles per wave.  A wave
+// sums its tiles' weight gradients in MFMA accumulators, an fp32 chain whose rounding error grows with its
+// length: at the 65,536-env batch 16 workgroups per agent left 6,400 tiles per wave and dW2 at 4x torch fp32's
+// error against float64 (tools/gpu/ppo_grads_full_batch.py); the G partials are summed by update_reduce_kernel
+// (G x N x P floats, 0.26 GB at that batch).
 #ifndef D2D_UPD_MAX_WAVE_TILES
 #define D2D_UPD_MAX_WAVE_TILES 256
 #endif
 constexpr int64_t kMaxWaveTiles = D2D_UPD_MAX_WAVE_TILES;
-static int update_blocks(int N, int64_t n_tiles) {
-  const int64_t fill = (1024 + N - 1) / N, cap = (n_tiles + 4 * kMaxWaveTiles - 1) / (4 * kMaxWaveTiles);
+static int update_blocks(int N, int64_t n_tiles, int resident) {
+  const int64_t need = (int64_t)N * ((n_tiles + 4 * kMaxWaveTiles - 1) / (4 * kMaxWaveTiles));
+  const int64_t rounds = std::max<int64_t>(1, (need + resident - 1) / resident);
+  const int64_t G = (rounds * resident + N - 1) / N;
   // (grid.y <= 65535: past that, more tiles per wave)
-  return (int)std::max<int64_t>(1, std::min<int64_t>({std::max(fill, cap), (n_tiles + 3) / 4, 65535}));
+  return (int)std::max<int64_t>(1, std::min<int64_t>({G, (n_tiles + 3) / 4, 65535}));
+}
+static int cu_count() {
+  static const int n = [] {  // (a function-local static: initialised once, thread-safe)
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+    return std::max(1, cus);
+  }();
+  return n;
+}
+// resident 256-thread workgroups of update kernel K on the device, queried once per instantiation
+template <auto K>
+static int upd_resident() {
+  static const int n = [] {
+    int per = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, K, 256, 0) != hipSuccess || per < 1) per = 2;
+    return per * cu_count();
+  }();
+  return n;
+}
+// the workspace bound for any kernel's G: rounds x resident < need + resident <= need + 8 workgroups per CU
+static int update_blocks_bound(int N, int64_t n_tiles) {
+  const int64_t need = (int64_t)N * ((n_tiles + 4 * kMaxWaveTiles - 1) / (4 * kMaxWaveTiles));
+  const int64_t G = (need + 8 * (int64_t)cu_count() + N - 1) / N;
+  return (int)std::max<int64_t>(1, std::min<int64_t>({G, (n_tiles + 3) / 4, 65535}));
 }
 
 extern "C" int64_t d2d_ppo_workspace(int32_t n_agents, int32_t T, int32_t n_envs, int32_t obs_dim, int32_t hidden,
                                      int32_t n_out) {
   if (n_agents <= 0 || T <= 0 || n_envs <= 0) return 0;
   const int64_t tiles = (int64_t)T * ((n_envs + 31) / 32);
-  const int G = update_blocks(n_agents, tiles);
+  const int G = update_blocks_bound(n_agents, tiles);
   const int64_t P = (int64_t)hidden * obs_dim + hidden + (int64_t)n_out * hidden + n_out + 2;
   return (int64_t)G * n_agents * P;
 }
@@ -1328,7 +1774,7 @@ static UpdArgs make_args(const d2d_mlp_desc* d, int T, const void* obs, float* w
   a.mask_bytes = a.A <= 8 ? 1 : a.A <= 16 ? 2 : 4;
   a.tiles_per_t = (a.E + 31) / 32;
   a.n_tiles = T * a.tiles_per_t;
-  a.G = update_blocks(a.N, a.n_tiles);
+  a.G = 0;  // set by the launch (update_blocks with the launched kernel's residency)
   a.P = a.H * a.F + a.H + a.A * a.H + a.A + 2;
   a.inv_A = 1.f / (float)a.A;
   a.w1 = d->w1; a.b1 = d->b1; a.w2 = d->w2; a.b2 = d->b2;
@@ -1346,28 +1792,48 @@ static int launch_reduce(const UpdArgs& a, float* gw1, float* gb1, float* gw2, f
   return D2D_OK;
 }
 
+// KRES: the instantiation whose residency sizes the grid -- the record (U8) one for both input formats, so that
+// fp32 rows and the record split the tiles into the same workgroup partials and sum them in the same order (their
+// gradients are bitwise equal on bf16-exact inputs, tests/test_record_gpu.py)
+template <auto K, auto KRES = K>
+static void launch_upd(UpdArgs& a, hipStream_t s) {
+  a.G = update_blocks(a.N, a.n_tiles, upd_resident<KRES>());
+  hipLaunchKernelGGL(K, dim3(a.N, a.G), dim3(256), 0, s, a);
+}
 template <int KC, int HT, bool U8>
-static void launch_actor_fmt(const UpdArgs& a, hipStream_t s) {
-  dim3 grid(a.N, a.G);
+static void launch_actor_fmt(UpdArgs& a, hipStream_t s) {
   const bool pair = a.A <= 8;
   // the headline action count (8 channels / 8 ids) on the record: A at compile time
-  if (U8 && a.kind == 0 && a.A == 8) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, true, U8, 8>), grid, dim3(256), 0, s, a);
-  else if (U8 && a.kind == 1 && a.A == 8) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, true, U8, 8>), grid, dim3(256), 0, s, a);
-  else if (a.kind == 0 && pair) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, true, U8>), grid, dim3(256), 0, s, a);
-  else if (a.kind == 0) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 0, false, U8>), grid, dim3(256), 0, s, a);
-  else if (pair) hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, true, U8>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((ppo_actor_grad_kernel<KC, HT, 1, false, U8>), grid, dim3(256), 0, s, a);
+  // (grids sized by the record instantiation of the same kind and pairing, launch_upd)
+  if (U8 && a.kind == 0 && a.A == 8) launch_upd<ppo_actor_grad_kernel<KC, HT, 0, true, U8, 8>>(a, s);
+  else if (U8 && a.kind == 1 && a.A == 8) launch_upd<ppo_actor_grad_kernel<KC, HT, 1, true, U8, 8>>(a, s);
+  else if (a.kind == 0 && a.A == 8)
+    launch_upd<ppo_actor_grad_kernel<KC, HT, 0, true, U8>, ppo_actor_grad_kernel<KC, HT, 0, true, true, 8>>(a, s);
+  else if (a.kind == 1 && a.A == 8)
+    launch_upd<ppo_actor_grad_kernel<KC, HT, 1, true, U8>, ppo_actor_grad_kernel<KC, HT, 1, true, true, 8>>(a, s);
+  else if (a.kind == 0 && pair) launch_upd<ppo_actor_grad_kernel<KC, HT, 0, true, U8>, ppo_actor_grad_kernel<KC, HT, 0, true, true>>(a, s);
+  else if (a.kind == 0) launch_upd<ppo_actor_grad_kernel<KC, HT, 0, false, U8>, ppo_actor_grad_kernel<KC, HT, 0, false, true>>(a, s);
+  else if (pair) launch_upd<ppo_actor_grad_kernel<KC, HT, 1, true, U8>, ppo_actor_grad_kernel<KC, HT, 1, true, true>>(a, s);
+  else launch_upd<ppo_actor_grad_kernel<KC, HT, 1, false, U8>, ppo_actor_grad_kernel<KC, HT, 1, false, true>>(a, s);
 }
 template <int KC, int HT>
-static void launch_actor(const UpdArgs& a, hipStream_t s) {
+static void launch_actor(UpdArgs& a, hipStream_t s) {
   if (a.rec) launch_actor_fmt<KC, HT, true>(a, s);
   else launch_actor_fmt<KC, HT, false>(a, s);
 }
+// d2d_set_option(D2D_OPT_CRITIC_GRAD_ROWS, 1): the sample-on-rows critic kernel of rounds 2-4 (A/B)
+std::atomic<int> g_critic_grad_rows{0};
 template <int KC, int HT>
-static void launch_critic(const UpdArgs& a, hipStream_t s) {
-  dim3 grid(a.N, a.G);
-  if (a.rec) hipLaunchKernelGGL((ppo_critic_grad_kernel<KC, HT, true>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((ppo_critic_grad_kernel<KC, HT, false>), grid, dim3(256), 0, s, a);
+static void launch_critic(UpdArgs& a, hipStream_t s) {
+  // H in (64, 128]: the hidden-on-rows kernel holds 340 VGPRs at one wave per SIMD and measured slower there
+  // (1.69 vs 1.54 ms per 26 M agent-samples, tools/gpu/upd_ab.py); the sample-on-rows kernel keeps that shape
+  if (HT > 4 || g_critic_grad_rows.load(std::memory_order_relaxed)) {
+    if (a.rec) launch_upd<ppo_critic_grad_kernel<KC, HT, true>>(a, s);
+    else launch_upd<ppo_critic_grad_kernel<KC, HT, false>, ppo_critic_grad_kernel<KC, HT, true>>(a, s);
+    return;
+  }
+  if (a.rec) launch_upd<ppo_critic_grad_t_kernel<KC, HT, true>>(a, s);
+  else launch_upd<ppo_critic_grad_t_kernel<KC, HT, false>, ppo_critic_grad_t_kernel<KC, HT, true>>(a, s);
 }
 
 extern "C" int d2d_ppo_actor_grad(const d2d_mlp_desc* d, int32_t T, const void* obs, const void* actions,

@@ -37,12 +37,13 @@ def refuse_ablation(what):
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 10
+ABI_VERSION = 11
 D2D_OBS_F32, D2D_OBS_U8 = 0, 1
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
 D2D_OPT_GRU_GRAD_HISTORY = 3  # 1: d2d_gru_grad through the global row history even where the LDS path applies
 D2D_OPT_POLICY_CRITIC_SPLIT = 4  # 1: the iPPO critic value as its own launch beside the actor (bitwise the same)
+D2D_OPT_CRITIC_GRAD_ROWS = 5  # 1: d2d_ppo_critic_grad on the sample-on-rows kernel of rounds 2-4 (A/B)
 
 _p = ctypes.c_void_p
 

@@ -6,9 +6,10 @@ from .record import set_format
 
 
 def policy_mlp_step(actor, obs, kind, critic=None, forced=None, rng_step=0, deterministic=False, seed=0,
-                    env_base=0, actions=None, logp=None, value=None):
+                    env_base=0, actions=None, logp=None, value=None, want_value=True):
     """actor/critic: dicts of agent-stacked fp32 tensors w1 [N][H][F], b1 [N][H], w2 [N][A][H], b2 [N][A]
     (critic: A = 1).  obs [E][N][F] fp32, or the env kernel's ObsRecord of that shape.  kind 'comb' (Bernoulli, masks out) or 'chsel' (Categorical, ids out).
+    want_value=False with critic weights passes value = NULL to the C ABI (valid usage: the value is skipped).
     Returns (actions [E][N], logp [N][E], value [N][E] or None)."""
     lib = _lib.require_gpu()
     N, H, F = actor["w1"].shape
@@ -27,7 +28,7 @@ def policy_mlp_step(actor, obs, kind, critic=None, forced=None, rng_step=0, dete
             actions = torch.zeros((E, N), dtype=torch.uint8, device=dev)
     if logp is None:
         logp = torch.empty((N, E), dtype=torch.float32, device=dev)
-    if critic is not None and value is None:
+    if critic is not None and value is None and want_value:
         value = torch.empty((N, E), dtype=torch.float32, device=dev)
     p = lambda t: t.data_ptr()  # noqa: E731
     desc = _lib.MlpDesc(N, E, F, H, A, k, p(actor["w1"]), p(actor["b1"]), p(actor["w2"]), p(actor["b2"]),
@@ -39,4 +40,4 @@ def policy_mlp_step(actor, obs, kind, critic=None, forced=None, rng_step=0, dete
                                  int(rng_step), 1 if deterministic else 0, actions.data_ptr(), logp.data_ptr(),
                                  None if value is None else value.data_ptr(), _lib.stream_ptr())
     _lib.check(rc, "d2d_policy_mlp_step")
-    return actions, logp, (value if critic is not None else None)
+    return actions, logp, (value if critic is not None and want_value else None)

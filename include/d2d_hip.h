@@ -43,11 +43,12 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 10  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
+#define D2D_ABI_VERSION 11  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
                               6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_states_to_bf16_exact,
                               d2d_critic_dpre_split; 8: d2d_gae_scan_moments, d2d_normalize_pair;
                               9: d2d_gae_scan_moments without outputs, d2d_gae_scan_normalized;
-                              10: d2d_states_to_bf16_padded, d2d_critic_dpre_split3 */
+                              10: d2d_states_to_bf16_padded, d2d_critic_dpre_split3;
+                              11: D2D_OPT_CRITIC_GRAD_ROWS */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -392,8 +393,12 @@ int d2d_gru_grad(const d2d_gru_desc* desc, int32_t T, const void* obs, const voi
  *   for a buffer sized under the other setting).
  * D2D_OPT_POLICY_CRITIC_SPLIT: d2d_policy_mlp_step with a critic runs the actor and the critic value as two
  *   launches of the split kernel (1) or as one fused launch (0); the same arithmetic either way (bitwise
- *   identical actions, log-probs and values).  Default: policy_kernels.hip's D2D_POLICY_CRITIC_SPLIT. */
-enum { D2D_OPT_NT_STORES = 1, D2D_OPT_POLICY_F32_MFMA = 2, D2D_OPT_GRU_GRAD_HISTORY = 3, D2D_OPT_POLICY_CRITIC_SPLIT = 4 };
+ *   identical actions, log-probs and values).  Default: policy_kernels.hip's D2D_POLICY_CRITIC_SPLIT.
+ * D2D_OPT_CRITIC_GRAD_ROWS: 1 = d2d_ppo_critic_grad on the sample-on-rows kernel of rounds 2-4 (A/B; the same
+ *   gradients within fp32 rounding); 0 (default) = the hidden-on-rows kernel (update_kernels.hip).
+ * Options are process-wide words (relaxed atomics) read once per call. */
+enum { D2D_OPT_NT_STORES = 1, D2D_OPT_POLICY_F32_MFMA = 2, D2D_OPT_GRU_GRAD_HISTORY = 3, D2D_OPT_POLICY_CRITIC_SPLIT = 4,
+       D2D_OPT_CRITIC_GRAD_ROWS = 5 };
 int d2d_set_option(int32_t option, int32_t value);
 
 const char* d2d_last_error(void);

@@ -13,6 +13,8 @@ probabilities propagated through log(p) / log(1 - p)) wherever every probability
 [1e-3, 1 - 1e-3], as the MLP kernel tests; deterministic actions exact away from ties; gradients within
 2e-5 * max|g| of float64 autograd where torch fp32 itself lands in that band, else within 4x torch
 fp32's distance (saturated gates / probabilities)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -470,7 +472,8 @@ def test_gru_grads_long_window(kind, c, grad_input):
     """gru_grad_kernel at history_len = n_agents = 128 / 256 (xp_n_agents.py:98-112): all eight gradient
     tensors vs float64 autograd over the padded training windows, the band rule of the xp_load test.  At 256
     the product input only (the compact record, cooperative path): the float64 reference there is minutes."""
-    if c["L"] > 128 and grad_input != "record":
+    if c["L"] > 128 and grad_input != "record" and os.environ.get("D2D_TEST_LONG_ALL") != "1":
+        # (D2D_TEST_LONG_ALL=1 runs them: profiles/r05/gru_long_window_all.log)
         pytest.skip("L = 256: the record (product) path; the fp32-row and row-history kernels are covered at 128")
     xp_grads_check(kind, grad_input, c["E"], cfg=c)
 

@@ -239,11 +239,16 @@ def test_learner_matches_reference(name, E):
             r0 = steps[0][k].astype(np.float64)
             band = np.abs(gt - r0).max()
             err = np.abs(g0 - r0).max()
-            tol = max(4e-5 * np.abs(r0).max(), 4 * band) + 1e-7
-            if err > 2e-5 * np.abs(r0).max():
+            gmax = np.abs(r0).max()
+            # the band term calibrates from a second implementation; its ceiling (25x the base bar) keeps the
+            # check pinned to the reference if both GPU paths drift the same way
+            assert band <= 1e-3 * gmax + 1e-7, ("torch path itself off the reference", msg, k, float(band), float(gmax))
+            tol = max(4e-5 * gmax, 4 * band) + 1e-7
+            if err > 2e-5 * gmax:
+                via = " (passes through the band term only)" if err > 4e-5 * gmax + 1e-7 else ""
                 print(f"  {msg} {k}: first-step |g - g_ref| {err:.2e}, torch path {band:.2e}, max|g_ref| "
-                      f"{np.abs(r0).max():.2e}")
-            assert err <= tol, (msg, k, float(err), float(band), float(np.abs(r0).max()))
+                      f"{gmax:.2e}{via}")
+            assert err <= tol, (msg, k, float(err), float(band), float(gmax))
             assert_weights_close(vd.cpu().numpy(), z[f"{pre}/{k}"], ref_adam_tolerance(steps, k, lr_, tuple(vd.shape)),
                                  f"{msg} {k}", rec.swing(vd))
 

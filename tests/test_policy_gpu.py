@@ -180,10 +180,11 @@ def test_forced_full_waves_equal_sampled_logp(kind, F, H, A, in_dims):
 
 @pytest.mark.parametrize("kind,F,H,A", [("comb", 30, 64, 8), ("chsel", 12, 64, 5)])
 def test_one_round_waves_and_critic_split(kind, F, H, A):
-    """Sampling and deterministic launches size every wave to one resident round (64 agents x 32,845 envs: about
-    1,000 envs per wave, a ragged tail); forced launches keep 256 envs per wave.  The sampled log-probs equal the
-    forced evaluation's bit for bit, values match torch (1e-5), and the actor + value-only launches
-    (D2D_OPT_POLICY_CRITIC_SPLIT) reproduce the fused kernel's actions, log-probs and values bit for bit."""
+    """Sampling, deterministic and forced launches all size every wave to one resident round (64 agents x 32,845
+    envs: about 1,000 envs per wave, a ragged tail; the forced bytes travel through the obs DMA ring).  The sampled
+    log-probs equal the forced evaluation's bit for bit, values match torch (1e-5), and the actor + value-only
+    launches (D2D_OPT_POLICY_CRITIC_SPLIT) reproduce the fused kernel's actions, log-probs and values bit for bit --
+    also with critic weights and value = NULL (the value-only launch is skipped, nothing is stored)."""
     from d2dhip import _lib
     from d2dhip.policy import policy_mlp_step
     lib = _lib.require_gpu()
@@ -200,10 +201,14 @@ def test_one_round_waves_and_critic_split(kind, F, H, A):
         lib.d2d_set_option(_lib.D2D_OPT_POLICY_CRITIC_SPLIT, 1)
         acts3, lp3, val3 = policy_mlp_step(actor, obs, kind, crit, rng_step=4, seed=5)
         acts_d3, lp_d3, val_d3 = policy_mlp_step(actor, obs, kind, crit, deterministic=True)
+        acts4, lp4, val4 = policy_mlp_step(actor, obs, kind, crit, rng_step=4, seed=5, want_value=False)
+        torch.cuda.synchronize()
     finally:
         lib.d2d_set_option(_lib.D2D_OPT_POLICY_CRITIC_SPLIT, 0)
     assert torch.equal(acts3, acts)
     torch.testing.assert_close(lp3, lp, rtol=0, atol=0)
+    assert val4 is None and torch.equal(acts4, acts)
+    torch.testing.assert_close(lp4, lp, rtol=0, atol=0)
     torch.testing.assert_close(val3, val, rtol=0, atol=0)
     acts_d, lp_d, val_d = policy_mlp_step(actor, obs, kind, crit, deterministic=True)
     assert torch.equal(acts_d3, acts_d)

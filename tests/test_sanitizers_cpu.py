@@ -9,7 +9,6 @@ GPU sanitizers are not available on the GPU pool).
 Each suite runs in a child process with the sanitizer runtime preloaded; the child first proves
 that the instrumented library is the one mapped.  Leak checking is off (CPython and torch keep
 allocations alive at exit) and so is the new/delete mismatch check inside uninstrumented torch."""
-import glob
 import os
 import subprocess
 import sys
@@ -18,21 +17,11 @@ import pytest
 
 from conftest import ROOT
 
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+from sanitizer_runtimes import clang_runtime, gcc_runtimes  # noqa: E402
+
 ENV_BASE = {"ASAN_OPTIONS": "detect_leaks=0:alloc_dealloc_mismatch=0:abort_on_error=1",
             "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1", "PYTHONDONTWRITEBYTECODE": "1"}
-
-
-def gcc_runtimes():
-    """The gcc ASan / UBSan runtimes (the C oracle's), or None when this host has none."""
-    paths = [subprocess.run(["gcc", f"-print-file-name={n}"], capture_output=True, text=True).stdout.strip()
-             for n in ("libasan.so", "libubsan.so")]
-    return paths if all(os.path.isabs(p) and os.path.exists(p) for p in paths) else None
-
-
-def clang_runtime():
-    """The clang ASan runtime of the ROCm toolchain (the HIP library's host code), or None."""
-    rts = glob.glob("/opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so")
-    return rts[0] if rts else None
 
 
 def _build(target_dir, lib):

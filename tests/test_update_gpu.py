@@ -369,9 +369,11 @@ def test_happo_chain_kernel_matches_torch_loop():
         torch.testing.assert_close(M, ref, rtol=2e-6, atol=0)
 
 
-def test_grads_on_large_rollout_vs_float64():
-    """iPPO's fused actor and critic gradients on a real 2,048-env x 200-slot rollout of the c3 config
-    (64 agents x 8 channels, 409,600 samples per agent) against float64 autograd, EVERY agent.
+@pytest.mark.parametrize("E", [2048, 8192])
+def test_grads_on_large_rollout_vs_float64(E):
+    """iPPO's fused actor and critic gradients on a real E-env x 200-slot rollout of the c3 config
+    (64 agents x 8 channels; 409,600 / 1,638,400 samples per agent -- 8,192 envs is the longest accumulation
+    chain update_blocks allows, 256 tiles per wave) against float64 autograd, EVERY agent.
 
     Criterion, elementwise: |g_kernel - g64| <= envelope + max(2e-5, 4 x torch fp32's own excess) x max|g64|.
     The envelope (tools/gpu/ppo_grads_full_batch.py _flip_envelope) is the largest change relu-mask flips
@@ -381,12 +383,13 @@ def test_grads_on_large_rollout_vs_float64():
     to 5e-4 of max|g| in torch fp32 autograd itself (agent 27) as well as in the kernels (agents 22, 45, 59),
     each on w1 / b1 only (profiles/r03k/ppo_full_2048_all.json); the envelope is computed, not fitted,
     and is zero for every tensor but w1 / b1.  Everything outside it is held to the fp32 band.
-    (The 65,536-env headline batch runs the same comparison in tools/gpu/ppo_grads_full_batch.py.)"""
+    (The 65,536-env headline batch runs the same comparison in tools/gpu/ppo_grads_full_batch.py:
+    profiles/r05/ppo_full_65536_all_envelope.json.)"""
     import os
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "gpu"))
     from ppo_grads_full_batch import grads_vs_float64
-    out = grads_vs_float64(2048, range(64), emulate=False, envelope=True)
+    out = grads_vs_float64(E, range(64), emulate=False, envelope=True)
     checked = 0
     worst = (0.0, None)
     for key, exc in out.items():

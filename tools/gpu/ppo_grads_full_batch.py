@@ -6,7 +6,7 @@ accumulated over sample chunks.  Prints max |kernel - f64| / max |g| per tensor,
 chunks (the fp32 band the kernels are held to).
 The kernels' accumulation chains are long here: at 65,536 envs 409,600 32-sample tiles per agent, at
 most 256 per wave since round 3 (update_blocks); tests/test_update_gpu.py runs the comparison at 8,192 envs.
-usage (GPU box): python3 tools/gpu/ppo_grads_full_batch.py [E] [K] [reversed] [envelope]"""
+usage (GPU box): python3 tools/gpu/ppo_grads_full_batch.py [E] [K | a:b] [reversed] [envelope] [noemu]"""
 import json
 import os
 import sys
@@ -81,6 +81,7 @@ def grads_vs_float64(E, agents, emulate=True, seed=11, reversed_fp32=False, enve
     sg = (rec.signed.to(torch.int64) & 0xFFFFFFFF)
     out = {"E": E, "T": T, "samples_per_agent": B}
     for k in agents:
+        print(f"[ppo_grads_full_batch] E {E}: agent {k}", file=sys.stderr, flush=True)  # progress (long runs)
         cols = torch.arange(F, device="cuda")
         neg = ((sg[k, cols // 32] >> (cols % 32)) & 1).bool()
         q = {n: v[k].double().clone().requires_grad_() for n, v in pp.items()}
@@ -173,8 +174,11 @@ def grads_vs_float64(E, agents, emulate=True, seed=11, reversed_fp32=False, enve
 
 if __name__ == "__main__":
     E = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
-    K = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-    out = grads_vs_float64(E, range(K), reversed_fp32="reversed" in sys.argv[3:], envelope="envelope" in sys.argv[3:])
+    ks = sys.argv[2] if len(sys.argv) > 2 else "2"   # K (agents 0..K-1) or a:b (agents a..b-1)
+    agents = range(*map(int, ks.split(":"))) if ":" in ks else range(int(ks))
+    K = len(agents)
+    out = grads_vs_float64(E, agents, reversed_fp32="reversed" in sys.argv[3:], envelope="envelope" in sys.argv[3:],
+                           emulate="noemu" not in sys.argv[3:])
     print(json.dumps(out), flush=True)
     summ = {}
     for kk, vv in out.items():
@@ -184,6 +188,6 @@ if __name__ == "__main__":
         elif kk.count("/") == 3:
             tag, net, _, n = kk.split("/")
             summ.setdefault(f"{tag}/{net}/{n}", []).append(vv)
-    res = {"E": E, "T": out["T"], "agents": K, "samples_per_agent": out["samples_per_agent"]}
+    res = {"E": E, "T": out["T"], "agents": K, "agent_range": ks, "samples_per_agent": out["samples_per_agent"]}
     res.update({kk: {"max": max(vv), "median": float(np.median(vv))} for kk, vv in sorted(summ.items())})
     print(json.dumps(res), flush=True)
