@@ -287,13 +287,17 @@ def rollout_leg(env, args, world):
     K = args.rollout_steps
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
 
+    # the training slot as iPPO.train runs it: actor-only when the values are deferred to the first epoch's
+    # critic pass (iPPO.defer_values), else actor + critic
+    vslot = None if lr._defer_values_ok() else val
+
     def slot(k, e=None):
         if b.timestep >= env.episode_length:
             b.reset(want_obs=True, out_obs=ring[k % 2])
         with torch.no_grad():
             if e is not None:
                 e[0].record()
-            lr._policy_slot(ring, 0, k % 2, True, act, logp, val, None, b)
+            lr._policy_slot(ring, 0, k % 2, True, act, logp, vslot, None, b)
             if e is not None:
                 e[1].record()
             b.step(act, want_obs=True, out_obs=ring[(k + 1) % 2], out_reward=rew)
@@ -316,12 +320,17 @@ def rollout_leg(env, args, world):
     pol_ms = max_over_ranks(float(np.mean([e[0].elapsed_time(e[1]) for e in ev])), world)
     env_ms = max_over_ranks(float(np.mean([e[1].elapsed_time(e[2]) for e in ev])), world)
     F, H, A = lr.policy.F, lr.policy.H, lr.policy.A
-    flop = 2 * (F * H + H * A) + 2 * (F * H + H)  # actor + critic forward per agent-step
+    # actor (+ critic when the slot computes values) forward per agent-step
+    flop = 2 * (F * H + H * A) + (2 * (F * H + H) if vslot is not None else 0)
     # the products run as exact bf16 splits: an fp32-equivalent rate is no roofline (it can
     # exceed the fp32 MFMA peak); the roofline figure is the executed MFMA pipe's busy fraction (PMC, with
     # its source file and commit), beside the algorithmic rate in GFLOP/s
     return {"env_steps_per_s": v, "agent_steps_per_s": v * b.spec.N, "ms_per_step": el / K * 1e3, "steps": K,
-            "policy": f"iPPO MLP H=64 actor+critic, 64 agents, Bernoulli sampling, fp32; {path}",
+            "policy": (f"iPPO MLP H=64 {'actor+critic' if vslot is not None else 'actor'}, 64 agents, Bernoulli "
+                       f"sampling, fp32; {path}"),
+            "values": ("per slot (actor + critic kernel)" if vslot is not None else
+                       "deferred: V(obs) of every sample from the first epoch's critic-gradient pass "
+                       "(d2d_ppo_critic_grad_values), GAE after it"),
             "obs_format": "compact record (u8)" if lr._record_ok() else "fp32",
             "policy_kernel_us": pol_ms * 1e3, "env_kernel_us": env_ms * 1e3,
             "policy_flop_per_agent_step": flop,
@@ -427,8 +436,9 @@ def train_leg(env, args, rank, world, local):
 
     def iteration(n_epoch):
         # the body of iPPO.train for one iteration (ippo.py:410-426) without the test(50) calls
-        # the reference makes when iter % test_freq == 0 (always true at iter 0)
-        ro = lr._rollout(E)
+        # the reference makes when iter % test_freq == 0 (always true at iter 0); as train() does, the rollout's
+        # values come from the first epoch's critic pass (iPPO.defer_values)
+        ro = lr._rollout(E, defer_values=True)
         upd = lr._update_state(ro)
         for _ in range(n_epoch):
             lr._update_epoch(ro, upd)

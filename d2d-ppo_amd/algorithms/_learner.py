@@ -210,10 +210,12 @@ class BatchedLearnerBase(DataParallelMixin):
             self._pseed = int(torch.randint(0, 2 ** 62, (1,)).item())
         return self._pseed
 
-    def _mlp_desc(self, E, env_base):
+    def _mlp_desc(self, E, env_base, critic=True):
+        """critic=False: the actor alone (the kernel's actor-only instantiation: no critic forward where no
+        value is stored -- test(), and training rollouts whose values come from the first epoch's critic pass)"""
         from d2dhip import _lib
         p = self.policy.params
-        crit = getattr(self, "value", None)
+        crit = getattr(self, "value", None) if critic else None
         cp = crit.params if (crit is not None and getattr(crit, "kind", None) == "mlp") else None
         ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
         return _lib.MlpDesc(self.policy.N, E, self.policy.F, self.policy.H, self.policy.A,
@@ -244,7 +246,7 @@ class BatchedLearnerBase(DataParallelMixin):
         if self._fused_ok() and (self.kind == "comb") == bool(self.combinatorial):
             from d2dhip import _lib
             lib = _lib.require_gpu()
-            desc = self._mlp_desc(b.E, b.desc.env_base)
+            desc = self._mlp_desc(b.E, b.desc.env_base, critic=val_out is not None)
             desc.rng_offset = b.rng_off.data_ptr()
             fz = None
             if forced is not None:

@@ -12,6 +12,8 @@ run as ONE agent-stacked forward/backward; the prefix is N elementwise
 multiplies over [B] in sigma order, left to right exactly like the
 reference's loop.  Per-agent clip_grad_norm_(20) and Adam are kept.
 """
+import os
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -284,6 +286,10 @@ class D2DPPO(BatchedLearnerBase):
     # iteration against 2.3-2.6 ms for the split-K bf16 path (profiles/r04/critic_small.log)
     CRITIC_SPLIT_MIN_DIM = 0
     CRITIC_F32_FWD_MAX_DIM = 768  # below this state width the forward's first layer is one fp32 GEMM
+    # round 5: the forward and the backward's per-sample glue as one HIP kernel over the bf16 operand
+    # (csrc/critic_kernels.hip, d2d_central_critic_fwd; hidden a multiple of 4 up to 128); D2D_CRITIC_FUSED=0
+    # keeps the hipBLASLt forward GEMM + the dpre split kernel (A/B, tests)
+    critic_fused = os.environ.get("D2D_CRITIC_FUSED", "1") != "0"
 
     def _critic_split_forward(self, ro):
         """Value(state) = linear2(relu(linear1(state))) (d2d_ppo.py:95-98) for all T*E states.  At
@@ -328,6 +334,8 @@ class D2DPPO(BatchedLearnerBase):
             ro.state_bf16 = xb
         l1, l2 = self.value_network.linear1, self.value_network.linear2
         H = l1.weight.shape[0]
+        if self.critic_fused and H % 4 == 0 and H <= 128:
+            return self._critic_fused_forward(ro, xb, S)
         if S < self.CRITIC_F32_FWD_MAX_DIM:
             # narrow states: the first layer as one fp32 GEMM on the env-major fp32 states (4 S + 4 H bytes
             # per sample) beats the split GEMM's [3H][B] fp32 output and its sum (2 S + 28 H bytes) below
@@ -355,14 +363,53 @@ class D2DPPO(BatchedLearnerBase):
             v = torch.addmm(l2.bias[:, None], l2.weight, hid)[0]                           # [B]
         return v, pre, hid
 
+    def _critic_fused_forward(self, ro, xb, S):
+        """d2d_central_critic_fwd: V(state) of every sample and, against the critic target returns.mean
+        (d2d_ppo.py:339, 440-446), dPre's three RNE bf16 parts [B][3H] and the sums db1 / dW2 / db2 / sum (v - R)^2
+        per workgroup, in one pass over the bf16 operand (the critic's weights are the same at the backward).
+        Returns (values [B], None, None, dhm, partial)."""
+        from d2dhip import _lib
+        lib = _lib.require_gpu()
+        l1, l2 = self.value_network.linear1, self.value_network.linear2
+        H = l1.weight.shape[0]
+        B = xb.shape[0]
+        dev = xb.device
+        G = int(lib.d2d_central_critic_blocks(H, B))
+        nimg = int(lib.d2d_central_critic_image_bytes(H, S))
+        img = getattr(self, "_critic_img", None)
+        if img is None or img.numel() < nimg // 16 or img.device != dev:
+            img = self._critic_img = torch.empty((nimg // 16, 4), dtype=torch.int32, device=dev)  # 16-byte entries
+        v = torch.empty(B, dtype=torch.float32, device=dev)
+        dhm = torch.empty((B, 3 * H), dtype=torch.bfloat16, device=dev)
+        part = torch.empty((max(G, 1), 2 * H + 2), dtype=torch.float32, device=dev)
+        w1 = l1.weight.detach().contiguous()
+        ret = ro.ret_mean.contiguous()
+        _lib.check(lib.d2d_central_critic_fwd(H, B, S, xb.shape[1], xb.data_ptr(), w1.data_ptr(),
+                                              l1.bias.detach().data_ptr(), l2.weight.detach().data_ptr(),
+                                              l2.bias.detach().data_ptr(), ret.data_ptr(), img.data_ptr(), v.data_ptr(),
+                                              dhm.data_ptr(), part.data_ptr(), G, _lib.stream_ptr()),
+                   "d2d_central_critic_fwd")
+        return v, None, None, dhm, part
+
     def _critic_split_backward(self, ro, crit):
         """Gradients of mse(V, returns) into the critic's .grad (what value_loss.backward() leaves,
         d2d_ppo.py:208-216): dW1 = dPreᵀ X on a three-way RNE bf16 split of dPre (~2^-24 relative per
         product term, torch fp32's level) against the exact bf16 states; dPre's split and the db1 / dW2 sums
         come from one HIP pass (d2d_critic_dpre_split3), dW1 from a split-K batched GEMM."""
-        v, pre, _ = crit
         l1, l2 = self.value_network.linear1, self.value_network.linear2
         H = l1.weight.shape[0]
+        if len(crit) == 5:  # the fused kernel already made dPre's parts and the sums
+            v, _, _, dhm, part = crit
+            with torch.no_grad():
+                sums = part.sum(0)                                                      # db1 | dW2 | db2 | sum d^2
+                value_loss = sums[2 * H + 1] / v.numel()
+                g = self._dw1_gemm_bm(dhm, ro.state_bf16)[:, :l1.weight.shape[1]]       # [3H][S]
+                grads = {l1.weight: (g[2 * H:] + g[H:2 * H]) + g[:H], l1.bias: sums[:H], l2.weight: sums[H:2 * H],
+                         l2.bias: sums[2 * H:2 * H + 1]}
+                for prm, gr in grads.items():
+                    prm.grad = gr.reshape(prm.shape).contiguous()
+            return value_loss
+        v, pre, _ = crit
         with torch.no_grad():
             d = v - ro.ret_mean
             value_loss = (d * d).mean()
@@ -389,6 +436,17 @@ class D2DPPO(BatchedLearnerBase):
             for prm, gr in grads.items():
                 prm.grad = gr.reshape(prm.shape).contiguous()
         return value_loss
+
+    @staticmethod
+    def _dw1_gemm_bm(dhm, xb):
+        """_dw1_gemm with dPre's parts sample-major ([B][pH], the fused kernel's layout): [pH][S] fp32."""
+        B = dhm.shape[0]
+        nc = next((c for c in (64, 50, 40, 32, 25, 20, 16, 10, 8, 5, 4, 2) if B % c == 0 and B // c >= 4096), 1)
+        if nc == 1:
+            return torch.mm(dhm.t(), xb, out_dtype=torch.float32)
+        Bc = B // nc
+        a = dhm.view(nc, Bc, dhm.shape[1]).transpose(1, 2)                              # [nc][pH][Bc], strided
+        return torch.bmm(a, xb.view(nc, Bc, xb.shape[1]), out_dtype=torch.float32).sum(0)
 
     @staticmethod
     def _dw1_gemm(dhm, xb):

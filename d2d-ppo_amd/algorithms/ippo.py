@@ -12,6 +12,8 @@ structures; the work runs agent-batched on the MI355X:
     (ippo.py:194-217), which are independent across agents, so summing them
     leaves every agent's gradient unchanged.
 """
+import os
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -164,11 +166,31 @@ class iPPO(BatchedLearnerBase):
         self._setup_data_parallel(self.policy.parameters() + self.value.parameters())
 
     # ------------------------------------------------------------ rollouts
-    def _rollout(self, num_episodes, teacher=None):
-        ro = self._collect(num_episodes, train=True, want_values=True, teacher=teacher)
+    # training rollouts of the fused MLP path take their values (ippo.py:308) from the first update epoch's
+    # critic pass instead of a critic forward in every rollout slot: the critic's weights are the same at both
+    # points, and that pass computes V(obs) of every sample anyway (d2d_ppo_critic_grad_values).  The rollout
+    # slot then runs the actor-only policy kernel; GAE follows the critic pass.  D2D_DEFER_VALUES=0: per-slot values
+    defer_values = os.environ.get("D2D_DEFER_VALUES", "1") != "0"
+
+    def _defer_values_ok(self):
+        return self.defer_values and not self.useRNN and self._fused_ok() and self._fused_update_ok()
+
+    def _rollout(self, num_episodes, teacher=None, defer_values=False):
+        """defer_values (train()): values and advantages are filled in by the first _epoch_fused on this rollout;
+        the reference-API paths (create_rollouts, tests) keep the per-slot values."""
+        defer = defer_values and teacher is None and self._defer_values_ok()
+        ro = self._collect(num_episodes, train=True, want_values=not defer, teacher=teacher)
         self._phase("rollout")
-        # values [T][N][E] as the policy kernel wrote them; adv / ret in the same layout (ippo.py:337-338)
-        ro.adv_tne, ro.ret_tne = self._gae(ro.rewards, ro.values, ro.dones, layout="tce")
+        if defer:
+            s = self.env.batch().spec
+            ro.values = torch.zeros((ro.T, s.N, ro.E), dtype=torch.float32, device=self.device)
+            # the returns (discount_rewards, ippo.py:338) read no value: they are the critic pass's targets
+            _, ro.ret_tne = self._gae(ro.rewards, ro.values, ro.dones, normalize_adv=False, layout="tce")
+            ro.adv_tne = None
+            ro.values_pending = True
+        else:
+            # values [T][N][E] as the policy kernel wrote them; adv / ret in the same layout (ippo.py:337-338)
+            ro.adv_tne, ro.ret_tne = self._gae(ro.rewards, ro.values, ro.dones, layout="tce")
         self._phase("gae")
         return ro
 
@@ -221,6 +243,22 @@ class iPPO(BatchedLearnerBase):
         pp, vp = self.policy.params, self.value.params
         kind = "comb" if self.combinatorial else "chsel"
         B = ro.T * ro.E
+        sv = None
+        critic_first = bool(getattr(ro, "values_pending", False))
+        if critic_first:
+            # first epoch on a deferred-values rollout: the critic pass first, writing V(obs) of every sample --
+            # the rollout critic's values (same weights) -- then its Adam step, then GAE for the actor (the two
+            # optimizers are independent, so the order of the two updates does not change either)
+            _, sv = critic_grads({k: v.data for k, v in vp.items()}, ro.obs, ro.ret_tne.permute(0, 2, 1),
+                                 grads=self._grad_buffers(vp), values=ro.values.permute(0, 2, 1))
+            self._phase("critic_grad")
+            self._reduce_grads(self.value.parameters())
+            self._phase("allreduce")
+            self.value_optimizer.step()
+            self._phase("adam")
+            ro.adv_tne, _ = self._gae(ro.rewards, ro.values, ro.dones, normalize_ret=False, layout="tce")
+            ro.values_pending = False
+            self._phase("gae")
         if self.useRNN:  # GRU policies / critics: BPTT over the padded training windows (gru_kernels.hip)
             from d2dhip import gru
             _, sa = gru.grads({k: v.data for k, v in pp.items()}, ro.obs, self._gru_kind(), self.history_len, ro.L,
@@ -235,18 +273,21 @@ class iPPO(BatchedLearnerBase):
         self._phase("allreduce")
         self.policy_optimizer.step()
         self._phase("adam")
-        if self.useRNN:
+        if critic_first:  # (the critic ran first on this epoch)
+            pass
+        elif self.useRNN:
             from d2dhip import gru
             _, sv = gru.grads({k: v.data for k, v in vp.items()}, ro.obs, None, self.history_len, ro.L,
                               ro.ret_tne.permute(0, 2, 1), grads=self._grad_buffers(vp))
         else:
             _, sv = critic_grads({k: v.data for k, v in vp.items()}, ro.obs, ro.ret_tne.permute(0, 2, 1),
                                  grads=self._grad_buffers(vp))
-        self._phase("critic_grad")
-        self._reduce_grads(self.value.parameters())
-        self._phase("allreduce")
-        self.value_optimizer.step()
-        self._phase("adam")
+        if not critic_first:
+            self._phase("critic_grad")
+            self._reduce_grads(self.value.parameters())
+            self._phase("allreduce")
+            self.value_optimizer.step()
+            self._phase("adam")
         return -(sa[:, 0] + beta * sa[:, 1]) / B, sv[:, 0] / B
 
     def _update_epoch(self, ro, upd):
@@ -263,7 +304,7 @@ class iPPO(BatchedLearnerBase):
         policy_loss_list = []
         value_loss_list = []
         for iter in range(num_iter):
-            ro = self._rollout(num_episodes)
+            ro = self._rollout(num_episodes, defer_values=True)
             scores = ro.scores
             scores_episode += scores
             upd = self._update_state(ro)

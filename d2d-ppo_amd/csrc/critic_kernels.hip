@@ -1,0 +1,285 @@
+// D2D-PPO's central critic on gfx950: the forward over the bf16 state operand fused with the per-sample part of
+// the backward.
+//
+// Replaces, for every sample b of an epoch (d2d_ppo.py:62-98 Value, 208-216 the critic's MSE update):
+//   pre_b = W1 x_b + b1,  v_b = w2 . relu(pre_b) + b2                  (Value.forward on state x_b)
+//   d_b = v_b - R_b,  dv_b = 2 d_b / B                                    (F.mse_loss(values, returns.mean(1)))
+//   dpre_b = [pre_b > 0] w2 dv_b                                           (linear2 / relu backward)
+// and the sums db1 = sum_b dpre_b, dW2 = sum_b relu(pre_b) dv_b, db2 = sum_b dv_b, sum_b d_b^2.  dW1 = sum_b
+// dpre_b x_b^T stays a split-K GEMM over the operand (d2d_ppo.py _dw1_gemm): dpre is written as its three-way RNE
+// bf16 split, sample-major [B][3H] (the d2d_critic_dpre_split3 parts, ~2^-24 relative per product term).
+//
+// Before (round 4): one hipBLASLt GEMM [3H x S] . [S x B] -> fp32 [3H][B] partial products of W1's three parts, a
+// sum, relu, the 64 -> 1 GEMM, then the dpre split kernel over pre: ~1.6 GB of fp32 intermediates per epoch at 256
+// agents x 4,096 envs beside the 6.3 GB operand (critic_fwd 3.5 ms per epoch, profiles/r04).  Here the operand
+// is read once, the intermediates stay in registers, and the kernel writes v [B] and dpre's parts [B][3H] (bf16).
+//
+// Mapping: a 256-thread workgroup owns 64 ST samples (each wave 16 ST: ST sample tiles of 16) and all H <= 16 HT
+// hidden units.  K loop over the state in chunks of 32 features: lane (g, i) of sample tile st holds sample
+// 16 st + i, features 32c + 8g .. + 7 as its B fragment (one 16-byte load, prefetched one chunk ahead); W1's exact
+// three-way split (truncation parts, mlp_common.h split3: the products are exact, x is an integer) arrives as a
+// per-chunk image of A fragments [t][part][lane] (built once per epoch by critic_w1_image_kernel), staged through
+// a double-buffered LDS slice shared by the workgroup's four waves (one barrier per chunk).  The accumulator
+// (hidden 16t + 4g + r on rows, sample on lanes) is the actor kernels' forward orientation: the 64 -> 1 head is a
+// per-lane fma over the lane's hidden units plus a sum over the four lane groups.
+#include <algorithm>
+
+#include "mlp_common.h"
+
+namespace d2d {
+
+struct CriticArgs {
+  int H, S, nchunk;
+  int64_t B, ldx;
+  const uint16_t* xb;   // [B][ldx] bf16 (exact integer states; columns [S, ldx) zero)
+  const bf16x8* w1img;  // [nchunk][HT][3][64] A fragments
+  const float *b1, *w2, *b2, *ret;
+  float two_over_B;
+  float* values;        // [B]
+  uint16_t* dhm;        // [B][3H] bf16: dpre's RNE parts h | m | l
+  float* partial;       // [G][2H + 2]: db1 | dW2 | db2 | sum d^2
+};
+
+// the chunk image: chunk c, hidden tile t, part p (0 h, 1 m, 2 l), lane (g, i) <- W1[16t + i][32c + 8g .. + 7]
+template <int HT>
+__global__ __launch_bounds__(256) void critic_w1_image_kernel(int H, int S, int nchunk, const float* __restrict__ w1,
+                                                              bf16x8* __restrict__ img) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (int64_t)nchunk * HT * 64) return;
+  const int lane = (int)(idx & 63), t = (int)((idx >> 6) % HT), c = (int)((idx >> 6) / HT);
+  const int g = lane >> 4, i = lane & 15, hrow = 16 * t + i;
+  float wv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = 32 * c + 8 * g + j;
+    wv[j] = (hrow < H && col < S) ? w1[(size_t)hrow * S + col] : 0.f;
+  }
+  const Parts p = split3(wv);
+  bf16x8* o = img + ((size_t)(c * HT + t) * 3) * 64 + lane;
+  o[0] = p.h;
+  o[64] = p.m;
+  o[128] = p.l;
+}
+
+// RNE bf16 of a (low half) and b (high half)
+__device__ __forceinline__ uint32_t rne_pk(float a, float b) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  const bf2 v = {(__bf16)a, (__bf16)b};  // v_cvt_pk_bf16_f32
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ float bf_lo(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
+
+template <int HT, int ST>
+__global__ __launch_bounds__(256, 2) void critic_fwd_kernel(CriticArgs a) {
+  constexpr int NI = HT * 3 * 64;  // 16-byte image entries per chunk
+  __shared__ __attribute__((aligned(16))) bf16x8 wl[2][NI];
+  __shared__ float red[4][2 * 16 * HT + 2];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int H = a.H;
+  const int64_t s0 = (int64_t)blockIdx.x * (64 * ST) + (int64_t)wave * (16 * ST);  // this wave's first sample
+  // the wave's rows through a range-checked descriptor: rows past B read 0
+  const int64_t rest = (a.B - s0) * a.ldx * 2;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.xb + (rest > 0 ? s0 * a.ldx : 0)), 0,
+      rest <= 0 ? 0u : rest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)rest, 0x00020000);
+  uint32_t vo[ST];
+#pragma unroll
+  for (int st = 0; st < ST; ++st) vo[st] = (uint32_t)(((int64_t)(16 * st + i) * a.ldx + 8 * g) * 2);
+  auto load_x = [&](bf16x8 (&x)[ST], int c) {
+#pragma unroll
+    for (int st = 0; st < ST; ++st)
+      x[st] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, vo[st] + 64u * (uint32_t)c, 0, 0));
+  };
+  constexpr int NW = (NI + 255) / 256;  // image entries per thread and chunk
+  bf16x8 wr[NW];
+  auto load_w = [&](int c) {
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const int e = tid + 256 * q;
+      if (NI % 256 == 0 || e < NI) wr[q] = a.w1img[(size_t)c * NI + e];
+    }
+  };
+  f32x4 acc[ST][HT];
+#pragma unroll
+  for (int st = 0; st < ST; ++st)
+#pragma unroll
+    for (int t = 0; t < HT; ++t) acc[st][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 xc[ST], xn[ST];
+  load_w(0);
+  load_x(xc, 0);
+  for (int c = 0; c < a.nchunk; ++c) {
+    // buffer c & 1 was last read in iteration c - 2: every wave passed iteration c - 1's barrier since
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      const int e = tid + 256 * q;
+      if (NI % 256 == 0 || e < NI) wl[c & 1][e] = wr[q];
+    }
+    if (c + 1 < a.nchunk) {
+      load_w(c + 1);
+      load_x(xn, c + 1);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      const bf16x8 ah = wl[c & 1][(t * 3 + 0) * 64 + lane], am = wl[c & 1][(t * 3 + 1) * 64 + lane],
+                   al = wl[c & 1][(t * 3 + 2) * 64 + lane];
+#pragma unroll
+      for (int st = 0; st < ST; ++st) {
+        acc[st][t] = mfma_bf16(al, xc[st], acc[st][t]);
+        acc[st][t] = mfma_bf16(am, xc[st], acc[st][t]);
+        acc[st][t] = mfma_bf16(ah, xc[st], acc[st][t]);
+      }
+    }
+#pragma unroll
+    for (int st = 0; st < ST; ++st) xc[st] = xn[st];
+  }
+
+  // ---- epilogue: bias, relu, value, dv, dpre's split; the lane's sums over its samples
+  float b1r[HT][4], w2r[HT][4];
+#pragma unroll
+  for (int t = 0; t < HT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = 16 * t + 4 * g + r;
+      b1r[t][r] = h < H ? a.b1[h] : 0.f;
+      w2r[t][r] = h < H ? a.w2[h] : 0.f;
+    }
+  const float b2 = a.b2[0];
+  float pdb1[HT][4], pdw2[HT][4], pdc2 = 0.f, ploss = 0.f;
+#pragma unroll
+  for (int t = 0; t < HT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pdb1[t][r] = pdw2[t][r] = 0.f;
+  const int H3 = 3 * H;
+#pragma unroll
+  for (int st = 0; st < ST; ++st) {
+    const int64_t b = s0 + 16 * st + i;
+    const bool ok = b < a.B;
+    float pre[HT][4], hr[HT][4], pv4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pre[t][r] = acc[st][t][r] + b1r[t][r];
+        hr[t][r] = relu(pre[t][r]);
+        pv4[r] = fmaf(hr[t][r], w2r[t][r], pv4[r]);
+      }
+    const float v = group_sum((pv4[0] + pv4[1]) + (pv4[2] + pv4[3])) + b2;
+    const float R = ok ? a.ret[b] : 0.f;
+    const float d = ok ? v - R : 0.f;
+    const float dv = d * a.two_over_B;
+    if (ok && g == 0) a.values[b] = v;
+    pdc2 += g == 0 ? dv : 0.f;
+    ploss = fmaf(g == 0 ? d : 0.f, d, ploss);
+    uint16_t* row = a.dhm + (ok ? b : 0) * H3;
+#pragma unroll
+    for (int t = 0; t < HT; ++t) {
+      float dp[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dp[r] = pre[t][r] > 0.f ? w2r[t][r] * dv : 0.f;
+        pdb1[t][r] += dp[r];
+        pdw2[t][r] = fmaf(hr[t][r], dv, pdw2[t][r]);
+      }
+      // three RNE parts (d2d_critic_dpre_split3): h = RNE(dp), m = RNE(dp - h), l = RNE(dp - h - m)
+      uint32_t ph[2], pm[2], pl[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float x0 = dp[2 * q], x1 = dp[2 * q + 1];
+        ph[q] = rne_pk(x0, x1);
+        const float r0 = x0 - bf_lo(ph[q]), r1 = x1 - bf_hi(ph[q]);
+        pm[q] = rne_pk(r0, r1);
+        pl[q] = rne_pk(r0 - bf_lo(pm[q]), r1 - bf_hi(pm[q]));
+      }
+      const int h0 = 16 * t + 4 * g;
+      if (ok && h0 < H) {  // (H is a multiple of 4 on this path: the four units of a lane are all real or none)
+        *reinterpret_cast<uint2*>(row + h0) = make_uint2(ph[0], ph[1]);
+        *reinterpret_cast<uint2*>(row + H + h0) = make_uint2(pm[0], pm[1]);
+        *reinterpret_cast<uint2*>(row + 2 * H + h0) = make_uint2(pl[0], pl[1]);
+      }
+    }
+  }
+  // ---- the workgroup's sums: over the 16 samples of a row (lanes i), then the four waves in order
+  float* rw = red[wave];
+#pragma unroll
+  for (int t = 0; t < HT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float s1 = row_sum16(pdb1[t][r]), s2 = row_sum16(pdw2[t][r]);
+      if (i == 0) {
+        rw[16 * t + 4 * g + r] = s1;
+        rw[16 * HT + 16 * t + 4 * g + r] = s2;
+      }
+    }
+  const float sc = group_sum(row_sum16(pdc2)), sl = group_sum(row_sum16(ploss));
+  if (lane == 0) {
+    rw[32 * HT] = sc;
+    rw[32 * HT + 1] = sl;
+  }
+  __syncthreads();
+  float* out = a.partial + (size_t)blockIdx.x * (2 * H + 2);
+  for (int q = tid; q < 2 * H + 2; q += 256) {
+    const int src = q < H ? q : q < 2 * H ? 16 * HT + (q - H) : 32 * HT + (q - 2 * H);
+    out[q] = ((red[0][src] + red[1][src]) + red[2][src]) + red[3][src];
+  }
+}
+
+}  // namespace d2d
+
+using namespace d2d;
+
+static int critic_ht(int H) { return H <= 32 ? 2 : H <= 64 ? 4 : H <= 128 ? 8 : 0; }
+static int critic_st(int ht) { return ht <= 4 ? 4 : 2; }
+
+extern "C" int32_t d2d_central_critic_blocks(int32_t H, int64_t B) {
+  const int ht = critic_ht(H);
+  if (ht == 0 || B <= 0) return 0;
+  const int64_t per = 64 * critic_st(ht);
+  return (int32_t)((B + per - 1) / per);
+}
+
+extern "C" int64_t d2d_central_critic_image_bytes(int32_t H, int32_t S) {
+  const int ht = critic_ht(H);
+  if (ht == 0 || S < 1) return 0;
+  return (int64_t)((S + 31) / 32) * ht * 3 * 64 * 16;
+}
+
+extern "C" int d2d_central_critic_fwd(int32_t H, int64_t B, int32_t S, int64_t ldx, const uint16_t* xb, const float* w1,
+                                      const float* b1, const float* w2, const float* b2, const float* ret,
+                                      void* w1img, float* values, uint16_t* dhm, float* partial, int32_t G,
+                                      void* stream) {
+  const int ht = critic_ht(H);
+  if (ht == 0 || H % 4) { d2d_set_error("d2d_central_critic_fwd: hidden=%d (a multiple of 4 in [4, 128])", H); return D2D_EUNSUPPORTED; }
+  if (B < 0 || S < 1 || ldx < S || (ldx & 7) || !w1 || !b1 || !w2 || !b2 || !w1img || G != d2d_central_critic_blocks(H, B) ||
+      (B > 0 && (!xb || !ret || !values || !dhm || !partial)) || (reinterpret_cast<uintptr_t>(xb) & 15) ||
+      (reinterpret_cast<uintptr_t>(w1img) & 15) || (reinterpret_cast<uintptr_t>(dhm) & 7)) {
+    d2d_set_error("d2d_central_critic_fwd: bad arguments (ldx a multiple of 8 >= S, 16-byte aligned operand and "
+                  "image, G = d2d_central_critic_blocks)");
+    return D2D_EINVAL;
+  }
+  if (B == 0) return D2D_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  CriticArgs a{};
+  a.H = H; a.S = S; a.nchunk = (S + 31) / 32; a.B = B; a.ldx = ldx; a.xb = xb;
+  a.w1img = reinterpret_cast<const bf16x8*>(w1img);
+  a.b1 = b1; a.w2 = w2; a.b2 = b2; a.ret = ret; a.two_over_B = 2.f / (float)B;
+  a.values = values; a.dhm = dhm; a.partial = partial;
+  const int64_t img_n = (int64_t)a.nchunk * ht * 64;
+  const unsigned ig = (unsigned)((img_n + 255) / 256);
+  bf16x8* img = reinterpret_cast<bf16x8*>(w1img);
+  if (ht == 2) {
+    hipLaunchKernelGGL(critic_w1_image_kernel<2>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
+    hipLaunchKernelGGL((critic_fwd_kernel<2, 4>), dim3(G), dim3(256), 0, s, a);
+  } else if (ht == 4) {
+    hipLaunchKernelGGL(critic_w1_image_kernel<4>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
+    hipLaunchKernelGGL((critic_fwd_kernel<4, 4>), dim3(G), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(critic_w1_image_kernel<8>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
+    hipLaunchKernelGGL((critic_fwd_kernel<8, 2>), dim3(G), dim3(256), 0, s, a);
+  }
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}

@@ -197,9 +197,11 @@ __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* 
 // KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even);
 // U8: the inputs are the env kernel's compact obs record (D2D_OBS_U8)
 template <int KC, int HT, int KIND, bool CRITIC, int MODE, bool U8>
-// (H <= 64, F + 1 <= 32: 2 waves / SIMD; H in (64, 128] -- the learners' default hidden_size 128 -- or
-// F + 1 > 32: one wave / SIMD with the doubled weight fragments in registers)
-__global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? 2 : 1) void policy_split_kernel(MlpArgs a) {
+// (H <= 64, F + 1 <= 32: 2 waves / SIMD with the iPPO critic or on fp32 rows (their DMA ring is 48 KB), 3 for the
+// actor alone on the record (137 VGPRs: test(), D2D-PPO,
+// and iPPO training rollouts whose values come from the first epoch's critic pass); H in (64, 128] -- the
+// learners' default hidden_size 128 -- or F + 1 > 32: one wave / SIMD with the doubled weight fragments)
+__global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 3) : 1) void policy_split_kernel(MlpArgs a) {
   static_assert(HT % 2 == 0, "layer 2 consumes hidden tiles in pairs");
   // Philox step of the launch, read once before the obs pipeline starts (the optional device
   // offset of graph replays; a load inside the epilogue would add a wait to every tile pair)

@@ -77,6 +77,14 @@
 // bit for bit (tests/test_record_gpu.py); off
 #define D2D_DW2_PAIRED 0
 #endif
+#ifndef D2D_ACTOR_DZ_ONCE
+// record-path actor, paired epilogue (A <= 8): dZ split three ways ONCE in the epilogue's paired layout (both
+// halves at once) and the parts moved to each half's dH A operand by permlane32 swaps -- was a split per half of
+// the swapped values; dW2's dZ operand (two-way RNE = the first two parts) reaches the sample-on-k layout as bf16
+// through LDS with ds_read_b64_tr_b16 instead of an fp32 transpose and a second split; dH's relu mask applied to
+// the split parts with packed u16 ops.  Bitwise the same operands (and so gradients) as before
+#define D2D_ACTOR_DZ_ONCE 1
+#endif
 #ifndef D2D_UPD_WAVES
 #define D2D_UPD_WAVES 2  // waves per SIMD the update kernels are register-budgeted for (KC = 1)
 #endif
@@ -103,6 +111,8 @@ struct UpdArgs {
   int64_t lo_st[3], w_st[3];
   int64_t lo_ext, w_ext;            // 1 + the largest element offset of logp_old / weight (floats)
   float* partial;                   // [G][N][P]
+  float* vout;                      // critic: NULL, or the value of sample (t, e, k) at t*v_st[0] + e*v_st[1] + k*v_st[2]
+  int64_t v_st[3];
 };
 
 
@@ -244,6 +254,18 @@ __device__ __forceinline__ uint32_t relu_mask_pair(float r0, float r1) {
   uint32_t m, o;
   asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(hi), "s"(0x00010001u));
   asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(o) : "v"(m), "s"(0x3F803F80u));
+  return o;
+}
+
+// v_pk_min_u16 / v_pk_mul_lo_u16 (asm: the compiler turns the packed forms into per-half compares + selects)
+__device__ __forceinline__ uint32_t pk_min1_u16(uint32_t x) {
+  uint32_t m;
+  asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(x), "s"(0x00010001u));
+  return m;
+}
+__device__ __forceinline__ uint32_t pk_mul_lo_u16(uint32_t a, uint32_t b) {
+  uint32_t o;
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(o) : "v"(a), "v"(b));
   return o;
 }
 
@@ -517,6 +539,9 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? D2D_UPD_WAVES : 1) void
   constexpr int XS16 = 32 * KC + 4;  // bf16 rows of 8-byte multiples, 8 banks apart per 4 rows
   __shared__ __attribute__((aligned(16))) unsigned char xs_raw[TR ? 4 * 32 * XS16 * 2 : 4 * 32 * XS * 4];
   __shared__ __attribute__((aligned(16))) float dzt[4][2][16][20];
+  // DZ1 (D2D_ACTOR_DZ_ONCE): dZ's bf16 parts [half][part h / m][sample][16 actions] in the dzt space
+  constexpr bool DZ1 = TR && PAIR && D2D_ACTOR_DZ_ONCE;
+  static_assert(2 * 2 * 16 * 16 * 2 <= 2 * 16 * 20 * 4, "the dZ part image fits the wave's dzt slice");
   constexpr int NV = HT * QT * 4 + HT * 4 + 4 + 2;
   // TR: relu(HT)'s split parts [wave][half][hidden tile][part][16 samples][16 hidden] bf16; the
   // cross-wave reduction buffer (used only after the tile loop) shares the space
@@ -528,6 +553,7 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? D2D_UPD_WAVES : 1) void
   float(*xw)[XS] = reinterpret_cast<float(*)[XS]>(xs_raw + (TR ? 0 : wave * 32 * XS * 4));
   uint16_t(*xw16)[XS16] = reinterpret_cast<uint16_t(*)[XS16]>(xs_raw + (TR ? wave * 32 * XS16 * 2 : 0));
   float(*zb)[16][20] = dzt[wave];
+  uint16_t* zim = reinterpret_cast<uint16_t*>(&dzt[wave][0][0][0]);  // DZ1: [s][part][16][16]
 
   const int stride = a.G * 4;
   const int tile0 = by * 4 + wave;
@@ -653,7 +679,44 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? D2D_UPD_WAVES : 1) void
 
       // ---- epilogue -> dZ (lane (g, i): sample 16s + i, actions 4g + r), written transposed to LDS
       f32x4 dz[2];
-      if constexpr (PAIR) {
+      bf16x8 za_hm[2], za_hl[2];  // DZ1: dH's A operands of each half
+      if constexpr (DZ1) {
+        f32x4 zc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) zc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(zt[0][r]), fu(zt[1][r]), false, false)[0]);
+        const int e = e0 + 16 * (g >> 1) + i;
+#if D2D_UPD_ABLATE == 1  // timing ablation: no epilogue (dz = z)
+        const f32x4 dzc = zc;
+#else
+        const f32x4 dzc = ppo_dz<KIND, true, false, AFIX>(a, zc, cur.act[0], cur.lo[0], cur.w[0], e < a.E, g & 1, surr_acc, ent_acc);
+#endif
+#pragma unroll
+        for (int r = 0; r < 4; ++r) db2[r].add(dzc[r]);
+        // three RNE parts of this lane's 4 actions (half g >> 1, sample i, actions 4 (g & 1) .. + 3)
+        const float dv[4] = {dzc[0], dzc[1], dzc[2], dzc[3]};
+        const Parts4 zp = split3rne_4(dv);
+        // dW2's operand: the h and m parts (= the two-way RNE split) as bf16 rows [half][part][sample][action]
+        uint16_t* zw = zim + ((g >> 1) * 2) * 256 + i * 16 + 4 * (g & 1);
+        *reinterpret_cast<uint2*>(zw) = make_uint2(zp.h[0], zp.h[1]);
+        *reinterpret_cast<uint2*>(zw + 256) = make_uint2(zp.m[0], zp.m[1]);
+        // each half's parts into lanes 0-31 (lanes 32-63: 0, against W2's zero k-slots of actions 8-15)
+        uint32_t ph[2][2], pm[2][2], pl[2][2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const auto sh = __builtin_amdgcn_permlane32_swap(zp.h[q], 0u, false, false);
+          const auto sm_ = __builtin_amdgcn_permlane32_swap(zp.m[q], 0u, false, false);
+          const auto sl = __builtin_amdgcn_permlane32_swap(zp.l[q], 0u, false, false);
+          ph[0][q] = sh[0]; ph[1][q] = sh[1];
+          pm[0][q] = sm_[0]; pm[1][q] = sm_[1];
+          pl[0][q] = sl[0]; pl[1][q] = sl[1];
+        }
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          // (part order l, h, m: the two operands share h's registers, as cat(zp.h, zp.m) / cat(zp.l, zp.h))
+          za_hm[h2] = cat(ph[h2], pm[h2]);
+          za_hl[h2] = cat(pl[h2], ph[h2]);
+        }
+      } else if constexpr (PAIR) {
         f32x4 zc;
 #pragma unroll
         for (int r = 0; r < 4; ++r) zc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(zt[0][r]), fu(zt[1][r]), false, false)[0]);
@@ -690,15 +753,28 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? D2D_UPD_WAVES : 1) void
       //      from LDS, bf16-exact on env observations, else split too)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        float dzn[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dzn[r] = zb[s][4 * g + r][i];
-        // dW2^T operand B: dZ (k = sample 4g + j of this half, column = action i), two-way split
-        // (v_mfma_f32_16x16x4_f32 on the unsplit operands -- four chains of 4 per hidden tile -- removes
-        // 120 VALU per tile but measured 13 % slower: the fp32 MFMAs' issue cost outweighs the VALU)
-        const Parts2x4 zn = split2_4(dzn);
+        bf16x8 bz1, bz2;
         const uint32_t zz[2] = {0u, 0u};
-        const bf16x8 bz1 = cat(zn.h, zn.h), bz2 = cat(zn.m, zz);
+        if constexpr (DZ1) {
+          // dZ's h / m parts of samples 4g .. 4g + 3 (this half), action i, transposed from the bf16 rows
+          typedef __attribute__((address_space(3))) v4i16* lds_v4i16;
+          const uint16_t* zr = zim + (s * 2) * 256 + (4 * g + (i >> 2)) * 16 + 4 * (i & 3);
+          const uint2 zh = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(zr)));
+          const uint2 zm = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(zr + 256)));
+          const uint32_t zh2[2] = {zh.x, zh.y}, zm2[2] = {zm.x, zm.y};
+          bz1 = cat(zh2, zh2);
+          bz2 = cat(zm2, zz);
+        } else {
+          float dzn[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dzn[r] = zb[s][4 * g + r][i];
+          // dW2^T operand B: dZ (k = sample 4g + j of this half, column = action i), two-way split
+          // (v_mfma_f32_16x16x4_f32 on the unsplit operands -- four chains of 4 per hidden tile -- removes
+          // 120 VALU per tile but measured 13 % slower: the fp32 MFMAs' issue cost outweighs the VALU)
+          const Parts2x4 zn = split2_4(dzn);
+          bz1 = cat(zn.h, zn.h);
+          bz2 = cat(zn.m, zz);
+        }
         bf16x8 bx1[QT], bx2[QT];
 #pragma unroll
         for (int q = 0; q < QT; ++q) {
@@ -727,10 +803,17 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? D2D_UPD_WAVES : 1) void
             bx2[q] = cat(xq.m, z2);    // dH_h x_m
           }
         }
-        const float dv[4] = {dz[s][0], dz[s][1], dz[s][2], dz[s][3]};
-        const Parts4 zp = split3rne_4(dv);
-        // (part order l, h, m: the two operands can share h's registers)
-        const bf16x8 a_hm = cat(zp.h, zp.m), a_hl = cat(zp.l, zp.h);
+        bf16x8 a_hm, a_hl;
+        if constexpr (DZ1) {
+          a_hm = za_hm[s];
+          a_hl = za_hl[s];
+        } else {
+          const float dv[4] = {dz[s][0], dz[s][1], dz[s][2], dz[s][3]};
+          const Parts4 zp = split3rne_4(dv);
+          // (part order l, h, m: the two operands can share h's registers)
+          a_hm = cat(zp.h, zp.m);
+          a_hl = cat(zp.l, zp.h);
+        }
 #pragma unroll
         for (int t2 = 0; t2 < HT; ++t2) {
           if constexpr (TR) {
@@ -745,17 +828,30 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? D2D_UPD_WAVES : 1) void
             acc = mfma_bf16(a_hm, w2b_s[t2][2][lane], acc);
             // relu' from the high part: nonzero exactly when relu(h) is (down to bf16's underflow at
             // ~1e-40, far below any pre-activation of normal-magnitude weights and inputs)
-            float dh[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) dh[r] = th[r] != 0 ? acc[r] : 0.f;
 #if !D2D_DW2_PAIRED
             const v4i16 tm = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(im + 256));
             const bf16x8 h_hm = cat_tr(th, tm);
             dw2[t2] = mfma_bf16(h_hm, bz2, dw2[t2]);
             dw2[t2] = mfma_bf16(h_hm, bz1, dw2[t2]);
 #endif
-            const Parts2x4 dp = split2_4(dh);
-            const bf16x8 d_hm = cat(dp.h, dp.m);
+            bf16x8 d_hm;
+            if constexpr (DZ1) {
+              // split, then the mask on the packed parts: min(h-part bits, 1) is 0 / 1 per sample, and
+              // x 0 / 1 keeps or zeroes a part (split2(0) = (0, 0): the same operand as masking first)
+              const float av[4] = {acc[0], acc[1], acc[2], acc[3]};
+              const Parts2x4 dp = split2_4(av);
+              const uint2 tw = __builtin_bit_cast(uint2, th);
+              const uint32_t m0 = pk_min1_u16(tw.x), m1 = pk_min1_u16(tw.y);
+              const uint32_t dh2[2] = {pk_mul_lo_u16(m0, dp.h[0]), pk_mul_lo_u16(m1, dp.h[1])};
+              const uint32_t dm2[2] = {pk_mul_lo_u16(m0, dp.m[0]), pk_mul_lo_u16(m1, dp.m[1])};
+              d_hm = cat(dh2, dm2);
+            } else {
+              float dh[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) dh[r] = th[r] != 0 ? acc[r] : 0.f;
+              const Parts2x4 dp = split2_4(dh);
+              d_hm = cat(dp.h, dp.m);
+            }
 #pragma unroll
             for (int q = 0; q < QT; ++q) dw1[t2][q] = mfma_bf16(d_hm, bx1[q], dw1[t2][q]);
             continue;
@@ -993,13 +1089,14 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? D2D_UPD_WAVES : 1) void
 
   const int stride = a.G * 4;
   const int tile0 = by * 4 + wave;
-  int e0 = 0;
+  int e0 = 0, tslot = 0;
   float R[2][4];
   bf16x8 xh[2][KC];
   uint32_t sm[KC][2];
   record_signs<KC, U8>(sm, a, k, g);
   auto stage = [&](const CriticIn<KC, U8>& src, TileCur c) -> bool {
     e0 = c.e0;
+    tslot = c.t;
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -1075,6 +1172,8 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? D2D_UPD_WAVES : 1) void
           const float v = row_sum16(pv) + c2;
 #endif
           const bool ok = e0 + 16 * s + 4 * g + r < a.E;
+          if (a.vout && i == 0 && ok)  // the value of every sample (d2d_ppo_critic_grad_values)
+            a.vout[(int64_t)tslot * a.v_st[0] + (int64_t)(e0 + 16 * s + 4 * g + r) * a.v_st[1] + (int64_t)k * a.v_st[2]] = v;
           // every lane of the row holds the same sample's v and R: all of them accumulate (no
           // per-lane selects) and the partial keeps lane i = 0's sums (the same values and order)
           const float d = ok ? v - R[s][r] : 0.f;
@@ -1285,17 +1384,6 @@ __device__ __forceinline__ void load_critic_in_t(CriticInT<KC, U8>& in, const Up
   for (int s = 0; s < 2; ++s) in.R[s] = ld_sample(rw, a.w_st, 16 * s + i);
 }
 
-// v_pk_min_u16 / v_pk_mul_lo_u16 (asm: the compiler turns the packed forms into per-half compares + selects)
-__device__ __forceinline__ uint32_t pk_min1_u16(uint32_t x) {
-  uint32_t m;
-  asm("v_pk_min_u16 %0, %1, %2" : "=v"(m) : "v"(x), "s"(0x00010001u));
-  return m;
-}
-__device__ __forceinline__ uint32_t pk_mul_lo_u16(uint32_t a, uint32_t b) {
-  uint32_t o;
-  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(o) : "v"(a), "v"(b));
-  return o;
-}
 
 #ifndef D2D_CRITIC_T_WAVES
 // waves per SIMD the hidden-on-rows critic is register-budgeted for (KC = 1, H <= 64, the record: 168 VGPRs, no
@@ -1379,9 +1467,11 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? (U8 ? D2D_CRITIC_T_WAVE
   record_signs<KC, U8>(sm, a, k, g);
   // inputs: bias column, zeros past it; bf16 high parts to registers (forward B operand) and LDS (dV1 B
   // operand); F32: the fp32 image too (the deferred pass).  Returns whether every input is bf16-exact.
+  int tslot = 0;
   auto stage = [&](const CriticInT<KC, U8>& src, TileCur c, auto f32img) -> bool {
     constexpr bool F32 = decltype(f32img)::value;
     e0 = c.e0;
+    tslot = c.t;
     R[0] = src.R[0];
     R[1] = src.R[1];
     uint32_t low = 0;
@@ -1477,6 +1567,9 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? (U8 ? D2D_CRITIC_T_WAVE
         const float v = group_sum(pv) + c2;
 #endif
         const bool ok = e0 + 16 * s + i < a.E;
+        // the critic's value of every sample (iPPO's deferred rollout values, d2d_ppo_critic_grad_values)
+        if (a.vout && g == 0 && ok)
+          a.vout[(int64_t)tslot * a.v_st[0] + (int64_t)(e0 + 16 * s + i) * a.v_st[1] + (int64_t)k * a.v_st[2]] = v;
         // the four lane groups hold the same sample: all accumulate, the partial keeps group 0's sums
         const float d = ok ? v - R[s] : 0.f;
         dvv[s] = 2.f * a.scale * d;
@@ -1873,21 +1966,41 @@ extern "C" int d2d_ppo_actor_grad(const d2d_mlp_desc* d, int32_t T, const void* 
   return launch_reduce(a, gw1, gb1, gw2, gb2, stats, s);
 }
 
+extern "C" int d2d_ppo_critic_grad_values(const d2d_mlp_desc* d, int32_t T, const void* obs, const float* returns,
+                                          const int64_t* return_strides, float scale, float* gw1, float* gb1,
+                                          float* gw2, float* gb2, float* stats, float* workspace,
+                                          int64_t workspace_floats, float* values, const int64_t* values_strides,
+                                          void* stream);
 extern "C" int d2d_ppo_critic_grad(const d2d_mlp_desc* d, int32_t T, const void* obs, const float* returns,
                                    const int64_t* return_strides, float scale, float* gw1, float* gb1, float* gw2,
                                    float* gb2, float* stats, float* workspace, int64_t workspace_floats,
                                    void* stream) {
+  return d2d_ppo_critic_grad_values(d, T, obs, returns, return_strides, scale, gw1, gb1, gw2, gb2, stats, workspace,
+                                    workspace_floats, nullptr, nullptr, stream);
+}
+
+extern "C" int d2d_ppo_critic_grad_values(const d2d_mlp_desc* d, int32_t T, const void* obs, const float* returns,
+                                          const int64_t* return_strides, float scale, float* gw1, float* gb1,
+                                          float* gw2, float* gb2, float* stats, float* workspace,
+                                          int64_t workspace_floats, float* values, const int64_t* values_strides,
+                                          void* stream) {
   int rc = check_update(d, T, obs, gw1, workspace, workspace_floats, 1);
   if (rc) return rc;
   if (!returns || !return_strides || !gb1 || !gw2 || !gb2) {
     d2d_set_error("d2d_ppo_critic_grad: NULL argument");
     return D2D_EINVAL;
   }
+  if (values && !values_strides) { d2d_set_error("d2d_ppo_critic_grad_values: values without strides"); return D2D_EINVAL; }
   UpdArgs a = make_args(d, T, obs, workspace, 1);
   a.weight = returns;
   for (int q = 0; q < 3; ++q) a.w_st[q] = return_strides[q];
   a.w_ext = tensor_extent(a.w_st, a.T, a.E, a.N);
   if (a.w_ext < 0) { d2d_set_error("negative return strides"); return D2D_EINVAL; }
+  a.vout = values;
+  if (values) {
+    for (int q = 0; q < 3; ++q) a.v_st[q] = values_strides[q];
+    if (tensor_extent(a.v_st, a.T, a.E, a.N) < 0) { d2d_set_error("negative value strides"); return D2D_EINVAL; }
+  }
   a.scale = scale;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (a.N == 0) return D2D_OK;

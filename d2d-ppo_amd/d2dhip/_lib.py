@@ -37,7 +37,7 @@ def refuse_ablation(what):
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 11
+ABI_VERSION = 12
 D2D_OBS_F32, D2D_OBS_U8 = 0, 1
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
@@ -140,6 +140,12 @@ _SIGS = {
                                            ctypes.c_int64, _p]),
     "d2d_ppo_critic_grad": (ctypes.c_int, [ctypes.POINTER(MlpDesc), ctypes.c_int32, _p, _p, _p, ctypes.c_float,
                                             _p, _p, _p, _p, _p, _p, ctypes.c_int64, _p]),
+    "d2d_ppo_critic_grad_values": (ctypes.c_int, [ctypes.POINTER(MlpDesc), ctypes.c_int32, _p, _p, _p, ctypes.c_float,
+                                                   _p, _p, _p, _p, _p, _p, ctypes.c_int64, _p, _p, _p]),
+    "d2d_central_critic_blocks": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int64]),
+    "d2d_central_critic_image_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
+    "d2d_central_critic_fwd": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, _p, _p, _p,
+                                               _p, _p, _p, _p, _p, _p, _p, ctypes.c_int32, _p]),
     "d2d_policy_gru": (ctypes.c_int, [ctypes.POINTER(GruDesc), ctypes.c_int32, _p, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, _p, ctypes.c_uint32, ctypes.c_int32, _p, _p, _p]),
     "d2d_gru_grad_workspace": (ctypes.c_int64, [ctypes.POINTER(GruDesc), ctypes.c_int32]),

@@ -90,8 +90,10 @@ def actor_grads(net, obs, actions, logp_old, weight, kind, clip=0.1, beta=0.01, 
     return grads, stats
 
 
-def critic_grads(net, obs, returns, scale=None, grads=None, stats=None, workspace=None):
+def critic_grads(net, obs, returns, scale=None, grads=None, stats=None, workspace=None, values=None):
     """net: dict w1 [N][H][F], b1 [N][H], w2 [N][1][H], b2 [N][1].  returns [T][E][N] or [N][E*T].
+    values: None, or an fp32 tensor viewed as [T][E][N] (or [N][E*T]) that receives V(obs) of every sample
+    (d2d_ppo_critic_grad_values: iPPO's rollout values from the first epoch's critic pass).
     Returns (grads, stats [N][2] = (sum (V - R)^2, 0))."""
     lib = _lib.require_gpu()
     T, E, N, F = obs.shape
@@ -109,9 +111,13 @@ def critic_grads(net, obs, returns, scale=None, grads=None, stats=None, workspac
     ws = (workspace or _ws).get(need, dev)
     desc = _desc(net, E, 0, critic=True)
     optr = set_format(desc, obs)
-    rc = lib.d2d_ppo_critic_grad(desc, T, optr, returns.data_ptr(), _arr(_strides3(returns, T, E, N)),
-                                 float(scale), grads["w1"].data_ptr(), grads["b1"].data_ptr(),
-                                 grads["w2"].data_ptr(), grads["b2"].data_ptr(), stats.data_ptr(), ws.data_ptr(),
-                                 ws.numel(), _lib.stream_ptr())
-    _lib.check(rc, "d2d_ppo_critic_grad")
+    if values is not None:
+        assert values.dtype == torch.float32 and values.device == dev
+    rc = lib.d2d_ppo_critic_grad_values(desc, T, optr, returns.data_ptr(), _arr(_strides3(returns, T, E, N)),
+                                        float(scale), grads["w1"].data_ptr(), grads["b1"].data_ptr(),
+                                        grads["w2"].data_ptr(), grads["b2"].data_ptr(), stats.data_ptr(),
+                                        ws.data_ptr(), ws.numel(),
+                                        None if values is None else values.data_ptr(),
+                                        None if values is None else _arr(_strides3(values, T, E, N)), _lib.stream_ptr())
+    _lib.check(rc, "d2d_ppo_critic_grad_values")
     return grads, stats

@@ -43,12 +43,12 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 11  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
+#define D2D_ABI_VERSION 12  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
                               6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_states_to_bf16_exact,
                               d2d_critic_dpre_split; 8: d2d_gae_scan_moments, d2d_normalize_pair;
                               9: d2d_gae_scan_moments without outputs, d2d_gae_scan_normalized;
                               10: d2d_states_to_bf16_padded, d2d_critic_dpre_split3;
-                              11: D2D_OPT_CRITIC_GRAD_ROWS */
+                              11: D2D_OPT_CRITIC_GRAD_ROWS; 12: d2d_ppo_critic_grad_values, d2d_central_critic_* */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -340,6 +340,30 @@ int d2d_ppo_actor_grad(const d2d_mlp_desc* desc, int32_t T, const void* obs, con
 int d2d_ppo_critic_grad(const d2d_mlp_desc* desc, int32_t T, const void* obs, const float* returns,
                         const int64_t* return_strides, float scale, float* gw1, float* gb1, float* gw2, float* gb2,
                         float* stats, float* workspace, int64_t workspace_floats, void* stream);
+/* ABI 12: d2d_ppo_critic_grad that also writes the critic's value V(obs) of every sample, element (t, e, k) at
+ * t * values_strides[0] + e * values_strides[1] + k * values_strides[2] (NULL values = d2d_ppo_critic_grad).
+ * Replaces the per-slot critic forward of iPPO.create_rollouts (algorithms/ippo.py:308, the values GAE needs,
+ * ippo.py:337): the critic's weights do not change between the rollout and the first epoch's critic gradient,
+ * so the learners take the rollout's values from that pass instead of from every rollout slot. */
+int d2d_ppo_critic_grad_values(const d2d_mlp_desc* desc, int32_t T, const void* obs, const float* returns,
+                               const int64_t* return_strides, float scale, float* gw1, float* gb1, float* gw2,
+                               float* gb2, float* stats, float* workspace, int64_t workspace_floats, float* values,
+                               const int64_t* values_strides, void* stream);
+
+/* ---- D2D-PPO central critic, forward + the backward's per-sample glue (ABI 12) -------------------------------
+ * The Value network over the whole state (d2d_ppo.py:62-98: linear1 [H][S], relu, linear2 [1][H]) for every sample
+ * b of xb [B][ldx] (the rollout's states as exact bf16 integers, columns [S, ldx) zero, ldx a multiple of 8,
+ * 16-byte aligned): values[b] = V(x_b); against ret [B] (the critic target, returns.mean(1), d2d_ppo.py:339) the
+ * MSE loss's backward through linear2 / relu (d2d_ppo.py:440-446, value_loss.backward()): dpre_b = [pre_b > 0] w2
+ * 2 (v_b - ret_b) / B as its three-way RNE bf16 split in dhm [B][3H] (parts h | m | l; dW1 = sum_b dpre_b x_b^T is
+ * the caller's split-K GEMM), and per-workgroup sums partial [G][2H + 2] = db1 | dW2 | db2 | sum (v - ret)^2.
+ * w1img: d2d_central_critic_image_bytes(H, S) bytes of device scratch (W1's split image, rebuilt by every call);
+ * G = d2d_central_critic_blocks(H, B).  H a multiple of 4 in [4, 128]; else D2D_EUNSUPPORTED. */
+int32_t d2d_central_critic_blocks(int32_t hidden, int64_t B);
+int64_t d2d_central_critic_image_bytes(int32_t hidden, int32_t S);
+int d2d_central_critic_fwd(int32_t hidden, int64_t B, int32_t S, int64_t ldx, const uint16_t* xb, const float* w1,
+                           const float* b1, const float* w2, const float* b2, const float* ret, void* w1img,
+                           float* values, uint16_t* dhm, float* partial, int32_t G, void* stream);
 
 /* ---- GRU window policies (the reference's RNN module, algorithms/ippo.py:14-51 == d2d_ppo.py:24-59) ----
  * Per agent: torch.nn.GRU(F, H) weights w_ih [N][3H][F], w_hh [N][3H][H], b_ih, b_hh [N][3H] (gate order

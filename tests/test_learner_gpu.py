@@ -206,7 +206,7 @@ def test_learner_matches_reference(name, E):
         assert lr._fused_ok() and lr._fused_update_ok()
 
     # --- one training iteration on the same rollout
-    lr._rollout = lambda num_episodes, teacher=None, _ro=ro: _ro
+    lr._rollout = lambda num_episodes, teacher=None, defer_values=False, _ro=ro: _ro
     lr.test = lambda num_episodes: (0.5, 1.0, 0, 0.0)
     np.random.seed(21)
     rec = GradRecorder(lr)
@@ -275,7 +275,7 @@ def _first_step_torch_path(z, E, algo, n_ep, teacher):
         lr.value_network.load_state_dict(_sd(z, "init/critic"))
     lr._fused_upd = False
     ro = lr._rollout(n_ep, teacher=teacher)
-    lr._rollout = lambda num_episodes, teacher=None, _ro=ro: _ro
+    lr._rollout = lambda num_episodes, teacher=None, defer_values=False, _ro=ro: _ro
     lr.test = lambda num_episodes: (0.5, 1.0, 0, 0.0)
     np.random.seed(21)
     rec = GradRecorder(lr)
@@ -455,21 +455,26 @@ def test_rollout_graph_bound_to_its_batch():
     assert ro.E == 4
 
 
-@pytest.mark.parametrize("case", ["comb12", "chsel16", "comb8", "comb16", "comb256", "chsel16-splitfwd"])
+@pytest.mark.parametrize("case", ["comb12", "chsel16", "comb8", "comb16", "comb256", "chsel16-splitfwd",
+                                  "comb256-gemm", "chsel16-gemm", "comb256-h128", "comb8-h32"])
 def test_d2d_central_critic_split_gemm_matches_fp32(case):
-    """The central critic on bf16 split GEMMs (exact bf16 states x three-way split W1; dPre two-way
+    """The central critic on the bf16 state operand (exact bf16 states x three-way split W1; dPre three-way
     split) == torch fp32 autograd of mse(Value(state), returns): values to 1e-5 relative,
     gradients to 2e-5 of their largest entry.  comb256: the configs[4] sweep's widest state
     (S = 15 N + 8 = 3,848 with deadlines 7); chsel16 / comb8 / comb16: the small widths the learners
     now also run on the split path -- configs[1] (S = 16 x 7 + 5 = 117, not a multiple of 8) and the
     sweep's 8 / 16 agents (S = 128 / 248), whose forward runs as one fp32 GEMM below
-    CRITIC_F32_FWD_MAX_DIM (the "-splitfwd" case forces the split forward at S = 117)."""
+    CRITIC_F32_FWD_MAX_DIM (the "-splitfwd" case forces the split forward at S = 117).  Default: the fused HIP
+    forward + backward glue (d2d_central_critic_fwd, hidden 64 / 128 / 32); "-gemm" cases: the round-4 hipBLASLt
+    forward GEMM and dpre split kernel."""
     from algorithms.d2d_ppo import D2DPPO
     from envs.channel_selection_env import ChannelSelectionEnv
     from envs.combinatorial_env import CombinatorialEnv
     C = 8
     comb = case.startswith("comb")
     split_fwd = case.endswith("-splitfwd")
+    gemm = case.endswith("-gemm") or split_fwd  # the round-4 hipBLASLt path (D2DPPO.critic_fused off)
+    hidden = int(case.split("-h")[1]) if "-h" in case else 64
     N = int((case[4:] if comb else case[5:]).split("-")[0])
     if comb:
         dl = np.array([7, 14] * (N // 2)) if N == 12 else np.full(N, 7)
@@ -484,13 +489,15 @@ def test_d2d_central_critic_split_gemm_matches_fp32(case):
                                   channel_switch=np.full(5, 0.8), n_envs=64, device="cuda", seed=4)
         assert env.state_space.shape[0] == 117
     torch.manual_seed(2)
-    lr = D2DPPO(env, hidden_size=64, gamma=0.5, device="cuda", combinatorial=comb, early_stopping=False)
+    lr = D2DPPO(env, hidden_size=hidden, gamma=0.5, device="cuda", combinatorial=comb, early_stopping=False)
     lr.CRITIC_SPLIT_MIN_DIM = 0
+    lr.critic_fused = not gemm
     if split_fwd:
         lr.CRITIC_F32_FWD_MAX_DIM = 0
     ro = lr._rollout(64)
     crit = lr._critic_split_forward(ro)
     assert crit is not None
+    assert (len(crit) == 5) == (not gemm)  # the fused kernel (d2d_central_critic_fwd) unless the case asks for the GEMMs
     loss = lr._critic_split_backward(ro, crit)
     got = {n: p.grad.clone() for n, p in lr.value_network.named_parameters()}
     for p in lr.value_network.parameters():

@@ -406,3 +406,32 @@ def test_grads_on_large_rollout_vs_float64(E):
         checked += 1
     print(f"  worst excess over the envelope: {worst}")
     assert checked == 64 * 8
+
+
+def test_deferred_values_equal_rollout_values():
+    """iPPO training rollouts take their values from the first epoch's critic pass (d2d_ppo_critic_grad_values,
+    iPPO.defer_values): the same V(obs) as the rollout critic's forward (same weights; 1e-5), the same advantages
+    (1e-5), and that epoch's losses (1e-5) and post-Adam weights (2 % of lr) equal those of the epoch on the
+    per-slot values.  The deferred epoch runs the critic first; the two optimizers are independent."""
+    import copy
+    from algorithms.ippo import iPPO
+    (ref, dfr), ro, _ = _learner_pair(iPPO, "comb", E=96, N=6, H=64)
+    assert dfr._defer_values_ok()
+    ro2 = copy.copy(ro)
+    ro2.values = torch.zeros_like(ro.values)
+    ro2.adv_tne = None
+    ro2.values_pending = True
+    pl1, vl1 = ref._update_epoch(ro, None)
+    pl2, vl2 = dfr._update_epoch(ro2, None)
+    torch.testing.assert_close(ro2.values, ro.values, rtol=0, atol=1e-5)
+    torch.testing.assert_close(ro2.adv_tne, ro.adv_tne, rtol=0, atol=1e-5)
+    torch.testing.assert_close(pl2, pl1, rtol=0, atol=1e-5)
+    torch.testing.assert_close(vl2, vl1, rtol=0, atol=1e-5)
+    for net in ("policy", "value"):
+        lr_ = 3e-3 if net == "policy" else 1e-3
+        for k, p in getattr(ref, net).params.items():
+            q = getattr(dfr, net).params[k]
+            assert (p.data - q.data).abs().max().item() <= 0.02 * lr_, (net, k)
+    # a second epoch on the deferred rollout runs the usual order (values are no longer pending)
+    assert not ro2.values_pending
+    dfr._update_epoch(ro2, None)
