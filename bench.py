@@ -233,10 +233,13 @@ def load_pmc_traffic(mode="fp32"):
     return load_profile_json("pmc_traffic.json" if mode == "fp32" else f"pmc_traffic_{mode}.json")
 
 
-def pmc_mfma(kernel_prefix):
-    """PMC-measured MFMA pipe utilisation of a kernel (profiles/pmc_mfma.json, tools/pmc_mfma.py:
-    SQ_VALU_MFMA_BUSY_CYCLES / (kernel cycles x 1024 SIMDs) over rocprofv3 --pmc passes), with its source."""
-    d, rel = load_profile_json("pmc_mfma.json")
+def pmc_mfma(kernel_prefix, leg=None):
+    """PMC-measured MFMA pipe utilisation of a kernel (tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES / (kernel
+    cycles x 1024 SIMDs) over rocprofv3 --pmc passes), with its source.  leg: the per-leg profile
+    profiles/pmc_mfma_<leg>.json (tools/gpu/pmc_legs.sh runs the bench with that leg alone, so every dispatch of
+    the row is one of the leg's launches -- the row's dispatch count is reported beside it); else the mixed
+    profiles/pmc_mfma.json."""
+    d, rel = load_profile_json(f"pmc_mfma_{leg}.json" if leg else "pmc_mfma.json")
     if not d:
         return None
     for k in d.get("kernels", []):
@@ -249,6 +252,7 @@ def pmc_mfma(kernel_prefix):
             # SQ_INSTS_VALU counts the MFMAs too: non-MFMA vector instructions per MFMA
             vpm = (valu - mfma) / mfma if valu is not None and mfma else None
             return {"mfma_busy_frac_pmc": k.get("mfma_busy_frac"), "valu_per_mfma_pmc": vpm,
+                    "wave_time_split": k.get("wave_time_split"), "dispatches": k.get("dispatches", {}).get("SQ_WAVES"),
                     "source": rel, "commit": d.get("commit"), "workload": d.get("workload"),
                     "pmc_kernel": k.get("kernel"), "avg_duration_us": k.get("avg_duration_us")}
     return None
@@ -335,7 +339,7 @@ def rollout_leg(env, args, world):
             "policy_kernel_us": pol_ms * 1e3, "env_kernel_us": env_ms * 1e3,
             "policy_flop_per_agent_step": flop,
             "policy_algorithmic_gflops": flop * b.E * b.spec.N / (pol_ms / 1e3) / 1e9,
-            "policy_mfma_pmc": pmc_mfma("d2d::policy_split_kernel")}
+            "policy_mfma_pmc": pmc_mfma("d2d::policy_split_kernel", "rollout")}
 
 
 def ppo_leg(args, rank, world, local):
@@ -419,7 +423,7 @@ def update_kernel_roofline(lr, ro, F, H, A, reps=4):
                      "algorithmic_gflops": agent_samples * fl / (ms / 1e3) / 1e9,
                      "executed_bf16_tflops": executed, "executed_over_bf16_dense_peak": executed / BF16_PEAK_TFLOPS,
                      "mfma_cycles_per_tile": pipe[name], "mfma_pipe_busy_frac_static": busy,
-                     "mfma_pmc": pmc_mfma(f"d2d::ppo_{name}_grad_kernel"), "bound": "mfma"}
+                     "mfma_pmc": pmc_mfma(f"d2d::ppo_{name}_grad_kernel", "ppo"), "bound": "mfma"}
     return res
 
 
@@ -751,6 +755,11 @@ def gru_leg(args, rank, world, local):
     pol_pipe = pol_tiles * (L * 12 * (3 + 2 * 6) * 16 + 80 * 32) / (1024 * 2.4e9) / (pol_ms / 1e3)
     del buf, lr, env, b
     torch.cuda.empty_cache()
+    slot_out = {"envs_per_gpu": E, "window": L, "ms": pol_ms, "agent_steps_per_s": E * world * N / (pol_ms / 1e3),
+                "env_steps_per_s": E * world / (pol_ms / 1e3), "flop": pol_flop,
+                "algorithmic_gflops": pol_flop / (pol_ms / 1e3) / 1e9, "mfma_pipe_busy_frac_static": pol_pipe}
+    if args.gru_slot_only:
+        return {"policy_slot": slot_out}
     # (2) + (3) at --gru-envs envs
     E2 = args.gru_envs
     env = CombinatorialEnv(**params, n_envs=E2, device=dev, seed=52)
@@ -795,7 +804,7 @@ def gru_leg(args, rank, world, local):
                            "ms": pol_ms, "agent_steps_per_s": E * world * N / (pol_ms / 1e3),
                            "env_steps_per_s": E * world / (pol_ms / 1e3),
                            "flop": pol_flop, "algorithmic_gflops": pol_flop / (pol_ms / 1e3) / 1e9,
-                           "mfma_pipe_busy_frac_static": pol_pipe, "mfma_pmc": pmc_mfma("d2d::gru_policy_kernel"),
+                           "mfma_pipe_busy_frac_static": pol_pipe, "mfma_pmc": pmc_mfma("d2d::gru_policy_kernel", "gru_slot"),
                            "bound": "mfma"},
            "update": {"envs_per_gpu": E2, "slots": ro.T, "agent_samples": samples,
                       "kernel": (f"d2d::gru_grad_kernel<4, {it_}, 0, true, true, {'true' if L > 64 else 'false'}>" if it_ <= 3
@@ -807,7 +816,7 @@ def gru_leg(args, rank, world, local):
                       # no headroom figure (it is not bounded by the fp32 MFMA peak) -- the executed pipe's
                       # utilisation is mfma_pmc.mfma_busy_frac_pmc; the algorithmic rate is in GFLOP/s
                       "algorithmic_gflops": grad_flop / (grad_ms / 1e3) / 1e9,
-                      "mfma_pmc": pmc_mfma("d2d::gru_grad_kernel")},
+                      "mfma_pmc": pmc_mfma("d2d::gru_grad_kernel", "gru")},
            "d2d_iteration_s": it_s, "d2d_iteration_envs_per_gpu": E2, "n_epoch": 5,
            "d2d_env_steps_per_s_end_to_end": E2 * world * ro.T / it_s,
            "flop_per_agent_step_cell": cell}
@@ -889,6 +898,7 @@ def main():
     ap.add_argument("--gru-c5-envs", type=int, default=4096, help="envs per GPU of the c5 GRU leg")
     ap.add_argument("--gru-c5-agents", default="64,128,256", help="agent counts of the c5 GRU leg")
     ap.add_argument("--gru-envs", type=int, default=256, help="envs per GPU in the GRU update / iteration")
+    ap.add_argument("--gru-slot-only", action="store_true", help="gru leg: the 65,536-env policy slot only (PMC passes)")
     ap.add_argument("--rollout-steps", type=int, default=60)
     ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
     ap.add_argument("--ppo-epochs", type=int, default=6)

@@ -323,11 +323,14 @@ class D2DPPO(BatchedLearnerBase):
                 _lib.check(lib.d2d_states_to_bf16_padded(T_, E_, S, st.shape[2], st.data_ptr(), xb.data_ptr(), S8,
                                                          flag.data_ptr(), _lib.stream_ptr()), "d2d_states_to_bf16_padded")
             else:
+                # the env-major fp32 copy exists (a consumer asked for it): the same padded operand from it (as one
+                # "slot" of B rows)
                 sq = ro.state_seq.contiguous()
-                xb = torch.empty(sq.shape, dtype=torch.bfloat16, device=sq.device)
+                S8 = -(-S // 8) * 8
+                xb = torch.empty((sq.shape[0], S8), dtype=torch.bfloat16, device=sq.device)
                 flag = torch.empty(1, dtype=torch.int32, device=sq.device)
-                _lib.check(lib.d2d_f32_to_bf16_exact(sq.numel(), sq.data_ptr(), xb.data_ptr(), flag.data_ptr(),
-                                                     _lib.stream_ptr()), "d2d_f32_to_bf16_exact")
+                _lib.check(lib.d2d_states_to_bf16_padded(1, sq.shape[0], S, sq.shape[1], sq.data_ptr(), xb.data_ptr(), S8,
+                                                         flag.data_ptr(), _lib.stream_ptr()), "d2d_states_to_bf16_padded")
             if int(flag.item()) != 0:
                 self.critic_split = False  # fractional / large states: keep torch fp32
                 return None

@@ -183,9 +183,13 @@ class iPPO(BatchedLearnerBase):
         self._phase("rollout")
         if defer:
             s = self.env.batch().spec
-            ro.values = torch.zeros((ro.T, s.N, ro.E), dtype=torch.float32, device=self.device)
-            # the returns (discount_rewards, ippo.py:338) read no value: they are the critic pass's targets
-            _, ro.ret_tne = self._gae(ro.rewards, ro.values, ro.dones, normalize_adv=False, layout="tce")
+            ro.values = torch.empty((ro.T, s.N, ro.E), dtype=torch.float32, device=self.device)
+            # the returns (discount_rewards, ippo.py:338) read no value: they are the critic pass's targets.  Every
+            # agent gets the same reward (the envs broadcast |S| / the ACK), so the N normalised return columns are
+            # identical: one column, viewed over the agents with stride 0
+            zero = torch.zeros((ro.T, 1, ro.E), dtype=torch.float32, device=self.device)
+            _, ret1 = self._gae(ro.rewards, zero, ro.dones, normalize_adv=False, layout="tce")
+            ro.ret_tne = ret1.expand(ro.T, s.N, ro.E)
             ro.adv_tne = None
             ro.values_pending = True
         else:

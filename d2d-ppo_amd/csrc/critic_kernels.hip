@@ -19,7 +19,7 @@
 // 16 st + i, features 32c + 8g .. + 7 as its B fragment (one 16-byte load, prefetched one chunk ahead); W1's exact
 // three-way split (truncation parts, mlp_common.h split3: the products are exact, x is an integer) arrives as a
 // per-chunk image of A fragments [t][part][lane] (built once per epoch by critic_w1_image_kernel), staged through
-// a double-buffered LDS slice shared by the workgroup's four waves (one barrier per chunk).  The accumulator
+// a double-buffered LDS slice shared by the workgroup's four waves (one barrier per KCH chunks).  The accumulator
 // (hidden 16t + 4g + r on rows, sample on lanes) is the actor kernels' forward orientation: the 64 -> 1 head is a
 // per-lane fma over the lane's hidden units plus a sum over the four lane groups.
 #include <algorithm>
@@ -70,10 +70,12 @@ __device__ __forceinline__ uint32_t rne_pk(float a, float b) {
 __device__ __forceinline__ float bf_lo(uint32_t p) { return __uint_as_float(p << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
 
-template <int HT, int ST>
+// KCH chunks of 32 features per iteration (one barrier per iteration; the operand loads of the next iteration in
+// flight behind this one's 48 KCH MFMAs per wave: at KCH = 1 the kernel read the 6.3 GB operand at ~3 TB/s)
+template <int HT, int ST, int KCH>
 __global__ __launch_bounds__(256, 2) void critic_fwd_kernel(CriticArgs a) {
   constexpr int NI = HT * 3 * 64;  // 16-byte image entries per chunk
-  __shared__ __attribute__((aligned(16))) bf16x8 wl[2][NI];
+  __shared__ __attribute__((aligned(16))) bf16x8 wl[2][KCH * NI];
   __shared__ float red[4][2 * 16 * HT + 2];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -87,18 +89,21 @@ __global__ __launch_bounds__(256, 2) void critic_fwd_kernel(CriticArgs a) {
   uint32_t vo[ST];
 #pragma unroll
   for (int st = 0; st < ST; ++st) vo[st] = (uint32_t)(((int64_t)(16 * st + i) * a.ldx + 8 * g) * 2);
-  auto load_x = [&](bf16x8 (&x)[ST], int c) {
+  auto load_x = [&](bf16x8 (&x)[KCH][ST], int it) {
 #pragma unroll
-    for (int st = 0; st < ST; ++st)
-      x[st] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, vo[st] + 64u * (uint32_t)c, 0, 0));
+    for (int q = 0; q < KCH; ++q)
+#pragma unroll
+      for (int st = 0; st < ST; ++st)
+        x[q][st] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  xr, vo[st] + 64u * (uint32_t)(KCH * it + q), 0, 0));
   };
-  constexpr int NW = (NI + 255) / 256;  // image entries per thread and chunk
+  constexpr int NE = KCH * NI, NW = (NE + 255) / 256;  // image entries per iteration, per thread
   bf16x8 wr[NW];
-  auto load_w = [&](int c) {
+  auto load_w = [&](int it) {
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
       const int e = tid + 256 * q;
-      if (NI % 256 == 0 || e < NI) wr[q] = a.w1img[(size_t)c * NI + e];
+      if (NE % 256 == 0 || e < NE) wr[q] = a.w1img[(size_t)it * NE + e];
     }
   };
   f32x4 acc[ST][HT];
@@ -107,34 +112,39 @@ __global__ __launch_bounds__(256, 2) void critic_fwd_kernel(CriticArgs a) {
 #pragma unroll
     for (int t = 0; t < HT; ++t) acc[st][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  bf16x8 xc[ST], xn[ST];
+  const int iters = a.nchunk / KCH;  // (nchunk is padded to a multiple of KCH; the image is zero there)
+  bf16x8 xc[KCH][ST], xn[KCH][ST];
   load_w(0);
   load_x(xc, 0);
-  for (int c = 0; c < a.nchunk; ++c) {
-    // buffer c & 1 was last read in iteration c - 2: every wave passed iteration c - 1's barrier since
+  for (int it = 0; it < iters; ++it) {
+    // buffer it & 1 was last read in iteration it - 2: every wave passed iteration it - 1's barrier since
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
       const int e = tid + 256 * q;
-      if (NI % 256 == 0 || e < NI) wl[c & 1][e] = wr[q];
+      if (NE % 256 == 0 || e < NE) wl[it & 1][e] = wr[q];
     }
-    if (c + 1 < a.nchunk) {
-      load_w(c + 1);
-      load_x(xn, c + 1);
+    if (it + 1 < iters) {
+      load_w(it + 1);
+      load_x(xn, it + 1);
     }
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < HT; ++t) {
-      const bf16x8 ah = wl[c & 1][(t * 3 + 0) * 64 + lane], am = wl[c & 1][(t * 3 + 1) * 64 + lane],
-                   al = wl[c & 1][(t * 3 + 2) * 64 + lane];
+    for (int q = 0; q < KCH; ++q)
 #pragma unroll
-      for (int st = 0; st < ST; ++st) {
-        acc[st][t] = mfma_bf16(al, xc[st], acc[st][t]);
-        acc[st][t] = mfma_bf16(am, xc[st], acc[st][t]);
-        acc[st][t] = mfma_bf16(ah, xc[st], acc[st][t]);
+      for (int t = 0; t < HT; ++t) {
+        const bf16x8* w = &wl[it & 1][q * NI + (t * 3) * 64 + lane];
+        const bf16x8 ah = w[0], am = w[64], al = w[128];
+#pragma unroll
+        for (int st = 0; st < ST; ++st) {
+          acc[st][t] = mfma_bf16(al, xc[q][st], acc[st][t]);
+          acc[st][t] = mfma_bf16(am, xc[q][st], acc[st][t]);
+          acc[st][t] = mfma_bf16(ah, xc[q][st], acc[st][t]);
+        }
       }
-    }
 #pragma unroll
-    for (int st = 0; st < ST; ++st) xc[st] = xn[st];
+    for (int q = 0; q < KCH; ++q)
+#pragma unroll
+      for (int st = 0; st < ST; ++st) xc[q][st] = xn[q][st];
   }
 
   // ---- epilogue: bias, relu, value, dv, dpre's split; the lane's sums over its samples
@@ -233,6 +243,8 @@ using namespace d2d;
 
 static int critic_ht(int H) { return H <= 32 ? 2 : H <= 64 ? 4 : H <= 128 ? 8 : 0; }
 static int critic_st(int ht) { return ht <= 4 ? 4 : 2; }
+static int critic_kch(int ht) { return ht <= 4 ? 2 : 1; }  // chunks per iteration (LDS: 2 x KCH x 12 HT/4 KB)
+static int critic_chunks(int ht, int S) { const int k = critic_kch(ht); return ((S + 31) / 32 + k - 1) / k * k; }
 
 extern "C" int32_t d2d_central_critic_blocks(int32_t H, int64_t B) {
   const int ht = critic_ht(H);
@@ -244,7 +256,7 @@ extern "C" int32_t d2d_central_critic_blocks(int32_t H, int64_t B) {
 extern "C" int64_t d2d_central_critic_image_bytes(int32_t H, int32_t S) {
   const int ht = critic_ht(H);
   if (ht == 0 || S < 1) return 0;
-  return (int64_t)((S + 31) / 32) * ht * 3 * 64 * 16;
+  return (int64_t)critic_chunks(ht, S) * ht * 3 * 64 * 16;
 }
 
 extern "C" int d2d_central_critic_fwd(int32_t H, int64_t B, int32_t S, int64_t ldx, const uint16_t* xb, const float* w1,
@@ -263,7 +275,7 @@ extern "C" int d2d_central_critic_fwd(int32_t H, int64_t B, int32_t S, int64_t l
   if (B == 0) return D2D_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   CriticArgs a{};
-  a.H = H; a.S = S; a.nchunk = (S + 31) / 32; a.B = B; a.ldx = ldx; a.xb = xb;
+  a.H = H; a.S = S; a.nchunk = critic_chunks(ht, S); a.B = B; a.ldx = ldx; a.xb = xb;
   a.w1img = reinterpret_cast<const bf16x8*>(w1img);
   a.b1 = b1; a.w2 = w2; a.b2 = b2; a.ret = ret; a.two_over_B = 2.f / (float)B;
   a.values = values; a.dhm = dhm; a.partial = partial;
@@ -272,13 +284,13 @@ extern "C" int d2d_central_critic_fwd(int32_t H, int64_t B, int32_t S, int64_t l
   bf16x8* img = reinterpret_cast<bf16x8*>(w1img);
   if (ht == 2) {
     hipLaunchKernelGGL(critic_w1_image_kernel<2>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
-    hipLaunchKernelGGL((critic_fwd_kernel<2, 4>), dim3(G), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((critic_fwd_kernel<2, 4, 2>), dim3(G), dim3(256), 0, s, a);
   } else if (ht == 4) {
     hipLaunchKernelGGL(critic_w1_image_kernel<4>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
-    hipLaunchKernelGGL((critic_fwd_kernel<4, 4>), dim3(G), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((critic_fwd_kernel<4, 4, 2>), dim3(G), dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL(critic_w1_image_kernel<8>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
-    hipLaunchKernelGGL((critic_fwd_kernel<8, 2>), dim3(G), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((critic_fwd_kernel<8, 2, 1>), dim3(G), dim3(256), 0, s, a);
   }
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;

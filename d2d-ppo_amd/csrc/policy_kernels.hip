@@ -188,6 +188,12 @@ __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* 
 // (r04i, two boxes' runs each) -- no gain, off
 #define D2D_POLICY_RNG_EARLY 0
 #endif
+#ifndef D2D_POLICY_ABLATE_NOREAD
+// != 0 only in tools/gpu/build_fusion_bound.sh's timing variant: every obs DMA aimed outside the buffer (zeros, no
+// memory traffic) -- the policy kernel without its read of the slot's record, i.e. what fusing the env step into
+// it could save at most (tools/gpu/fusion_bound.py)
+#define D2D_POLICY_ABLATE_NOREAD 0
+#endif
 #ifndef D2D_POLICY_L2_F32
 // 1 (A/B): actor layer 2 on v_mfma_f32_16x16x4_f32 straight from relu(H^T) (an exact fmaf chain, 16 MFMAs
 // of 32 cycles per tile) instead of the three-way split of relu(H^T) (88 VALU per tile) and 6 bf16 MFMAs
@@ -318,7 +324,8 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
   auto issue = [&](int t) {
     // look-ahead tiles past this wave's last are still issued (the counted waits need a fixed
     // DMA count) but aimed outside the descriptor's range: no memory traffic, zeros
-    const uint32_t vo = t < tiles ? (uint32_t)((t * 16 + i) * N * RB) + (U8 ? 8 : 32) * g : 0x80000000u;
+    const uint32_t vo = (t < tiles && !D2D_POLICY_ABLATE_NOREAD) ? (uint32_t)((t * 16 + i) * N * RB) + (U8 ? 8 : 32) * g
+                                                                   : 0x80000000u;
 #pragma unroll
     for (int c = 0; c < KC; ++c)
 #pragma unroll

@@ -456,11 +456,12 @@ def test_rollout_graph_bound_to_its_batch():
 
 
 @pytest.mark.parametrize("case", ["comb12", "chsel16", "comb8", "comb16", "comb256", "chsel16-splitfwd",
-                                  "comb256-gemm", "chsel16-gemm", "comb256-h128", "comb8-h32"])
+                                  "comb256-gemm", "chsel16-gemm", "comb256-h128", "comb256-h128-gemm", "comb8-h32"])
 def test_d2d_central_critic_split_gemm_matches_fp32(case):
     """The central critic on the bf16 state operand (exact bf16 states x three-way split W1; dPre three-way
-    split) == torch fp32 autograd of mse(Value(state), returns): values to 1e-5 relative,
-    gradients to 2e-5 of their largest entry.  comb256: the configs[4] sweep's widest state
+    split) == torch fp32 autograd of mse(Value(state), returns): values to 1e-5 relative; gradients against
+    float64 autograd to 2e-5 of their largest entry, or 4x torch fp32's own distance from float64 where that is
+    larger (relu-mask flips).  comb256: the configs[4] sweep's widest state
     (S = 15 N + 8 = 3,848 with deadlines 7); chsel16 / comb8 / comb16: the small widths the learners
     now also run on the split path -- configs[1] (S = 16 x 7 + 5 = 117, not a multiple of 8) and the
     sweep's 8 / 16 agents (S = 128 / 248), whose forward runs as one fp32 GEMM below
@@ -474,7 +475,7 @@ def test_d2d_central_critic_split_gemm_matches_fp32(case):
     comb = case.startswith("comb")
     split_fwd = case.endswith("-splitfwd")
     gemm = case.endswith("-gemm") or split_fwd  # the round-4 hipBLASLt path (D2DPPO.critic_fused off)
-    hidden = int(case.split("-h")[1]) if "-h" in case else 64
+    hidden = int(case.split("-h")[1].split("-")[0]) if "-h" in case else 64
     N = int((case[4:] if comb else case[5:]).split("-")[0])
     if comb:
         dl = np.array([7, 14] * (N // 2)) if N == 12 else np.full(N, 7)
@@ -507,7 +508,21 @@ def test_d2d_central_critic_split_gemm_matches_fp32(case):
     ref_loss.backward()
     torch.testing.assert_close(crit[0], v.detach(), rtol=1e-5, atol=1e-5)
     assert abs(loss.item() - ref_loss.item()) <= 1e-5 * abs(ref_loss.item()) + 1e-7
+    # float64 autograd of the same loss: the bar is 2e-5 of max|g| or, where torch fp32 itself is further from
+    # float64 (relu masks of pre-activations within fp32 rounding of 0 -- identical integer states repeat them over
+    # many samples, see tests/test_update_gpu.py's flip envelope), 4x torch fp32's own distance
+    import copy
+    net64 = copy.deepcopy(lr.value_network).double()
+    for p in net64.parameters():
+        p.grad = None
+    v64 = net64(ro.state_seq.double()).squeeze()
+    torch.nn.functional.mse_loss(v64, ro.ret_mean.double()).backward()
+    g64 = dict(net64.named_parameters())
+    errs = {}
     for n, p in lr.value_network.named_parameters():
-        scale = p.grad.abs().max().item()
-        err = (got[n] - p.grad).abs().max().item()
-        assert err <= 2e-5 * scale + 1e-8, (n, err, scale)
+        r = g64[n].grad
+        scale = r.abs().max().item()
+        errs[n] = ((got[n].double() - r).abs().max().item(), (p.grad.double() - r).abs().max().item(), scale)
+    print(f"  {case}: " + ", ".join(f"{n} {e:.2e} (torch fp32 {b:.2e}) of {sc:.2e}" for n, (e, b, sc) in errs.items()))
+    for n, (err, band, scale) in errs.items():
+        assert err <= max(2e-5 * scale, 4 * band) + 1e-8, (n, err, band, scale)

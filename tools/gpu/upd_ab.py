@@ -2,7 +2,7 @@
 F = 30, H = 64 (or argv[2]), at E envs x 200 slots (argv[1], default 2,048): the actor kernel, and the critic on the
 hidden-on-rows kernel (default) vs the sample-on-rows kernel of rounds 2-4 (D2D_OPT_CRITIC_GRAD_ROWS = 1), with the
 two critics' gradient difference relative to max|g| (fp32 rounding only).
-usage (GPU box): python3 tools/gpu/upd_ab.py [E] [H] [reps]"""
+usage (GPU box): python3 tools/gpu/upd_ab.py [E] [H] [reps] [real]"""
 import json
 import os
 import sys
@@ -49,7 +49,19 @@ def main():
         torch.cuda.synchronize()
         return ev[0].elapsed_time(ev[1]) / reps
 
-    res = {"E": E, "T": T, "N": N, "F": F, "H": H, "agent_samples": T * E * N}
+    if "real" in sys.argv[4:]:  # a real iPPO rollout of the bench's c3 config instead of random inputs
+        import bench
+        from algorithms.ippo import iPPO
+        from envs.combinatorial_env import CombinatorialEnv
+        env = CombinatorialEnv(**bench.config3_params(200), n_envs=E, device="cuda:0", seed=7)
+        torch.manual_seed(1)
+        lr = iPPO(env, hidden_size=H, gamma=0.6, policy_lr=3e-4, value_lr=1e-3, device="cuda:0", combinatorial=True)
+        ro = lr._rollout(E)
+        net = {k: v.data for k, v in lr.policy.params.items()}
+        vnet = {k: v.data for k, v in lr.value.params.items()}
+        rec, acts = ro.obs, ro.actions
+        lo, W, R = ro.logp.permute(0, 2, 1), ro.adv_tne.permute(0, 2, 1), ro.ret_tne.permute(0, 2, 1)
+    res = {"E": E, "T": T, "N": N, "F": F, "H": H, "agent_samples": T * E * N, "inputs": "real" if "real" in sys.argv[4:] else "random"}
     res["actor_ms"] = timed(lambda: actor_grads(net, rec, acts, lo, W, "comb"))
     grads = {}
     for name, opt in (("critic_t", 0), ("critic_rows", 1)):
