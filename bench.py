@@ -850,9 +850,13 @@ def gru_c5_leg(args, rank, world, local):
                     useRNN=True, combinatorial=True, history_len=N, early_stopping=False)
         gru_ok = bool(lr._gru_ok())
         # warm-up: one rollout and one epoch (kernel loads, hipBLASLt heuristics, allocator growth)
+        tw = time.perf_counter()
         ro = lr._rollout(E)
         lr._update_epoch(ro, lr._update_state(ro))
         torch.cuda.synchronize()
+        if rank == 0:
+            print(f"[bench gru_c5] N={N} E={E}: warm-up rollout + epoch {time.perf_counter() - tw:.1f} s",
+                  file=sys.stderr, flush=True)
         barrier(world)
         t0 = time.perf_counter()
         ro = lr._rollout(E)
@@ -866,6 +870,9 @@ def gru_c5_leg(args, rank, world, local):
         torch.cuda.synchronize()
         t3 = time.perf_counter()
         barrier(world)
+        if rank == 0:
+            print(f"[bench gru_c5] N={N}: rollout {t1 - t0:.2f} s, epochs {t2 - t1:.2f} / {t3 - t2:.2f} s",
+                  file=sys.stderr, flush=True)
         roll = max_over_ranks(t1 - t0, world)
         ep1 = max_over_ranks(t2 - t1, world)
         ep = max_over_ranks(t3 - t2, world)
@@ -895,7 +902,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--legs", default="env,rollout,ppo,train,configs,d2denv,gru,gru_c5")
-    ap.add_argument("--gru-c5-envs", type=int, default=4096, help="envs per GPU of the c5 GRU leg")
+    ap.add_argument("--gru-c5-envs", type=int, default=512,
+                    help="envs per GPU of the c5 GRU leg (512 x 256 agents = 131,072 GRU windows per slot fill the "
+                         "chip; the O(L H^2) BPTT at L = 256 makes a 4,096-env epoch minutes long)")
     ap.add_argument("--gru-c5-agents", default="64,128,256", help="agent counts of the c5 GRU leg")
     ap.add_argument("--gru-envs", type=int, default=256, help="envs per GPU in the GRU update / iteration")
     ap.add_argument("--gru-slot-only", action="store_true", help="gru leg: the 65,536-env policy slot only (PMC passes)")

@@ -45,9 +45,14 @@ class Rollout:
     def __getattr__(self, name):
         if name == "state_seq" and "state_dim" in self.__dict__:
             # env-major fp32 states [E*T][S] (d2d_ppo.py's rollout states), copied from the slot-major
-            # buffer only when a consumer asks (the bf16 central critic reads the buffer directly)
-            st = self.__dict__["states"]
-            v = st[:, :, : self.__dict__["state_dim"]].transpose(0, 1).reshape(st.shape[0] * st.shape[1], -1)
+            # buffer only when a consumer asks (the bf16 central critic reads the buffer directly); from the env
+            # kernel's bf16 rows (exact integers) when the rollout kept no fp32 copy
+            st = self.__dict__.get("states")
+            S = self.__dict__["state_dim"]
+            if st is None:
+                v = self.__dict__["state_bf16"][:, :S].float()
+            else:
+                v = st[:, :, :S].transpose(0, 1).reshape(st.shape[0] * st.shape[1], -1)
             self.__dict__[name] = v
             return v
         if name == "obs_f32":
@@ -366,7 +371,12 @@ class BatchedLearnerBase(DataParallelMixin):
                     logp=torch.empty((T, s.N, E), dtype=torch.float32, device=dev),
                     rew=torch.empty((T, E), dtype=torch.int32, device=dev),
                     val=torch.empty((T, s.N, E), dtype=torch.float32, device=dev) if want_values else None,
-                    state=torch.empty((T, E, s.state_stride), dtype=torch.float32, device=dev) if want_state else None,
+                    state=(torch.empty((T, E, s.state_stride), dtype=torch.float32, device=dev)
+                           if want_state and want_state != "bf16" else None),
+                    # want_state "bf16": the env kernel's exact bf16 rows, env-major [E][T][S8] (the D2D central
+                    # critic's operand as it is, no fp32 copy and no conversion pass)
+                    state_b=(torch.empty((E, T, -(-s.S // 8) * 8), dtype=torch.bfloat16, device=dev)
+                             if want_state == "bf16" else None),
                     recv=f64(), disc=f64(), eprew=f64(), jains=f64(), ch=f64())
 
     def _waves(self, bufs, b, waves, train, tf):
@@ -375,24 +385,29 @@ class BatchedLearnerBase(DataParallelMixin):
         env, s = self.env, b.spec
         L = env.episode_length
         obs_buf, act_buf, logp_buf, rew_i32 = bufs["obs"], bufs["act"], bufs["logp"], bufs["rew"]
-        val_buf, state_buf = bufs["val"], bufs["state"]
-        want_state = state_buf is not None
+        val_buf, state_buf, state_b = bufs["val"], bufs["state"], bufs["state_b"]
+        want_state = state_buf is not None or state_b is not None
         s.arrival_kinds()  # the reference's reset-time validation (ValueError / AssertionError)
         with torch.no_grad():
             for w in range(waves):
                 t0 = w * L
-                b.reset(want_obs=True, want_state=want_state, out_obs=obs_buf[t0],
-                        out_state=state_buf[t0] if want_state else None,
-                        replay_arrivals=None if tf is None else tf["reset_arrivals"][w])
-                for t in range(L):
+                b.reset(want_obs=True, want_state=state_buf is not None, out_obs=obs_buf[t0],
+                        out_state=state_buf[t0] if state_buf is not None else None,
+                        replay_arrivals=None if tf is None else tf["reset_arrivals"][w],
+                        out_state_bf16=None if state_b is None else state_b[:, t0])
+                fused = self._fused_slot_ok(b, obs_buf, val_buf, want_state, tf)
+                if fused:
+                    self._fused_slots(b, obs_buf, act_buf, logp_buf, rew_i32, t0, L, train)
+                for t in range(0 if fused else L):
                     i = t0 + t
                     act = self._policy_slot(obs_buf, t0, i, train, act_buf[i], logp_buf[i],
                                             val_buf[i] if val_buf is not None else None, tf, b)
                     last = t + 1 == L
-                    b.step(act, want_obs=not last, want_state=want_state and not last,
+                    b.step(act, want_obs=not last, want_state=state_buf is not None and not last,
                            out_obs=None if last else obs_buf[i + 1],
-                           out_state=None if (last or not want_state) else state_buf[i + 1],
-                           out_reward=rew_i32[i], replay=None if tf is None else tf["replay"][i])
+                           out_state=None if (last or state_buf is None) else state_buf[i + 1],
+                           out_reward=rew_i32[i], replay=None if tf is None else tf["replay"][i],
+                           out_state_bf16=None if (last or state_b is None) else state_b[:, i + 1])
                 env.timestep = b.timestep
                 bufs["recv"][w].copy_(b.received.sum(1))
                 bufs["disc"][w].copy_(b.discarded.sum(1))
@@ -401,6 +416,33 @@ class BatchedLearnerBase(DataParallelMixin):
                     bufs["jains"][w].copy_(self._jains_dev(b))
                     if s.kind == "single":  # D2DEnv.channel_errors of the episode (env.py:144-145)
                         bufs["ch"][w].copy_(b.sel_quality)
+
+    # ------------------------------------------ fused env + policy slots
+    fused_slot = os.environ.get("D2D_FUSED_SLOT", "0") == "1"
+
+    def _fused_slot_ok(self, b, obs_buf, val_buf, want_state, tf):
+        """D2D_FUSED_SLOT=1 (A/B, off by default: tools/gpu/fused_slot.py): the slots of a wave as
+        one launch each of the env step fused with the next slot's policy (d2d_comb_policy_fused_step), where
+        the prototype covers the rollout: the MLP actor alone (no per-slot values, no states, no teacher) on
+        the record of the combinatorial env with 64 agents x 8 channels, hidden <= 64."""
+        s = b.spec
+        return (self.fused_slot and tf is None and val_buf is None and not want_state
+                and isinstance(obs_buf, ObsRecord) and not self.useRNN and self._fused_ok()
+                and self.kind == "comb" and bool(self.combinatorial) and s.N == 64 and s.C == 8
+                and _lib_record_bytes(s.F) == 32 and self.policy.H <= 64)
+
+    def _fused_slots(self, b, obs_buf, act_buf, logp_buf, rew_i32, t0, L, train):
+        """Slot t0 on the policy kernel, then L - 1 fused (env step t, policy t + 1) launches, then the last
+        env step: the launches and Philox counters of the two-kernel loop, bit-identical results."""
+        self._policy_slot(obs_buf, t0, t0, train, act_buf[t0], logp_buf[t0], None, None, b)
+        desc = self._mlp_desc(b.E, b.desc.env_base, critic=False)
+        desc.rng_offset = b.rng_off.data_ptr()
+        set_format(desc, obs_buf[t0])
+        for t in range(L - 1):
+            i = t0 + t
+            b.step_policy_fused(act_buf[i], obs_buf[i + 1], rew_i32[i], desc, not train, act_buf[i + 1],
+                                logp_buf[i + 1])
+        b.step(act_buf[t0 + L - 1], want_obs=False, out_reward=rew_i32[t0 + L - 1])
 
     def _rollout_result(self, bufs, b, waves, train):
         L = self.env.episode_length
@@ -415,9 +457,13 @@ class BatchedLearnerBase(DataParallelMixin):
         ch_errors = em(bufs["ch"]).cpu().tolist() if (not train and b.spec.kind == "single") else []
         dones = torch.zeros(T, dtype=torch.uint8, device=self.device)
         dones[L - 1::L] = 1
-        return Rollout(obs=bufs["obs"], actions=bufs["act"], logp=bufs["logp"], rewards=bufs["rew"].float(),
-                       values=bufs["val"], states=bufs["state"], dones=dones, scores=scores, ep_rewards=ep_rewards,
-                       jains=jains, ch_errors=ch_errors, T=T, E=b.E, waves=waves, L=L)
+        ro = Rollout(obs=bufs["obs"], actions=bufs["act"], logp=bufs["logp"], rewards=bufs["rew"].float(),
+                     values=bufs["val"], states=bufs["state"], dones=dones, scores=scores, ep_rewards=ep_rewards,
+                     jains=jains, ch_errors=ch_errors, T=T, E=b.E, waves=waves, L=L)
+        if bufs["state_b"] is not None:
+            sb = bufs["state_b"]
+            ro.state_bf16 = sb.view(sb.shape[0] * sb.shape[1], sb.shape[2])  # [E*T][S8], env-major samples
+        return ro
 
     # ------------------------------------------------------- HIP-graph rollout
     graph_rollout = os.environ.get("D2D_GRAPH_ROLLOUT", "1") != "0"
@@ -439,7 +485,8 @@ class BatchedLearnerBase(DataParallelMixin):
         row = _lib_record_bytes(s.F) if self._record_ok() else 4 * s.F
         act = b.action_buffer().element_size()
         per_slot_agent = row + act + 4 + (4 if want_values else 0)
-        per_slot_env = s.N * per_slot_agent + 4 + (4 * s.state_stride if want_state else 0)
+        state_row = (2 * (-(-s.S // 8) * 8) if want_state == "bf16" else 4 * s.state_stride) if want_state else 0
+        per_slot_env = s.N * per_slot_agent + 4 + state_row
         return T * b.E * per_slot_env <= self.GRAPH_ROLLOUT_MAX_BYTES
 
     def _collect_graph(self, b, waves, want_values, want_state):
@@ -452,7 +499,7 @@ class BatchedLearnerBase(DataParallelMixin):
         # the graph bakes in the env batch's state buffers and the stacked parameters' addresses; the
         # entry holds the batch itself (so its buffers outlive the graph) and must be THIS batch — a
         # new batch could reuse a freed one's id()
-        key = (id(b), b.E, L, waves, bool(want_values), bool(want_state),
+        key = (id(b), b.E, L, waves, bool(want_values), want_state or False,
                tuple(t.data_ptr() for t in self.policy.params.values()),
                tuple(t.data_ptr() for t in getattr(self.value, "params", {}).values()) if hasattr(self, "value") else ())
         cache = self.__dict__.setdefault("_rollout_graphs", {})

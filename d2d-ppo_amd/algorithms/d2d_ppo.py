@@ -143,8 +143,19 @@ class D2DPPO(BatchedLearnerBase):
         self._setup_data_parallel(self.policy.parameters() + list(self.value_network.parameters()))
 
     # ------------------------------------------------------------ rollouts
+    # round 5: the combinatorial env writes the rollout states as the central critic's bf16 operand (exact
+    # integers; d2d_env_out.state_bf16) when the fused critic takes them -- no fp32 state buffer, no conversion
+    # pass; D2D_STATE_BF16=0 keeps the fp32 buffer + d2d_states_to_bf16_padded (A/B)
+    state_bf16_rollout = os.environ.get("D2D_STATE_BF16", "1") != "0"
+
+    def _state_mode(self):
+        H = self.value_network.linear1.weight.shape[0]
+        bf = (self.state_bf16_rollout and self.kind == "comb" and bool(self.combinatorial) and self.critic_split
+              and self.critic_fused and H % 4 == 0 and H <= 128)
+        return "bf16" if bf else True
+
     def _rollout(self, num_episodes, teacher=None):
-        ro = self._collect(num_episodes, train=True, want_state=True, teacher=teacher)
+        ro = self._collect(num_episodes, train=True, want_state=self._state_mode(), teacher=teacher)
         self._phase("rollout")
         # the actor parameters the rollout sampled with (a device copy: 2.5 K floats per MLP agent), so the
         # first update epoch can prove they are unchanged (any in-place write: Adam, load(), a direct

@@ -70,6 +70,11 @@ __device__ __forceinline__ uint32_t rne_pk(float a, float b) {
 __device__ __forceinline__ float bf_lo(uint32_t p) { return __uint_as_float(p << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
 
+#ifndef D2D_CRITIC_PD
+// operand prefetch distance in iterations + 1: 3 = three register sets in rotation (two iterations in flight), 2 =
+// two sets, the next iteration's chunks only (round 5 first version)
+#define D2D_CRITIC_PD 3
+#endif
 // KCH chunks of 32 features per iteration (one barrier per iteration; the operand loads of the next iteration in
 // flight behind this one's 48 KCH MFMAs per wave: at KCH = 1 the kernel read the 6.3 GB operand at ~3 TB/s)
 template <int HT, int ST, int KCH>
@@ -113,20 +118,17 @@ __global__ __launch_bounds__(256, 2) void critic_fwd_kernel(CriticArgs a) {
     for (int t = 0; t < HT; ++t) acc[st][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int iters = a.nchunk / KCH;  // (nchunk is padded to a multiple of KCH; the image is zero there)
-  bf16x8 xc[KCH][ST], xn[KCH][ST];
-  load_w(0);
-  load_x(xc, 0);
-  for (int it = 0; it < iters; ++it) {
+  // one iteration: W1's image slice of iteration it to LDS, the next slice's and (PD) the operand chunks of iteration
+  // it + PD - 1 into flight, one barrier, the MFMAs on xc
+  auto body = [&](int it, const bf16x8 (&xc)[KCH][ST], bf16x8 (&xl)[KCH][ST]) {
     // buffer it & 1 was last read in iteration it - 2: every wave passed iteration it - 1's barrier since
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
       const int e = tid + 256 * q;
       if (NE % 256 == 0 || e < NE) wl[it & 1][e] = wr[q];
     }
-    if (it + 1 < iters) {
-      load_w(it + 1);
-      load_x(xn, it + 1);
-    }
+    if (it + 1 < iters) load_w(it + 1);
+    if (it + D2D_CRITIC_PD - 1 < iters) load_x(xl, it + D2D_CRITIC_PD - 1);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < KCH; ++q)
@@ -141,11 +143,30 @@ __global__ __launch_bounds__(256, 2) void critic_fwd_kernel(CriticArgs a) {
           acc[st][t] = mfma_bf16(ah, xc[q][st], acc[st][t]);
         }
       }
+  };
+  load_w(0);
+#if D2D_CRITIC_PD == 3
+  // three operand register sets in rotation (the loop unrolled by three, so no set is copied: a copy would wait on
+  // its load at the end of the iteration that issued it): each chunk's loads are in flight for two iterations
+  bf16x8 x0[KCH][ST], x1[KCH][ST], x2[KCH][ST];
+  load_x(x0, 0);
+  if (iters > 1) load_x(x1, 1);
+  for (int it = 0; it < iters; it += 3) {
+    body(it, x0, x2);
+    if (it + 1 < iters) body(it + 1, x1, x0);
+    if (it + 2 < iters) body(it + 2, x2, x1);
+  }
+#else
+  bf16x8 xc[KCH][ST], xn[KCH][ST];
+  load_x(xc, 0);
+  for (int it = 0; it < iters; ++it) {
+    body(it, xc, xn);
 #pragma unroll
     for (int q = 0; q < KCH; ++q)
 #pragma unroll
       for (int st = 0; st < ST; ++st) xc[q][st] = xn[q][st];
   }
+#endif
 
   // ---- epilogue: bias, relu, value, dv, dpre's split; the lane's sums over its samples
   float b1r[HT][4], w2r[HT][4];

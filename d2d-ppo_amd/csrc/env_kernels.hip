@@ -23,6 +23,7 @@
 #include <cstring>
 
 #include "common.h"
+#include "policy_split.h"
 
 namespace d2d {
 
@@ -61,6 +62,8 @@ struct EnvArgs {
   uint8_t* rec;   // comb: compact obs record [E][N][rec_bytes] (D2D_RECORD_BYTES(F))
   int rec_bytes;
   float* state;
+  uint16_t* state_b;       // comb: bf16 state rows (d2d_env_out.state_bf16), row e at state_b + e * state_b_ld
+  int64_t state_b_ld;
   int32_t* reward;
   void* ack;
   uint8_t* success;
@@ -252,11 +255,11 @@ struct Lane {
 };
 
 template <bool LARGE>
-__device__ __forceinline__ Lane lane_geometry(const EnvArgs& a) {
+__device__ __forceinline__ Lane lane_geometry(const EnvArgs& a, int bidx = blockIdx.x) {
   Lane L;
   L.lane = threadIdx.x & (kWave - 1);
   if (LARGE) {
-    L.env = blockIdx.x;
+    L.env = bidx;
     L.k = threadIdx.x;
     L.local_env = 0;
     L.envs_per_block = 1;
@@ -265,7 +268,7 @@ __device__ __forceinline__ Lane lane_geometry(const EnvArgs& a) {
     L.local_env = threadIdx.x / a.seg;
     L.k = threadIdx.x - L.local_env * a.seg;
     L.envs_per_block = blockDim.x / a.seg;
-    L.env = blockIdx.x * L.envs_per_block + L.local_env;
+    L.env = bidx * L.envs_per_block + L.local_env;
     const int seg_base = L.lane & ~(a.seg - 1);
     L.segmask = (a.seg == kWave) ? ~0ull : (((1ull << a.seg) - 1ull) << seg_base);
   }
@@ -315,6 +318,25 @@ __device__ __forceinline__ void wave_flush(float* __restrict__ dst, const float*
   }
 }
 
+// The same rows as bf16 (state values are integers in [-1, 255]: the fp32 -> bf16 truncation is exact), S8 =
+// S rounded up to 8 columns, the pad zero: one 16-byte store per 8 columns.  lanes / stride: the lanes that
+// share the row (a wave, or the whole block for one LARGE env)
+__device__ __forceinline__ void flush_bf16(uint16_t* __restrict__ dst, const float* src, int S, int first, int stride,
+                                           bool nt) {
+  const int q8 = (S + 7) >> 3;
+  for (int q = first; q < q8; q += stride) {
+    uint32_t w[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int j = 8 * q + 2 * p;
+      const uint32_t lo = j < S ? __float_as_uint(src[j]) >> 16 : 0u;
+      const uint32_t hi = j + 1 < S ? __float_as_uint(src[j + 1]) & 0xFFFF0000u : 0u;
+      w[p] = lo | hi;
+    }
+    st_rec(reinterpret_cast<uint4*>(dst) + q, w[0], w[1], w[2], w[3], nt);
+  }
+}
+
 // =====================================================================
 // Combinatorial env: action = binary N x C matrix, per-(agent, channel)
 // Markov channel, ACK vector in {-1, 0, 1}.
@@ -324,10 +346,13 @@ __device__ __forceinline__ void wave_flush(float* __restrict__ dst, const float*
 //   N <= 64 : state staged per wave (the wave's envs), flushed by the wave;
 //   N  > 64 : state of the block's single env staged per block.
 // =====================================================================
+// The step of the envs of one (virtual) workgroup index bidx: comb_kernel runs it once per workgroup
+// (bidx = blockIdx.x); the fused env + policy slot (comb_policy_fused_kernel) runs it for the consecutive
+// env groups of its slice and passes lrec, an LDS image of the slice's records (agent k's row of env e at
+// lrec[k * lstride + 2 (e - lenv0)], two 16-byte words) that the slot's policy then reads instead of HBM.
 template <typename MaskT, int DW, bool LARGE, int CT, bool RESET>
-__global__ __launch_bounds__(kMaxAgents) __attribute__((amdgpu_waves_per_eu(D2D_COMB_WAVES_PER_EU))) void comb_kernel(EnvArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const Lane L = lane_geometry<LARGE>(a);
+__device__ __forceinline__ void comb_step(const EnvArgs& a, float* lds, int bidx, uint4* lrec, int lstride, int lenv0) {
+  const Lane L = lane_geometry<LARGE>(a, bidx);
   const int N = a.N, F = a.F;
   const int C = CT ? CT : a.C;
   const int wave = threadIdx.x >> 6;
@@ -456,7 +481,7 @@ __global__ __launch_bounds__(kMaxAgents) __attribute__((amdgpu_waves_per_eu(D2D_
   }
   // reset obs/state carry ones(C) in the channel and feedback slots (108-112)
   // ---- obs_k = [B'[k,:w_k], channel_obs[k] (pre-evolve), acknack] (199-206)
-  const int wave_env0 = LARGE ? blockIdx.x : (blockIdx.x * L.envs_per_block + wave * epw);
+  const int wave_env0 = LARGE ? bidx : (bidx * L.envs_per_block + wave * epw);
   const int wave_nenv = LARGE ? 1 : max(0, min(epw, a.E - wave_env0));
   if (a.obs) {
     if (L.active) {
@@ -482,7 +507,7 @@ __global__ __launch_bounds__(kMaxAgents) __attribute__((amdgpu_waves_per_eu(D2D_
     if (LARGE) {
       const int k0 = wave * kWave;
       const int nrows = max(0, min(kWave, N - k0));
-      if (nrows > 0) wave_flush(a.obs + ((size_t)blockIdx.x * N + k0) * F, lds_obs, nrows * F, a.flags & 1u);
+      if (nrows > 0) wave_flush(a.obs + ((size_t)bidx * N + k0) * F, lds_obs, nrows * F, a.flags & 1u);
     } else if (wave_nenv > 0) {
       wave_flush(a.obs + (size_t)wave_env0 * N * F, lds_obs, wave_nenv * N * F, a.flags & 1u);
     }
@@ -539,6 +564,11 @@ __global__ __launch_bounds__(kMaxAgents) __attribute__((amdgpu_waves_per_eu(D2D_
         const bool nt = a.flags & 1u;
         st_rec(dst, v[0], v[1], v[2], v[3], nt);
         st_rec(dst + 1, v[4], v[5], v[6], v[7], nt);
+        if (lrec) {
+          uint4* l = lrec + (size_t)L.k * lstride + 2 * (L.env - lenv0);
+          l[0] = make_uint4(v[0], v[1], v[2], v[3]);
+          l[1] = make_uint4(v[4], v[5], v[6], v[7]);
+        }
         built = true;
       }
     }
@@ -556,6 +586,11 @@ __global__ __launch_bounds__(kMaxAgents) __attribute__((amdgpu_waves_per_eu(D2D_
     }
     dst[0] = make_uint4(v[0], v[1], v[2], v[3]);
     dst[1] = make_uint4(v[4], v[5], v[6], v[7]);
+    if (lrec) {  // (the fused slot takes 32-byte records only)
+      uint4* l = lrec + (size_t)L.k * lstride + 2 * (L.env - lenv0);
+      l[0] = make_uint4(v[0], v[1], v[2], v[3]);
+      l[1] = make_uint4(v[4], v[5], v[6], v[7]);
+    }
     for (int q32 = 1; q32 < a.rec_bytes / 32; ++q32) {  // columns >= 32: channel bits and acks only
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -570,7 +605,7 @@ __global__ __launch_bounds__(kMaxAgents) __attribute__((amdgpu_waves_per_eu(D2D_
     }
   }
   // state = [concat_k B'[k,:d_k], channel_state (post-evolve).flatten(), acknack] (207-209)
-  if (a.state) {
+  if (a.state || a.state_b) {
     if (L.active) {
       float* st = lds_state + (LARGE ? 0 : (L.local_env - wave * epw) * a.S);
       const int off = ag.state_offset, d = ag.deadline;
@@ -585,11 +620,78 @@ __global__ __launch_bounds__(kMaxAgents) __attribute__((amdgpu_waves_per_eu(D2D_
     }
     if (LARGE) {
       __syncthreads();
-      flush_rows(a.state + (size_t)blockIdx.x * a.state_stride, a.state_stride, lds_state, 1, a.S, a.flags & 1u);
+      if (a.state) flush_rows(a.state + (size_t)bidx * a.state_stride, a.state_stride, lds_state, 1, a.S, a.flags & 1u);
+      if (a.state_b) flush_bf16(a.state_b + (size_t)bidx * a.state_b_ld, lds_state, a.S, threadIdx.x, blockDim.x, a.flags & 1u);
     } else {
       wave_lds_sync();
-      for (int r = 0; r < wave_nenv; ++r)
-        wave_flush(a.state + (size_t)(wave_env0 + r) * a.state_stride, lds_state + r * a.S, a.S, a.flags & 1u);
+      for (int r = 0; r < wave_nenv; ++r) {
+        if (a.state)
+          wave_flush(a.state + (size_t)(wave_env0 + r) * a.state_stride, lds_state + r * a.S, a.S, a.flags & 1u);
+        if (a.state_b)
+          flush_bf16(a.state_b + (size_t)(wave_env0 + r) * a.state_b_ld, lds_state + r * a.S, a.S, L.lane, kWave,
+                     a.flags & 1u);
+      }
+    }
+  }
+}
+
+template <typename MaskT, int DW, bool LARGE, int CT, bool RESET>
+__global__ __launch_bounds__(kMaxAgents) __attribute__((amdgpu_waves_per_eu(D2D_COMB_WAVES_PER_EU))) void comb_kernel(EnvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  comb_step<MaskT, DW, LARGE, CT, RESET>(a, lds, blockIdx.x, nullptr, 0, 0);
+}
+
+// =====================================================================
+// Fused env + policy slot (ippo.py:293-330): one launch runs the env step of slot t
+// (comb_step, actions_t -> record_{t+1}, env state, rewards) and the behaviour policy of slot t + 1
+// (SplitNet, record_{t+1} -> actions_{t+1}, log-probs) for a slice of SE envs.  The record is still written to
+// HBM (it is the rollout buffer the update reads) but the policy reads the slice's copy in LDS, and the launch
+// boundary between the two kernels is gone.  The policy's weight split, amortised over 256 envs per wave in
+// policy_split_kernel, is here paid once per (slice, agent): the price of an env-major slice.
+// Prototype for the benched shape: 64 agents (one wave per env), 8 channels, the 32-byte record, the actor
+// alone (no critic value), the Bernoulli head with A <= 8 (paired epilogue).
+//   LDS: the slice's records [agent][SE envs x 32 B + 16 B] (the pad makes the 64 agents' 16-byte writes of one
+//   env conflict-free); a tile read is 64 lanes x 8 contiguous bytes of one agent row.
+// =====================================================================
+template <int DW, int HT, int SE, int MODE>
+__global__ __launch_bounds__(256, SE <= 32 ? 2 : 1) void comb_policy_fused_kernel(EnvArgs e, MlpArgs p) {
+  static_assert(SE % 32 == 0, "the policy runs 16-env tiles in pairs");
+  constexpr int LSTR = 2 * SE + 1;  // uint4 words per agent row
+  __shared__ uint4 lrec[64 * LSTR];
+  const int env0 = blockIdx.x * SE;
+  // ---- env step of slot t: SE / 4 groups of four envs (one per wave, lane = agent)
+  for (int q = 0; q < SE / 4; ++q)
+    comb_step<uint8_t, DW, false, 8, false>(e, nullptr, blockIdx.x * (SE / 4) + q, lrec, LSTR, env0);
+  __syncthreads();
+  // ---- policy of slot t + 1 on the slice: wave w takes agents w, w + 4, ...
+  const uint32_t rng = (MODE == kModeSample && p.rng_off) ? p.rng_step + *p.rng_off : p.rng_step;
+  const int lane = threadIdx.x & 63, g = lane >> 4, i = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int k = wave; k < p.N; k += 4) {
+    SplitNet<1, HT, true, false> net;
+    net.load(p, k, g, i);
+    uint32_t sm[1][2];
+    record_sign_masks<1>(sm, p.sgn, k, g);
+    const uint4* row = lrec + k * LSTR;
+    auto tile = [&](int t, f32x4& lg) {
+      // bytes 8g .. 8g + 7 of env 16t + i's record
+      const uint2 w = reinterpret_cast<const uint2*>(row + 2 * (16 * t + i))[g];
+      const uint32_t d[1][2] = {{w.x, w.y}};
+      float xc[1][8];
+      stage_record_words<1>(xc, d, sm);
+      float v;
+      net.template tile<true>(xc, lg, v);
+    };
+    for (int tt = 0; tt < SE / 16; tt += 2) {
+      f32x4 lg0, lg1;
+      tile(tt, lg0);
+      tile(tt + 1, lg1);
+      // paired epilogue (policy_split_kernel): lanes 0-31 keep tile tt, lanes 32-63 take tile tt + 1
+      f32x4 lgc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) lgc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(lg0[r]), fu(lg1[r]), false, false)[0]);
+      const int envc = env0 + tt * 16 + i + (g < 2 ? 0 : 16);
+      policy_epilogue<0, false, true, MODE>(p, lgc, 0.f, envc, envc < p.E, k, g, rng);
     }
   }
 }
@@ -1024,7 +1126,7 @@ int set_lds(K kernel, size_t bytes) {
 // dynamic LDS of one workgroup (must match the carve in the kernels)
 size_t lds_need(const EnvArgs& a, int block, int kind) {
   const bool large = a.N > kWave;
-  const bool stage = a.obs || a.state;
+  const bool stage = a.obs || a.state || a.state_b;
   const bool comb = kind == D2D_ENV_COMBINATORIAL;
   if (kind == D2D_ENV_SINGLE) {
     const int epb = large ? 1 : block / a.seg;
@@ -1035,7 +1137,7 @@ size_t lds_need(const EnvArgs& a, int block, int kind) {
     const int epw = large ? 1 : kWave / a.seg;
     const size_t slot = (size_t)((kWave * a.F + 3) & ~3);
     size_t w = (size_t)a.cnt_words + (stage ? nwaves * slot : 0);
-    if (a.state) w += large ? (size_t)a.S : (size_t)nwaves * ((epw * a.S + 3) & ~3);
+    if (a.state || a.state_b) w += large ? (size_t)a.S : (size_t)nwaves * ((epw * a.S + 3) & ~3);
     return sizeof(float) * w;
   }
   const int epb = large ? 1 : block / a.seg;
@@ -1092,20 +1194,19 @@ int dispatch_dw(const EnvArgs& a, int block, int kind, hipStream_t s) {
   return dispatch_comb<DW>(a, block, s);
 }
 
-int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions, const d2d_env_replay* rp,
-            const d2d_env_out* out, int reset, int t, uint32_t rng_step, void* stream) {
+// the kernel arguments of one reset / step (everything but the launch geometry)
+int env_args(const d2d_env_desc* d, const d2d_env_state* st, const void* actions, const d2d_env_replay* rp,
+             const d2d_env_out* out, int reset, int t, uint32_t rng_step, EnvArgs& a) {
   int rc = check_desc(d);
   if (rc) return rc;
   if (!st || !st->buffers || !st->channels || !st->received || !st->discarded) {
     d2d_set_error("state buffers must be non-NULL"); return D2D_EINVAL;
   }
   const bool comb = d->env_kind == D2D_ENV_COMBINATORIAL;
-  const int kind = d->env_kind;
   if (!comb && (!st->sel_quality || !st->sel_count)) {
     d2d_set_error("chsel / single need sel_quality / sel_count"); return D2D_EINVAL;
   }
   if (!reset && !actions) { d2d_set_error("actions is NULL"); return D2D_EINVAL; }
-  EnvArgs a;
   memset(&a, 0, sizeof(a));
   a.E = d->n_envs; a.N = d->n_agents; a.C = d->n_channels; a.D = d->max_deadline; a.F = d->obs_dim;
   a.S = d->state_dim; a.state_stride = d->state_stride; a.reset = reset; a.rng_step = rng_step;
@@ -1119,12 +1220,30 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
   if (out) {
     a.obs = out->obs; a.state = out->state; a.reward = out->reward; a.ack = out->ack; a.success = out->success;
     a.rec = out->obs_record;
+    a.state_b = out->state_bf16;
+    a.state_b_ld = out->state_bf16_ld;
+  }
+  if (a.state_b) {
+    if (!comb) { d2d_set_error("state_bf16 is implemented for the combinatorial env only"); return D2D_EUNSUPPORTED; }
+    if ((reinterpret_cast<uintptr_t>(a.state_b) & 15) || (a.state_b_ld & 7) || a.state_b_ld < ((int64_t)a.S + 7) / 8 * 8) {
+      d2d_set_error("state_bf16: 16-byte aligned rows of state_bf16_ld >= state_dim rounded up to 8 (a multiple of 8)");
+      return D2D_EINVAL;
+    }
   }
   a.rec_bytes = D2D_RECORD_BYTES(a.F);
   if (a.rec && !comb) { d2d_set_error("obs_record is implemented for the combinatorial env only"); return D2D_EUNSUPPORTED; }
   if (a.rec && (reinterpret_cast<uintptr_t>(a.rec) & 15)) { d2d_set_error("obs_record must be 16-byte aligned"); return D2D_EINVAL; }
   draw_mask(d, reset ? 0 : t, a.draw);
   a.flags = store_flags();
+  return D2D_OK;
+}
+
+int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions, const d2d_env_replay* rp,
+            const d2d_env_out* out, int reset, int t, uint32_t rng_step, void* stream) {
+  EnvArgs a;
+  if (const int rc = env_args(d, st, actions, rp, out, reset, t, rng_step, a)) return rc;
+  const int kind = d->env_kind;
+  const bool comb = kind == D2D_ENV_COMBINATORIAL;
   const bool large = a.N > kWave;
   int seg = 1;
   while (seg < a.N) seg <<= 1;
@@ -1138,7 +1257,7 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
   // 512: 125 us, 1024: 134 us per 65,536 x 64-agent step)
   // 512-lane blocks (8 envs of 64 agents): comb 64 x 8 x 65,536 141 -> 137 us against 256-lane
   // blocks; single: 8 envs per gather-table read (256: 130 us, 512: 125 us, 1024: 134 us)
-  int block = large ? a.seg : (comb && !a.obs && !a.state) ? D2D_COMB_REC_BLOCK : 512;
+  int block = large ? a.seg : (comb && !a.obs && !a.state && !a.state_b) ? D2D_COMB_REC_BLOCK : 512;
   a.cnt_words = cnt_words(large ? 1 : block / a.seg);
   while (!large && block > kWave && block > a.seg && lds_need(a, block, kind) > 65536) {
     block >>= 1;
@@ -1152,6 +1271,26 @@ int run_env(const d2d_env_desc* d, const d2d_env_state* st, const void* actions,
     case 4: return dispatch_dw<4>(a, block, kind, s);
     default: return dispatch_dw<8>(a, block, kind, s);
   }
+}
+
+// envs per workgroup of the fused slot: 32 (default) or 64 (d2d_set_option(D2D_OPT_FUSED_SLICE, 64))
+std::atomic<int> g_fused_slice{32};
+
+template <int DW, int HT, int MODE>
+int launch_fused_se(const EnvArgs& e, const MlpArgs& p, hipStream_t s) {
+  const int se = g_fused_slice.load(std::memory_order_relaxed);
+  const dim3 grid((e.E + se - 1) / se);
+  if (se == 64) hipLaunchKernelGGL((comb_policy_fused_kernel<DW, HT, 64, MODE>), grid, dim3(256), 0, s, e, p);
+  else hipLaunchKernelGGL((comb_policy_fused_kernel<DW, HT, 32, MODE>), grid, dim3(256), 0, s, e, p);
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
+template <int DW>
+int launch_fused(const EnvArgs& e, const MlpArgs& p, hipStream_t s) {
+  const bool det = p.deterministic != 0;
+  if (p.H <= 32) return det ? launch_fused_se<DW, 2, kModeDeterministic>(e, p, s) : launch_fused_se<DW, 2, kModeSample>(e, p, s);
+  return det ? launch_fused_se<DW, 4, kModeDeterministic>(e, p, s) : launch_fused_se<DW, 4, kModeSample>(e, p, s);
 }
 
 }  // namespace
@@ -1168,6 +1307,11 @@ extern "C" int d2d_set_option(int32_t option, int32_t value) {
   }
   if (option == D2D_OPT_NT_STORES) {
     g_nt_stores.store(value ? 1 : 0, std::memory_order_relaxed);
+    return D2D_OK;
+  }
+  if (option == D2D_OPT_FUSED_SLICE) {
+    if (value != 0 && value != 32 && value != 64) { d2d_set_error("D2D_OPT_FUSED_SLICE: 0, 32 or 64"); return D2D_EINVAL; }
+    g_fused_slice.store(value == 64 ? 64 : 32, std::memory_order_relaxed);
     return D2D_OK;
   }
   if (option == D2D_OPT_CRITIC_GRAD_ROWS) {
@@ -1241,6 +1385,46 @@ extern "C" int d2d_env_step(const d2d_env_desc* desc, const d2d_env_state* st, c
                             const d2d_env_replay* replay, const d2d_env_out* out, int32_t timestep, uint32_t rng_step,
                             void* stream) {
   return run_env(desc, st, actions, replay, out, 0, timestep, rng_step, stream);
+}
+
+extern "C" int d2d_comb_policy_fused_step(const d2d_env_desc* desc, const d2d_env_state* st, const void* actions,
+                                          const d2d_env_out* out, int32_t timestep, uint32_t env_rng_step,
+                                          const d2d_mlp_desc* policy, uint32_t policy_rng_step, int32_t deterministic,
+                                          void* actions_out, float* logp_out, void* stream) {
+  EnvArgs e;
+  if (const int rc = env_args(desc, st, actions, nullptr, out, 0, timestep, env_rng_step, e)) return rc;
+  if (desc->env_kind != D2D_ENV_COMBINATORIAL || e.N != 64 || e.C != 8 || e.rec_bytes != 32) {
+    d2d_set_error("the combinatorial env with 64 agents, 8 channels and a 32-byte record only");
+    return D2D_EUNSUPPORTED;
+  }
+  if (!e.rec || e.obs || e.state || e.state_b) {
+    d2d_set_error("out must carry obs_record and no obs / state rows");
+    return D2D_EINVAL;
+  }
+  e.seg = 64;  // run_env's geometry for N = 64: one env per wave, no LDS staging
+  e.cnt_words = 0;
+  if (!policy) { d2d_set_error("policy is NULL"); return D2D_EINVAL; }
+  MlpArgs p;
+  if (const int rc = policy_mlp_args(policy, e.rec, nullptr, policy_rng_step, deterministic, actions_out, logp_out,
+                                     nullptr, p))
+    return rc;
+  if (!p.rec || p.N != e.N || p.E != e.E || p.F != e.F || policy->env_base != desc->env_base) {
+    d2d_set_error("the policy must read this env's record (D2D_OBS_U8, same agents, envs, obs_dim and env_base)");
+    return D2D_EINVAL;
+  }
+  if (p.kind != 0 || p.A > 8 || p.H > 64 || p.F + 1 > 32 || p.v1) {
+    d2d_set_error("the Bernoulli actor with n_out <= 8, hidden <= 64, obs_dim < 32 and no critic only");
+    return D2D_EUNSUPPORTED;
+  }
+  if (e.E == 0) return D2D_OK;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (buffer_words(e.D)) {
+    case 1: return launch_fused<1>(e, p, s);
+    case 2: return launch_fused<2>(e, p, s);
+    case 3: return launch_fused<3>(e, p, s);
+    case 4: return launch_fused<4>(e, p, s);
+    default: return launch_fused<8>(e, p, s);
+  }
 }
 
 extern "C" int d2d_sample_actions(const d2d_env_desc* d, void* actions, uint64_t threshold, uint32_t rng_step,

@@ -24,7 +24,7 @@
 #include <cmath>
 #include <cstdlib>
 
-#include "policy_epilogue.h"
+#include "policy_split.h"
 
 namespace d2d {
 
@@ -152,33 +152,19 @@ template <bool U8>
 constexpr int chunk_dwords() { return U8 ? 2 : 8; }
 
 
-// x[c][j] <- slot, then input F := 1.0 (layer-1 bias input) and inputs past F := 0
-template <int KC>
-__device__ __forceinline__ void stage_inputs(float (&x)[KC][8], const float* slot, int lane, int F, int g) {
-#pragma unroll
-  for (int c = 0; c < KC; ++c)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      // (v & keep) | bias: one v_and_or_b32 -- a select of the loaded value would be turned
-      // into a branch around the LDS read
-      const int col = 32 * c + 8 * g + j;
-      const uint32_t keep = col < F ? 0xFFFFFFFFu : 0u, bias = col == F ? 0x3F800000u : 0u;
-      x[c][j] = uf((fu(slot[(c * 8 + j) * 64 + lane]) & keep) | bias);
-    }
-}
-
 // The same from a ring slot of compact-record words [c][2][lane]: the record row already holds the
 // bias input 1 at column F and zeros past it (the env kernel writes them); sm[c][h] = this lane's
 // int8 byte masks of words h = 0, 1 (rec_byte)
 template <int KC>
 __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* slot, int lane,
                                              const uint32_t (&sm)[KC][2]) {
+  uint32_t d[KC][2];
 #pragma unroll
   for (int c = 0; c < KC; ++c) {
-    const uint32_t d0 = slot[(c * 2) * 64 + lane], d1 = slot[(c * 2 + 1) * 64 + lane];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x[c][j] = rec_byte(j < 4 ? d0 : d1, j & 3, sm[c][j >> 2]);
+    d[c][0] = slot[(c * 2) * 64 + lane];
+    d[c][1] = slot[(c * 2 + 1) * 64 + lane];
   }
+  stage_record_words<KC>(x, d, sm);
 }
 
 #ifndef D2D_POLICY_RNG_EARLY
@@ -194,12 +180,6 @@ __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* 
 // it could save at most (tools/gpu/fusion_bound.py)
 #define D2D_POLICY_ABLATE_NOREAD 0
 #endif
-#ifndef D2D_POLICY_L2_F32
-// 1 (A/B): actor layer 2 on v_mfma_f32_16x16x4_f32 straight from relu(H^T) (an exact fmaf chain, 16 MFMAs
-// of 32 cycles per tile) instead of the three-way split of relu(H^T) (88 VALU per tile) and 6 bf16 MFMAs
-#define D2D_POLICY_L2_F32 0
-#endif
-
 // KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even);
 // U8: the inputs are the env kernel's compact obs record (D2D_OBS_U8)
 template <int KC, int HT, int KIND, bool CRITIC, int MODE, bool U8>
@@ -218,76 +198,15 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
   int k, by;
   xcd_block(k, by);  // k = agent, by = env chunk
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
-  const int N = a.N, F = a.F, H = a.H, A = a.A;
+  const int N = a.N, F = a.F, A = a.A;
   const int tiles = a.envs_per_wave / 16;
   const int wave_env0 = (by * (blockDim.x >> 6) + wave) * a.envs_per_wave;
 
   // ---- weight fragments of agent k, split once per workgroup (kModeValue: the critic's only)
   constexpr bool ACTOR = MODE != kModeValue;
   static_assert(ACTOR || CRITIC, "the value-only instantiation needs the critic");
-  Parts w1p[ACTOR ? HT : 1][KC], v1p[CRITIC ? HT : 1][KC];
-#if D2D_POLICY_L2_F32
-  float w2f[HT][4];  // A operand of step (t, r): row = action i, k-slot g <-> hidden 16t + 4g + r
-#else
-  Parts w2p[HT / 2];
-#endif
-  float v2f[HT][4];
-  f32x4 b2i;
-  {
-    const float* W1 = a.w1 + (size_t)k * H * F;
-    const float* V1 = CRITIC ? a.v1 + (size_t)k * H * F : nullptr;
-#pragma unroll
-    for (int t = 0; t < HT; ++t) {
-      const int hrow = 16 * t + i;
-      const bool hok = hrow < H;
-#pragma unroll
-      for (int c = 0; c < KC; ++c) {
-        float wv[8], vv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int col = 32 * c + 8 * g + j;
-          wv[j] = !hok ? 0.f : col < F ? W1[(size_t)hrow * F + col] : col == F ? a.b1[(size_t)k * H + hrow] : 0.f;
-          if constexpr (CRITIC)
-            vv[j] = !hok ? 0.f : col < F ? V1[(size_t)hrow * F + col] : col == F ? a.c1[(size_t)k * H + hrow] : 0.f;
-        }
-        if constexpr (ACTOR) w1p[t][c] = split3(wv);
-        if constexpr (CRITIC) v1p[t][c] = split3(vv);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int hid = 16 * t + 4 * g + r;
-        v2f[t][r] = (CRITIC && hid < H) ? a.v2[(size_t)k * H + hid] : 0.f;
-      }
-    }
-#if D2D_POLICY_L2_F32
-#pragma unroll
-    for (int t = 0; t < HT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int hid = 16 * t + 4 * g + r;
-        w2f[t][r] = (i < A && hid < H) ? a.w2[((size_t)k * A + i) * H + hid] * kLog2e : 0.f;
-      }
-#else
-#pragma unroll
-    for (int c2 = 0; c2 < (ACTOR ? HT / 2 : 0); ++c2) {
-      // element j of lane group g <-> hidden 16 * (2 c2 + (j >> 2)) + 4 g + (j & 3): the
-      // accumulator registers of layer-1 tiles 2 c2 and 2 c2 + 1
-      float wv[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int hid = 16 * (2 * c2 + (j >> 2)) + 4 * g + (j & 3);
-        wv[j] = (i < A && hid < H) ? a.w2[((size_t)k * A + i) * H + hid] * kLog2e : 0.f;
-      }
-      w2p[c2] = split3(wv);
-    }
-#endif
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int act = 4 * g + r;
-      b2i[r] = act < A ? a.b2[(size_t)k * A + act] * kLog2e : 0.f;
-    }
-  }
-  const float c2 = CRITIC ? a.c2[k] : 0.f;
+  SplitNet<KC, HT, ACTOR, CRITIC> net;
+  net.load(a, k, g, i);
 
   // Two obs register sets alternate (loop unrolled by two), so each tile's loads are issued two
   // tiles ahead of their use without a register copy that would wait on them early.
@@ -314,13 +233,8 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(wbase), 0, nbytes, 0x00020000);
   // int8 byte masks of this lane's record words (agent k, columns 32c + 8g + 4h + r)
-  uint32_t sm[KC][2];
-#pragma unroll
-  for (int c = 0; c < KC; ++c) {
-    const uint32_t sg = U8 ? (a.sgn[(size_t)k * KC + c] >> (8 * g)) & 0xFFu : 0u;
-    sm[c][0] = sign_bytes(sg & 0xFu);
-    sm[c][1] = sign_bytes(sg >> 4);
-  }
+  uint32_t sm[KC][2] = {};
+  if constexpr (U8) record_sign_masks<KC>(sm, a.sgn, k, g);
   auto issue = [&](int t) {
     // look-ahead tiles past this wave's last are still issued (the counted waits need a fixed
     // DMA count) but aimed outside the descriptor's range: no memory traffic, zeros
@@ -343,111 +257,12 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
   };
   // layers 1-2 of one tile -> (pre-scaled) logits lg and critic value
   auto tile = [&](int tt, f32x4& lg, float& value) {
-      float xc[KC][8];
-      if constexpr (U8)
-        stage_record<KC>(xc, reinterpret_cast<const uint32_t*>(&ring[wave][tt % RING][0][0][0]), lane, sm);
-      else
-        stage_inputs<KC>(xc, &ring[wave][tt % RING][0][0][0], lane, F, g);
-      // bf16 high parts of the inputs; the residual parts only when some input of the tile is
-      // not bf16-exact (wave-uniform branch, rare for env observations; never for the record,
-      // whose integers in [-128, 255] are bf16-exact)
-      bf16x8 xh[KC];
-      uint32_t low = 0;
-#pragma unroll
-      for (int c = 0; c < KC; ++c) {
-        uint32_t u[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          low |= (fbits(xc[c][2 * q]) | fbits(xc[c][2 * q + 1])) & 0xFFFFu;
-          u[q] = pack_hi(xc[c][2 * q], xc[c][2 * q + 1]);
-        }
-        xh[c] = as_frag(u);
-      }
-      const bool x_exact = U8 || __builtin_amdgcn_ballot_w64(low != 0) == 0;  // wave-uniform
-
-      // ---- layer 1 (actor, critic), transposed: H^T = W1' . [X | 1]^T; the three weight parts
-      // against the high parts of X, then (rarely) the residual terms of X
-      f32x4 ha[HT], hv[HT];
-#pragma unroll
-      for (int t = 0; t < HT; ++t) {
-#pragma unroll
-        for (int c = 0; c < KC; ++c) {
-          if constexpr (ACTOR) {
-            const f32x4 za = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ha[t];
-            ha[t] = mfma_bf16(w1p[t][c].l, xh[c], za);
-            ha[t] = mfma_bf16(w1p[t][c].m, xh[c], ha[t]);
-            ha[t] = mfma_bf16(w1p[t][c].h, xh[c], ha[t]);
-          }
-          if constexpr (CRITIC) {
-            const f32x4 zv = c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : hv[t];
-            hv[t] = mfma_bf16(v1p[t][c].l, xh[c], zv);
-            hv[t] = mfma_bf16(v1p[t][c].m, xh[c], hv[t]);
-            hv[t] = mfma_bf16(v1p[t][c].h, xh[c], hv[t]);
-          }
-        }
-      }
-      if (!x_exact) {
-#pragma unroll
-        for (int c = 0; c < KC; ++c) {
-          const Parts xp = split3(xc[c]);
-#pragma unroll
-          for (int t = 0; t < HT; ++t) {
-            if constexpr (ACTOR) {
-              ha[t] = mfma_bf16(w1p[t][c].h, xp.l, ha[t]);
-              ha[t] = mfma_bf16(w1p[t][c].m, xp.m, ha[t]);
-              ha[t] = mfma_bf16(w1p[t][c].h, xp.m, ha[t]);
-            }
-            if constexpr (CRITIC) {
-              hv[t] = mfma_bf16(v1p[t][c].h, xp.l, hv[t]);
-              hv[t] = mfma_bf16(v1p[t][c].m, xp.m, hv[t]);
-              hv[t] = mfma_bf16(v1p[t][c].h, xp.m, hv[t]);
-            }
-          }
-        }
-      }
-
-      // ---- actor layer 2 on the accumulators of tile pairs (split, full six terms)
-      lg = b2i;
-#if D2D_POLICY_L2_F32 == 1
-#pragma unroll
-      for (int t = 0; t < HT; ++t)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) lg = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[t][r], relu(ha[t][r]), lg, 0, 0, 0);
-#elif D2D_POLICY_L2_F32 == 2
-      {  // two independent accumulation chains (hidden tiles [0, HT/2) and [HT/2, HT)), summed once
-        f32x4 lh = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int t = 0; t < HT / 2; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            lg = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[t][r], relu(ha[t][r]), lg, 0, 0, 0);
-            lh = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[HT / 2 + t][r], relu(ha[HT / 2 + t][r]), lh, 0, 0, 0);
-          }
-        lg += lh;
-      }
-#else
-#pragma unroll
-      for (int c2 = 0; c2 < (ACTOR ? HT / 2 : 0); ++c2) {
-        float hvals[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          hvals[r] = relu(ha[2 * c2][r]);
-          hvals[4 + r] = relu(ha[2 * c2 + 1][r]);
-        }
-        lg = mfma_split(w2p[c2], split3(hvals), false, lg);
-      }
-#endif
-      // ---- critic layer 2 (64 -> 1) on VALU
-      value = 0.f;
-      if constexpr (CRITIC) {
-        float pv = 0.f;
-#pragma unroll
-        for (int t = 0; t < HT; ++t)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) pv = fmaf(relu(hv[t][r]), v2f[t][r], pv);
-        pv = group_sum(pv);
-        value = pv + c2;
-      }
+    float xc[KC][8];
+    if constexpr (U8)
+      stage_record<KC>(xc, reinterpret_cast<const uint32_t*>(&ring[wave][tt % RING][0][0][0]), lane, sm);
+    else
+      stage_inputs<KC>(xc, &ring[wave][tt % RING][0][0][0], lane, F, g);
+    net.template tile<U8>(xc, lg, value);
   };
   // every wave runs the same even number of tiles (tiles past E read zeros and store nothing), so
   // the DMA count between a tile's issue and its wait is fixed: RING - 2 tiles of KC * DPC DMAs
@@ -618,8 +433,10 @@ static int launch_policy_split(const MlpArgs& a, hipStream_t s) {
   return D2D_OK;
 }
 
-extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const void* obs, const void* forced, uint32_t rng_step,
-                                   int32_t deterministic, void* actions, float* logp, float* value, void* stream) {
+// d2d_policy_mlp_step's argument checks and kernel arguments (also the fused env + policy slot's,
+// env_kernels.hip d2d_comb_policy_fused_step)
+int d2d::policy_mlp_args(const d2d_mlp_desc* d, const void* obs, const void* forced, uint32_t rng_step,
+                         int32_t deterministic, void* actions, float* logp, float* value, MlpArgs& a) {
   if (!d || !obs || !actions || !logp || !d->w1 || !d->b1 || !d->w2 || !d->b2) {
     d2d_set_error("d2d_policy_mlp_step: NULL argument");
     return D2D_EINVAL;
@@ -635,7 +452,7 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const void* obs, const
   }
   if (d->kind == 0 && d->n_out > 32) { d2d_set_error("too many channels"); return D2D_EUNSUPPORTED; }
   if (d->v1 && (!d->c1 || !d->v2 || !d->c2)) { d2d_set_error("critic needs v1, c1, v2, c2"); return D2D_EINVAL; }
-  MlpArgs a;
+  a = MlpArgs{};
   a.E = d->n_envs; a.N = d->n_agents; a.F = d->obs_dim; a.H = d->hidden; a.A = d->n_out; a.kind = d->kind;
   a.deterministic = deterministic ? 1 : 0;
   a.inv_A = 1.f / (float)a.A;
@@ -655,6 +472,13 @@ extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const void* obs, const
                   (long long)d->n_envs * d->n_agents * a.mask_bytes);
     return D2D_EUNSUPPORTED;
   }
+  return D2D_OK;
+}
+
+extern "C" int d2d_policy_mlp_step(const d2d_mlp_desc* d, const void* obs, const void* forced, uint32_t rng_step,
+                                   int32_t deterministic, void* actions, float* logp, float* value, void* stream) {
+  MlpArgs a;
+  if (const int rc = policy_mlp_args(d, obs, forced, rng_step, deterministic, actions, logp, value, a)) return rc;
   if (a.E == 0 || a.N == 0) return D2D_OK;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int ht = (a.H + 15) / 16;

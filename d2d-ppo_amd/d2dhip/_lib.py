@@ -37,13 +37,14 @@ def refuse_ablation(what):
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 12
+ABI_VERSION = 13
 D2D_OBS_F32, D2D_OBS_U8 = 0, 1
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
 D2D_OPT_GRU_GRAD_HISTORY = 3  # 1: d2d_gru_grad through the global row history even where the LDS path applies
 D2D_OPT_POLICY_CRITIC_SPLIT = 4  # 1: the iPPO critic value as its own launch beside the actor (bitwise the same)
 D2D_OPT_CRITIC_GRAD_ROWS = 5  # 1: d2d_ppo_critic_grad on the sample-on-rows kernel of rounds 2-4 (A/B)
+D2D_OPT_FUSED_SLICE = 6  # envs per workgroup of d2d_comb_policy_fused_step: 32 (0 = default) or 64
 
 _p = ctypes.c_void_p
 
@@ -63,7 +64,8 @@ class EnvState(ctypes.Structure):
 
 
 class EnvOut(ctypes.Structure):
-    _fields_ = [("obs", _p), ("state", _p), ("reward", _p), ("ack", _p), ("success", _p), ("obs_record", _p)]
+    _fields_ = [("obs", _p), ("state", _p), ("reward", _p), ("ack", _p), ("success", _p), ("obs_record", _p),
+                ("state_bf16", _p), ("state_bf16_ld", ctypes.c_int64)]
 
 
 def record_bytes(obs_dim):
@@ -132,6 +134,9 @@ _SIGS = {
     "d2d_critic_dpre_blocks": (ctypes.c_int32, [ctypes.c_int64]),
     "d2d_critic_dpre_split": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, _p, _p, _p, _p, _p, ctypes.c_int32, _p]),
     "d2d_critic_dpre_split3": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, _p, _p, _p, _p, _p, ctypes.c_int32, _p]),
+    "d2d_comb_policy_fused_step": (ctypes.c_int, [ctypes.POINTER(EnvDesc), ctypes.POINTER(EnvState), _p,
+                                                   ctypes.POINTER(EnvOut), ctypes.c_int32, ctypes.c_uint32,
+                                                   ctypes.POINTER(MlpDesc), ctypes.c_uint32, ctypes.c_int32, _p, _p, _p]),
     "d2d_policy_mlp_step": (ctypes.c_int, [ctypes.POINTER(MlpDesc), _p, _p, ctypes.c_uint32, ctypes.c_int32, _p, _p,
                                             _p, _p]),
     "d2d_ppo_workspace": (ctypes.c_int64, [ctypes.c_int32] * 6),

@@ -151,7 +151,8 @@ class EnvBatch:
             keep.append(arrivals)
         return _lib.EnvReplay(fp, ap), keep
 
-    def _out(self, want_obs, want_state, want_ack, want_success, out_obs, out_state, out_reward, out_record=None):
+    def _out(self, want_obs, want_state, want_ack, want_success, out_obs, out_state, out_reward, out_record=None,
+             out_state_bf16=None):
         s = self.spec
         if isinstance(out_obs, ObsRecord):
             out_obs, out_record = None, out_obs
@@ -171,12 +172,21 @@ class EnvBatch:
         ack = self.ack if want_ack else None
         succ = self.success if want_success else None
         o = _lib.EnvOut(*(None if t is None else t.data_ptr() for t in (obs, state, reward, ack, succ, rec)))
+        if out_state_bf16 is not None:
+            # [E][ld] bf16 rows with any row stride (a slot's rows of an env-major [E][T][ld] buffer): d2d_env_out.state_bf16
+            x = out_state_bf16
+            ld8 = -(-s.S // 8) * 8
+            if (x.dtype != torch.bfloat16 or x.dim() != 2 or x.shape[0] != self.E or x.shape[1] < ld8 or x.stride(1) != 1
+                    or x.device != self.device):
+                raise ValueError(f"out_state_bf16: expected bf16 ({self.E}, >= {ld8}) rows on {self.device}, got "
+                                 f"{x.dtype} {tuple(x.shape)} strides {x.stride()}")
+            o.state_bf16, o.state_bf16_ld = x.data_ptr(), x.stride(0)
         return o, dict(obs=obs if rec is None else out_record, state=state, reward=reward, ack=ack, success=succ)
 
     # ---------------------------------------------------------- reset/step
     def reset(self, want_obs=True, want_state=False, replay_arrivals=None, out_obs=None, out_state=None,
-              stream=None):
-        o, res = self._out(want_obs, want_state, False, False, out_obs, out_state, None)
+              stream=None, out_state_bf16=None):
+        o, res = self._out(want_obs, want_state, False, False, out_obs, out_state, None, out_state_bf16=out_state_bf16)
         rp, _keep = self._replay(None if replay_arrivals is None else (None, replay_arrivals))
         rc = self.lib.d2d_env_reset(self.desc, self.st, rp, o, self.rng_step, _lib.stream_ptr(stream))
         _lib.check(rc, "d2d_env_reset")
@@ -186,17 +196,39 @@ class EnvBatch:
         return res
 
     def step(self, actions, want_obs=True, want_state=False, want_ack=False, want_success=False, replay=None,
-             out_obs=None, out_state=None, out_reward=None, stream=None):
+             out_obs=None, out_state=None, out_reward=None, stream=None, out_state_bf16=None):
         s = self.spec
         want_act = (self.E, s.N)
         dt = _MASK_DTYPE[s.mask_bytes] if s.kind == COMB else torch.uint8
         self._check_out(actions, want_act, dt, "actions")
-        o, res = self._out(want_obs, want_state, want_ack, want_success, out_obs, out_state, out_reward)
+        o, res = self._out(want_obs, want_state, want_ack, want_success, out_obs, out_state, out_reward,
+                           out_state_bf16=out_state_bf16)
         rp, _keep = self._replay(replay)
         self.timestep += 1
         rc = self.lib.d2d_env_step(self.desc, self.st, actions.data_ptr(), rp, o, self.timestep, self.rng_step,
                                    _lib.stream_ptr(stream))
         _lib.check(rc, "d2d_env_step")
+        self.rng_step += 1
+        res["done"] = self.timestep >= s.episode_length
+        return res
+
+    def step_policy_fused(self, actions, out_record, out_reward, mlp_desc, deterministic, actions_out, logp_out,
+                          stream=None):
+        """step() into the compact record out_record, fused with the MLP policy of the next slot on that record
+        (d2d_comb_policy_fused_step, one launch): actions_out [E][N] and logp_out [N][E] of slot t + 1, drawn at
+        the rng_step the two-call sequence (step, then the policy) gives it -- bit-identical results.  mlp_desc:
+        an actor-only d2d_mlp_desc on this batch's record (obs_format D2D_OBS_U8)."""
+        s = self.spec
+        dt = _MASK_DTYPE[s.mask_bytes] if s.kind == COMB else torch.uint8
+        self._check_out(actions, (self.E, s.N), dt, "actions")
+        self._check_out(actions_out, (self.E, s.N), dt, "actions_out")
+        self._check_out(logp_out, (s.N, self.E), torch.float32, "logp_out")
+        o, res = self._out(False, False, False, False, out_record, None, out_reward)
+        self.timestep += 1
+        rc = self.lib.d2d_comb_policy_fused_step(self.desc, self.st, actions.data_ptr(), o, self.timestep,
+                                                 self.rng_step, mlp_desc, self.rng_step + 1, 1 if deterministic else 0,
+                                                 actions_out.data_ptr(), logp_out.data_ptr(), _lib.stream_ptr(stream))
+        _lib.check(rc, "d2d_comb_policy_fused_step")
         self.rng_step += 1
         res["done"] = self.timestep >= s.episode_length
         return res

@@ -43,12 +43,13 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 12  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
+#define D2D_ABI_VERSION 13  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
                               6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_states_to_bf16_exact,
                               d2d_critic_dpre_split; 8: d2d_gae_scan_moments, d2d_normalize_pair;
                               9: d2d_gae_scan_moments without outputs, d2d_gae_scan_normalized;
                               10: d2d_states_to_bf16_padded, d2d_critic_dpre_split3;
-                              11: D2D_OPT_CRITIC_GRAD_ROWS; 12: d2d_ppo_critic_grad_values, d2d_central_critic_* */
+                              11: D2D_OPT_CRITIC_GRAD_ROWS; 12: d2d_ppo_critic_grad_values, d2d_central_critic_*;
+                              13: d2d_comb_policy_fused_step, D2D_OPT_FUSED_SLICE, d2d_env_out.state_bf16 */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -123,6 +124,13 @@ typedef struct d2d_env_out {  /* any field may be NULL */
      * zeros.  Every obs value of this env is an integer in those ranges, so the record is exact;
      * consumers take it with obs_format = D2D_OBS_U8. */
     uint8_t* obs_record;
+    /* comb only (ABI v13): the state row as bf16 -- exact, every state value is an integer in [-1, 255] -- for
+     * the D2D central critic's operand: env e's row at state_bf16 + e * state_bf16_ld (elements; a multiple of
+     * 8, >= state_dim rounded up to 8, 16-byte aligned base), columns [state_dim, round_up(state_dim, 8)) zero.
+     * A caller passing the slot-t base of an env-major [E][T][ld] buffer with ld_env = T * ld gets the
+     * learner's [E*T][ld] operand with no fp32 copy and no conversion pass. */
+    uint16_t* state_bf16;
+    int64_t state_bf16_ld;
 } d2d_env_out;
 
 /* Row bytes of the compact obs record: 32 per chunk of 32 network inputs (obs columns + the
@@ -314,6 +322,22 @@ typedef struct d2d_mlp_desc {
 int d2d_policy_mlp_step(const d2d_mlp_desc* desc, const void* obs, const void* forced, uint32_t rng_step,
                         int32_t deterministic, void* actions, float* logp, float* value, void* stream);
 
+/* Fused env + policy rollout slot (the loop body of create_rollouts,
+ * /root/reference/algorithms/ippo.py:293-330): d2d_env_step of slot t (actions -> out->obs_record = the
+ * record of slot t + 1, env state, rewards; timestep / env_rng_step as d2d_env_step) followed by
+ * d2d_policy_mlp_step of slot t + 1 on that record (policy_rng_step, deterministic; actions_out,
+ * logp_out) in ONE launch: each workgroup steps a slice of envs and runs the policy of every agent on
+ * the slice's records from LDS.  The results equal the two calls' bit for bit.  actions_out may alias
+ * actions (a slice reads its own envs' actions before it writes them).  Prototype scope: the
+ * combinatorial env with 64 agents and 8 channels, obs_dim < 32 (32-byte record), out without obs /
+ * state rows; policy D2D_OBS_U8 on this env (same agents, envs, obs_dim, env_base), kind 0, n_out <= 8,
+ * hidden <= 64, no critic, no forced actions -- else D2D_EUNSUPPORTED / D2D_EINVAL.
+ * Measured against the two-launch slot in tools/gpu/fused_slot.py. */
+int d2d_comb_policy_fused_step(const d2d_env_desc* desc, const d2d_env_state* st, const void* actions,
+                               const d2d_env_out* out, int32_t timestep, uint32_t env_rng_step,
+                               const d2d_mlp_desc* policy, uint32_t policy_rng_step, int32_t deterministic,
+                               void* actions_out, float* logp_out, void* stream);
+
 /* ---- fused PPO update: per-agent gradients of the MLP learners' losses ----
  * Replaces evaluate() + loss + backward() of PPO.train_step for every agent at once
  * (algorithms/ippo.py:178-217; d2d_ppo.py:183-216): the actor loss
@@ -420,9 +444,11 @@ int d2d_gru_grad(const d2d_gru_desc* desc, int32_t T, const void* obs, const voi
  *   identical actions, log-probs and values).  Default: policy_kernels.hip's D2D_POLICY_CRITIC_SPLIT.
  * D2D_OPT_CRITIC_GRAD_ROWS: 1 = d2d_ppo_critic_grad on the sample-on-rows kernel of rounds 2-4 (A/B; the same
  *   gradients within fp32 rounding); 0 (default) = the hidden-on-rows kernel (update_kernels.hip).
+ * D2D_OPT_FUSED_SLICE: envs per workgroup of d2d_comb_policy_fused_step, 32 (0 = default) or 64 (A/B; the same
+ *   results, bit for bit); other values D2D_EINVAL.
  * Options are process-wide words (relaxed atomics) read once per call. */
 enum { D2D_OPT_NT_STORES = 1, D2D_OPT_POLICY_F32_MFMA = 2, D2D_OPT_GRU_GRAD_HISTORY = 3, D2D_OPT_POLICY_CRITIC_SPLIT = 4,
-       D2D_OPT_CRITIC_GRAD_ROWS = 5 };
+       D2D_OPT_CRITIC_GRAD_ROWS = 5, D2D_OPT_FUSED_SLICE = 6 };
 int d2d_set_option(int32_t option, int32_t value);
 
 const char* d2d_last_error(void);

@@ -385,7 +385,7 @@ def test_graph_rollout_equals_eager(algo, kind):
             ro = lr._rollout(60)
             res.append((ro.obs_f32.clone(), ro.actions.clone(), ro.logp.clone(), ro.rewards.clone(),
                         None if ro.values is None else ro.values.clone(),
-                        None if ro.states is None else ro.states[..., :env.state_space.shape[0]].clone(),  # no pad
+                        ro.state_seq.clone() if "state_dim" in ro.__dict__ else None,  # fp32 or bf16 rows, no pad
                         list(ro.scores), list(ro.ep_rewards)))
         outs.append(res)
         if graph:
