@@ -70,6 +70,11 @@ __device__ __forceinline__ uint32_t rne_pk(float a, float b) {
 __device__ __forceinline__ float bf_lo(uint32_t p) { return __uint_as_float(p << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
 
+#ifndef D2D_CRITIC_WAVES
+// waves per workgroup (2 per SIMD either way): 8 halves the W1 image slices each sample's workgroup reads from L2
+// and writes to LDS
+#define D2D_CRITIC_WAVES 4
+#endif
 #ifndef D2D_CRITIC_PD
 // operand prefetch distance in iterations + 1: 3 = three register sets in rotation (two iterations in flight), 2 =
 // two sets, the next iteration's chunks only (round 5 first version)
@@ -78,14 +83,15 @@ __device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 
 // KCH chunks of 32 features per iteration (one barrier per iteration; the operand loads of the next iteration in
 // flight behind this one's 48 KCH MFMAs per wave: at KCH = 1 the kernel read the 6.3 GB operand at ~3 TB/s)
 template <int HT, int ST, int KCH>
-__global__ __launch_bounds__(256, 2) void critic_fwd_kernel(CriticArgs a) {
+__global__ __launch_bounds__(64 * D2D_CRITIC_WAVES, 8 / D2D_CRITIC_WAVES) void critic_fwd_kernel(CriticArgs a) {
+  constexpr int WV = D2D_CRITIC_WAVES, NT = 64 * WV;  // waves / threads per workgroup
   constexpr int NI = HT * 3 * 64;  // 16-byte image entries per chunk
   __shared__ __attribute__((aligned(16))) bf16x8 wl[2][KCH * NI];
-  __shared__ float red[4][2 * 16 * HT + 2];
+  __shared__ float red[WV][2 * 16 * HT + 2];
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H;
-  const int64_t s0 = (int64_t)blockIdx.x * (64 * ST) + (int64_t)wave * (16 * ST);  // this wave's first sample
+  const int64_t s0 = (int64_t)blockIdx.x * (16 * ST * WV) + (int64_t)wave * (16 * ST);  // this wave's first sample
   // the wave's rows through a range-checked descriptor: rows past B read 0
   const int64_t rest = (a.B - s0) * a.ldx * 2;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
@@ -102,13 +108,13 @@ __global__ __launch_bounds__(256, 2) void critic_fwd_kernel(CriticArgs a) {
         x[q][st] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
                                                   xr, vo[st] + 64u * (uint32_t)(KCH * it + q), 0, 0));
   };
-  constexpr int NE = KCH * NI, NW = (NE + 255) / 256;  // image entries per iteration, per thread
+  constexpr int NE = KCH * NI, NW = (NE + NT - 1) / NT;  // image entries per iteration, per thread
   bf16x8 wr[NW];
   auto load_w = [&](int it) {
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
-      const int e = tid + 256 * q;
-      if (NE % 256 == 0 || e < NE) wr[q] = a.w1img[(size_t)it * NE + e];
+      const int e = tid + NT * q;
+      if (NE % NT == 0 || e < NE) wr[q] = a.w1img[(size_t)it * NE + e];
     }
   };
   f32x4 acc[ST][HT];
@@ -124,8 +130,8 @@ __global__ __launch_bounds__(256, 2) void critic_fwd_kernel(CriticArgs a) {
     // buffer it & 1 was last read in iteration it - 2: every wave passed iteration it - 1's barrier since
 #pragma unroll
     for (int q = 0; q < NW; ++q) {
-      const int e = tid + 256 * q;
-      if (NE % 256 == 0 || e < NE) wl[it & 1][e] = wr[q];
+      const int e = tid + NT * q;
+      if (NE % NT == 0 || e < NE) wl[it & 1][e] = wr[q];
     }
     if (it + 1 < iters) load_w(it + 1);
     if (it + D2D_CRITIC_PD - 1 < iters) load_x(xl, it + D2D_CRITIC_PD - 1);
@@ -252,9 +258,12 @@ __global__ __launch_bounds__(256, 2) void critic_fwd_kernel(CriticArgs a) {
   }
   __syncthreads();
   float* out = a.partial + (size_t)blockIdx.x * (2 * H + 2);
-  for (int q = tid; q < 2 * H + 2; q += 256) {
+  for (int q = tid; q < 2 * H + 2; q += NT) {
     const int src = q < H ? q : q < 2 * H ? 16 * HT + (q - H) : 32 * HT + (q - 2 * H);
-    out[q] = ((red[0][src] + red[1][src]) + red[2][src]) + red[3][src];
+    float v = red[0][src];
+#pragma unroll
+    for (int w = 1; w < WV; ++w) v += red[w][src];
+    out[q] = v;
   }
 }
 
@@ -270,7 +279,7 @@ static int critic_chunks(int ht, int S) { const int k = critic_kch(ht); return (
 extern "C" int32_t d2d_central_critic_blocks(int32_t H, int64_t B) {
   const int ht = critic_ht(H);
   if (ht == 0 || B <= 0) return 0;
-  const int64_t per = 64 * critic_st(ht);
+  const int64_t per = 16 * D2D_CRITIC_WAVES * critic_st(ht);
   return (int32_t)((B + per - 1) / per);
 }
 
@@ -305,13 +314,13 @@ extern "C" int d2d_central_critic_fwd(int32_t H, int64_t B, int32_t S, int64_t l
   bf16x8* img = reinterpret_cast<bf16x8*>(w1img);
   if (ht == 2) {
     hipLaunchKernelGGL(critic_w1_image_kernel<2>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
-    hipLaunchKernelGGL((critic_fwd_kernel<2, 4, 2>), dim3(G), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((critic_fwd_kernel<2, 4, 2>), dim3(G), dim3(64 * D2D_CRITIC_WAVES), 0, s, a);
   } else if (ht == 4) {
     hipLaunchKernelGGL(critic_w1_image_kernel<4>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
-    hipLaunchKernelGGL((critic_fwd_kernel<4, 4, 2>), dim3(G), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((critic_fwd_kernel<4, 4, 2>), dim3(G), dim3(64 * D2D_CRITIC_WAVES), 0, s, a);
   } else {
     hipLaunchKernelGGL(critic_w1_image_kernel<8>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
-    hipLaunchKernelGGL((critic_fwd_kernel<8, 2, 1>), dim3(G), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((critic_fwd_kernel<8, 2, 1>), dim3(G), dim3(64 * D2D_CRITIC_WAVES), 0, s, a);
   }
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;

@@ -351,7 +351,7 @@ __device__ __forceinline__ void flush_bf16(uint16_t* __restrict__ dst, const flo
 // env groups of its slice and passes lrec, an LDS image of the slice's records (agent k's row of env e at
 // lrec[k * lstride + 2 (e - lenv0)], two 16-byte words) that the slot's policy then reads instead of HBM.
 template <typename MaskT, int DW, bool LARGE, int CT, bool RESET>
-__device__ __forceinline__ void comb_step(const EnvArgs& a, float* lds, int bidx, uint4* lrec, int lstride, int lenv0) {
+__device__ __forceinline__ void comb_step(const EnvArgs a, float* lds, int bidx, uint4* lrec, int lstride, int lenv0) {
   const Lane L = lane_geometry<LARGE>(a, bidx);
   const int N = a.N, F = a.F;
   const int C = CT ? CT : a.C;

@@ -40,6 +40,7 @@ def test_fused_slot_equals_env_step_then_policy(slice_envs, deterministic, H):
 def _check_slots(deterministic, H, set_format):
     E = 1000  # ragged: 31.25 slices of 32, 15.6 of 64
     lr_a, lr_b = _learner(E, H=H), _learner(E, H=H)
+    lr_b._pseed = lr_a._policy_seed()  # (drawn lazily from torch's RNG: the second learner's draw would differ)
     ba, bb = lr_a.env.batch(), lr_b.env.batch()
     recs = [b.record_buffer((2,)) for b in (ba, bb)]
     for b, rec in zip((ba, bb), recs):

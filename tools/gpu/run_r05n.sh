@@ -9,6 +9,8 @@ timeout -k 10 300 python3 -u tools/gpu/critic_probe.py 256 > "$O/critic_probe.js
 rc=$?; echo "critic rc=$rc"; cat "$O/critic_probe.json"; tail -n 3 "$O/critic_probe.err"; [ $rc -eq 0 ] || exit $rc
 D2D_LIB_VARIANT=critpd2 D2D_ALLOW_ABLATION=1 timeout -k 10 300 python3 -u tools/gpu/critic_probe.py 256 > "$O/critic_probe_pd2.json" 2> "$O/critic_probe_pd2.err"
 rc=$?; echo "critic pd2 rc=$rc"; cat "$O/critic_probe_pd2.json"; [ $rc -eq 0 ] || exit $rc
+D2D_LIB_VARIANT=critw8 D2D_ALLOW_ABLATION=1 timeout -k 10 300 python3 -u tools/gpu/critic_probe.py 256 > "$O/critic_probe_w8.json" 2> "$O/critic_probe_w8.err"
+rc=$?; echo "critic w8 rc=$rc"; cat "$O/critic_probe_w8.json"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 500 python3 -u tools/gpu/fused_slot.py 65536 > "$O/fused_slot.json" 2> "$O/fused_slot.err"
 rc=$?; echo "fused rc=$rc"; cat "$O/fused_slot.json"; tail -n 4 "$O/fused_slot.err"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 python3 -u bench.py --legs env,configs --no-cpu-baseline --steps 20 --warmup 5 > "$O/bench.json" 2> "$O/bench.err"
