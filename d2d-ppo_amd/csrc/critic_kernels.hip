@@ -75,6 +75,13 @@ __device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 
 // and writes to LDS
 #define D2D_CRITIC_WAVES 4
 #endif
+#ifndef D2D_CRITIC_XLDS
+// 1: the operand through LDS in full 128-byte lines (KCH = 2, ST = 4): each load instruction brings 8 sample rows x 128 B
+// (the iteration's two chunks) instead of 16 rows x 64 B, the rows are written to a per-wave XOR-swizzled image and the
+// MFMA B fragments read back by ds_read_b128 (MI355X_MICROARCH / cdna_hip_programming: fragment-shaped loads cost the
+// texture path twice the work of full-line ones)
+#define D2D_CRITIC_XLDS 1
+#endif
 #ifndef D2D_CRITIC_PD
 // operand prefetch distance in iterations + 1: 3 = three register sets in rotation (two iterations in flight), 2 =
 // two sets, the next iteration's chunks only (round 5 first version)
@@ -86,8 +93,16 @@ template <int HT, int ST, int KCH>
 __global__ __launch_bounds__(64 * D2D_CRITIC_WAVES, 8 / D2D_CRITIC_WAVES) void critic_fwd_kernel(CriticArgs a) {
   constexpr int WV = D2D_CRITIC_WAVES, NT = 64 * WV;  // waves / threads per workgroup
   constexpr int NI = HT * 3 * 64;  // 16-byte image entries per chunk
+  // XL: the operand through the per-wave LDS image (D2D_CRITIC_XLDS): 64 rows x 8 16-byte slots per wave, slot s of row r
+  // at r * 8 + (s ^ ((r >> 1) & 7)) -- conflict-free for the 8-lane row writes and the 16-lane groups of the fragment
+  // reads; the workgroup's sums reuse wave 0's image after the loop (80 KB per workgroup: two per CU)
+  constexpr bool XL = D2D_CRITIC_XLDS && KCH == 2 && ST == 4;
+  constexpr int NRED = WV * (2 * 16 * HT + 2);
   __shared__ __attribute__((aligned(16))) bf16x8 wl[2][KCH * NI];
-  __shared__ float red[WV][2 * 16 * HT + 2];
+  __shared__ __attribute__((aligned(16))) uint4 xim[XL ? WV : 1][XL ? 64 * 8 : 1];
+  __shared__ float red_s[XL ? 1 : NRED];
+  static_assert(!XL || NRED * 4 <= 64 * 8 * 16, "the sums fit wave 0's image");
+  float (*red)[2 * 16 * HT + 2] = reinterpret_cast<float (*)[2 * 16 * HT + 2]>(XL ? reinterpret_cast<float*>(&xim[0][0]) : red_s);
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H;
@@ -151,6 +166,63 @@ __global__ __launch_bounds__(64 * D2D_CRITIC_WAVES, 8 / D2D_CRITIC_WAVES) void c
       }
   };
   load_w(0);
+  if constexpr (XL) {
+    // lane l brings row 8j + (l >> 3), 16-byte slot l & 7 of the iteration's 128-byte segment, for j = 0..7
+    uint32_t lo[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lo[j] = (uint32_t)(((int64_t)(8 * j + (lane >> 3)) * a.ldx) * 2 + 16 * (lane & 7));
+    uint4 xv[8];
+    auto load_xl = [&](int it) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(xr, lo[j] + 128u * (uint32_t)it, 0, 0);
+        xv[j] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+    };
+    uint4* own = &xim[XL ? wave : 0][0];
+    load_xl(0);
+    for (int it = 0; it < iters; ++it) {
+      // buffer it & 1 was last read in iteration it - 2: every wave passed iteration it - 1's barrier since
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int e = tid + NT * q;
+        if (NE % NT == 0 || e < NE) wl[it & 1][e] = wr[q];
+      }
+      // the wave's rows of iteration it (its own reads of the image in iteration it - 1 were issued before these
+      // writes, and one wave's LDS operations complete in order)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int r = 8 * j + (lane >> 3);
+        own[r * 8 + ((lane & 7) ^ ((r >> 1) & 7))] = xv[j];
+      }
+      if (it + 1 < iters) {
+        load_w(it + 1);
+        load_xl(it + 1);
+      }
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < KCH; ++q) {
+        bf16x8 xf[ST];
+#pragma unroll
+        for (int st = 0; st < ST; ++st) {
+          const int r = 16 * st + i;
+          xf[st] = __builtin_bit_cast(bf16x8, own[r * 8 + ((4 * q + g) ^ ((r >> 1) & 7))]);
+        }
+#pragma unroll
+        for (int t = 0; t < HT; ++t) {
+          const bf16x8* w = &wl[it & 1][q * NI + (t * 3) * 64 + lane];
+          const bf16x8 ah = w[0], am = w[64], al = w[128];
+#pragma unroll
+          for (int st = 0; st < ST; ++st) {
+            acc[st][t] = mfma_bf16(al, xf[st], acc[st][t]);
+            acc[st][t] = mfma_bf16(am, xf[st], acc[st][t]);
+            acc[st][t] = mfma_bf16(ah, xf[st], acc[st][t]);
+          }
+        }
+      }
+    }
+    __syncthreads();  // wave 0's image becomes the workgroup's sums below
+  } else {
 #if D2D_CRITIC_PD == 3
   // three operand register sets in rotation (the loop unrolled by three, so no set is copied: a copy would wait on
   // its load at the end of the iteration that issued it): each chunk's loads are in flight for two iterations
@@ -173,6 +245,7 @@ __global__ __launch_bounds__(64 * D2D_CRITIC_WAVES, 8 / D2D_CRITIC_WAVES) void c
       for (int st = 0; st < ST; ++st) xc[q][st] = xn[q][st];
   }
 #endif
+  }
 
   // ---- epilogue: bias, relu, value, dv, dpre's split; the lane's sums over its samples
   float b1r[HT][4], w2r[HT][4];
