@@ -407,7 +407,8 @@ def update_kernel_roofline(lr, ro, F, H, A, reps=4):
         tc += ev[1].elapsed_time(ev[2]) / reps
     # MFMA pipe time per 32-sample tile from the kernels' static instruction mix (F + 1 <= 32,
     # H <= 64, A <= 8: csrc/update_kernels.hip, bf16 logits): 104 (actor on the compact record: no
-    # HN recompute) or 128 (fp32 rows) / 40 (critic) v_mfma_f32_16x16x32_bf16 at 16 cycles/SIMD
+    # HN recompute) or 128 (fp32 rows) / 40 (critic, either orientation; PMC-confirmed,
+    # profiles/r05/pmc_upd_r05c.json) v_mfma_f32_16x16x32_bf16 at 16 cycles/SIMD
     # (MI355X_MICROARCH.md cycle table), 2.4 GHz peak clock
     from d2dhip.record import ObsRecord
     pipe = {"actor": (104 if isinstance(ro.obs, ObsRecord) else 128) * 16, "critic": 40 * 16}
@@ -423,7 +424,9 @@ def update_kernel_roofline(lr, ro, F, H, A, reps=4):
                      "algorithmic_gflops": agent_samples * fl / (ms / 1e3) / 1e9,
                      "executed_bf16_tflops": executed, "executed_over_bf16_dense_peak": executed / BF16_PEAK_TFLOPS,
                      "mfma_cycles_per_tile": pipe[name], "mfma_pipe_busy_frac_static": busy,
-                     "mfma_pmc": pmc_mfma(f"d2d::ppo_{name}_grad_kernel", "ppo"), "bound": "mfma"}
+                     # (the critic at H <= 64 runs the hidden-on-rows ppo_critic_grad_t_kernel since round 5)
+                     "mfma_pmc": (pmc_mfma("d2d::ppo_critic_grad_t_kernel", "ppo") if name == "critic" else None)
+                     or pmc_mfma(f"d2d::ppo_{name}_grad_kernel", "ppo"), "bound": "mfma"}
     return res
 
 

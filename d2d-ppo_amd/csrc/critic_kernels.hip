@@ -82,6 +82,11 @@ __device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 
 // texture path twice the work of full-line ones)
 #define D2D_CRITIC_XLDS 1
 #endif
+#ifndef D2D_CRITIC_WPD
+// XL path: W1's image slices loaded 1 iteration ahead, or (2) two ahead in two register sets -- measured 4 % SLOWER
+// (1.82-1.84 vs 1.75-1.76 ms per epoch at 256 agents, profiles/r05/critic_wpd: +46 VGPRs, and the slice is L2-resident)
+#define D2D_CRITIC_WPD 1
+#endif
 #ifndef D2D_CRITIC_PD
 // operand prefetch distance in iterations + 1: 3 = three register sets in rotation (two iterations in flight), 2 =
 // two sets, the next iteration's chunks only (round 5 first version)
@@ -180,13 +185,22 @@ __global__ __launch_bounds__(64 * D2D_CRITIC_WAVES, 8 / D2D_CRITIC_WAVES) void c
       }
     };
     uint4* own = &xim[XL ? wave : 0][0];
-    load_xl(0);
-    for (int it = 0; it < iters; ++it) {
+    // W1's image slices two iterations ahead in two register sets (the loop unrolled by two: no set is copied),
+    // the operand one iteration ahead
+    bf16x8 wr2[NW];
+    auto load_w2 = [&](bf16x8 (&w)[NW], int it) {
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        const int e = tid + NT * q;
+        if (NE % NT == 0 || e < NE) w[q] = a.w1img[(size_t)it * NE + e];
+      }
+    };
+    auto xbody = [&](int it, bf16x8 (&wc)[NW]) {
       // buffer it & 1 was last read in iteration it - 2: every wave passed iteration it - 1's barrier since
 #pragma unroll
       for (int q = 0; q < NW; ++q) {
         const int e = tid + NT * q;
-        if (NE % NT == 0 || e < NE) wl[it & 1][e] = wr[q];
+        if (NE % NT == 0 || e < NE) wl[it & 1][e] = wc[q];
       }
       // the wave's rows of iteration it (its own reads of the image in iteration it - 1 were issued before these
       // writes, and one wave's LDS operations complete in order)
@@ -195,10 +209,8 @@ __global__ __launch_bounds__(64 * D2D_CRITIC_WAVES, 8 / D2D_CRITIC_WAVES) void c
         const int r = 8 * j + (lane >> 3);
         own[r * 8 + ((lane & 7) ^ ((r >> 1) & 7))] = xv[j];
       }
-      if (it + 1 < iters) {
-        load_w(it + 1);
-        load_xl(it + 1);
-      }
+      if (it + 1 < iters) load_xl(it + 1);
+      if (it + D2D_CRITIC_WPD < iters) load_w2(wc, it + D2D_CRITIC_WPD);
       __syncthreads();
 #pragma unroll
       for (int q = 0; q < KCH; ++q) {
@@ -220,7 +232,17 @@ __global__ __launch_bounds__(64 * D2D_CRITIC_WAVES, 8 / D2D_CRITIC_WAVES) void c
           }
         }
       }
+    };
+    load_xl(0);
+#if D2D_CRITIC_WPD == 2
+    if (iters > 1) load_w2(wr2, 1);
+    for (int it = 0; it < iters; it += 2) {
+      xbody(it, wr);
+      if (it + 1 < iters) xbody(it + 1, wr2);
     }
+#else
+    for (int it = 0; it < iters; ++it) xbody(it, wr);
+#endif
     __syncthreads();  // wave 0's image becomes the workgroup's sums below
   } else {
 #if D2D_CRITIC_PD == 3

@@ -76,6 +76,35 @@ def test_library_validates_arguments_without_gpu():
     out = _lib.EnvOut(None, None, None, None, None, 16)
     assert lib.d2d_env_reset(ctypes.byref(dsc), ctypes.byref(st), None, ctypes.byref(out), 0, None) == -2
     assert b"obs_record" in lib.d2d_last_error()
+    # ABI v13: bf16 state rows (combinatorial env only, 16-byte aligned rows of >= round_up(S, 8) elements)
+    out_b = _lib.EnvOut(None, None, None, None, None, None, 16, 64)
+    assert lib.d2d_env_reset(ctypes.byref(dsc), ctypes.byref(st), None, ctypes.byref(out_b), 0, None) == -2
+    assert b"state_bf16" in lib.d2d_last_error()
+    # (the host-side tables are read on the host by argument-checked calls that pass: real arrays)
+    kinds, period, offs = np.zeros(64, np.uint8), np.ones(64), np.zeros(64)
+    comb = _lib.EnvDesc(0, 64, 8, 14, 30, 100, 100, 1, 0, 0, w, w, kinds.ctypes.data, period.ctypes.data,
+                        offs.ctypes.data, None, None, w)
+    for ptr, ld in ((16, 100), (24, 104), (16, 96)):  # ld not a multiple of 8, misaligned, narrower than 104
+        bad = _lib.EnvOut(None, None, None, None, None, None, ptr, ld)
+        assert lib.d2d_env_reset(ctypes.byref(comb), ctypes.byref(st), None, ctypes.byref(bad), 0, None) == -1
+        assert b"state_bf16" in lib.d2d_last_error()
+    # ABI v13: the fused env + policy slot's scope checks (before any HIP call)
+    rec_out = _lib.EnvOut(None, None, None, None, None, 16)
+    pol = _lib.MlpDesc(64, 1, 30, 64, 8, 0, w, w, w, w, None, None, None, None, 0, 0, None, _lib.D2D_OBS_U8, 0, w)
+    args = (1, 0, ctypes.byref(pol), 0, 0, w, w, None)
+    assert lib.d2d_comb_policy_fused_step(ctypes.byref(dsc), ctypes.byref(st), w, ctypes.byref(rec_out), *args) == -2
+    assert b"combinatorial" in lib.d2d_last_error()
+    rows_out = _lib.EnvOut(16, None, None, None, None, None)  # fp32 obs rows instead of the record
+    assert lib.d2d_comb_policy_fused_step(ctypes.byref(comb), ctypes.byref(st), w, ctypes.byref(rows_out), *args) == -1
+    assert b"obs_record" in lib.d2d_last_error()
+    pol.hidden = 128
+    assert lib.d2d_comb_policy_fused_step(ctypes.byref(comb), ctypes.byref(st), w, ctypes.byref(rec_out), *args) == -2
+    assert b"hidden <= 64" in lib.d2d_last_error()
+    pol.hidden, pol.n_envs = 64, 2
+    assert lib.d2d_comb_policy_fused_step(ctypes.byref(comb), ctypes.byref(st), w, ctypes.byref(rec_out), *args) == -1
+    assert b"same agents, envs" in lib.d2d_last_error()
+    assert lib.d2d_set_option(_lib.D2D_OPT_FUSED_SLICE, 48) == -1
+    assert lib.d2d_set_option(_lib.D2D_OPT_FUSED_SLICE, 0) == 0
 
 
 def test_record_signed_masks_and_decode():
