@@ -472,7 +472,7 @@ class D2DPPO(BatchedLearnerBase):
         if nc == 1:
             return torch.mm(dhm, xb, out_dtype=torch.float32)
         Bc = B // nc
-        a = dhm.view(dhm.shape[0], nc, Bc).permute(1, 0, 2)                          # [nc][2H][Bc], strided
+        a = dhm.view(dhm.shape[0], nc, Bc).permute(1, 0, 2)                          # [nc][pH][Bc], strided
         return torch.bmm(a, xb.view(nc, Bc, xb.shape[1]), out_dtype=torch.float32).sum(0)
 
     def _chain_dev(self, A, logp_new, logp_old_tne, cycle, T, E):
