@@ -1386,9 +1386,10 @@ __device__ __forceinline__ void load_critic_in_t(CriticInT<KC, U8>& in, const Up
 
 
 #ifndef D2D_CRITIC_T_WAVES
-// waves per SIMD the hidden-on-rows critic is register-budgeted for (KC = 1, H <= 64, the record: 168 VGPRs, no
-// spills; fp32 rows keep D2D_UPD_WAVES: their deferred fractional-input body would spill at 168)
-#define D2D_CRITIC_T_WAVES 3
+// waves per SIMD the hidden-on-rows critic is register-budgeted for (KC = 1, H <= 64, the record).  3 (168 VGPRs)
+// spills 18 registers, two scratch accesses per tile; on real rollouts 2 is faster: 0.708 / 0.712 -> 0.660 / 0.663 ms
+// per 26.2 M agent-samples, alternating A/B on one box (profiles/r05/critic_waves); random inputs had favoured 3
+#define D2D_CRITIC_T_WAVES 2
 #endif
 template <int KC, int HT, bool U8>
 __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? (U8 ? D2D_CRITIC_T_WAVES : D2D_UPD_WAVES) : 1) void ppo_critic_grad_t_kernel(UpdArgs a) {
