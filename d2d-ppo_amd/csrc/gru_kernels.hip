@@ -20,6 +20,7 @@
 #include <atomic>
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 
 #include "gru_common.h"
 #include "policy_epilogue.h"
@@ -107,7 +108,7 @@ struct GruArgs {
   const float* weight;                    // advantage / M (actor) or return target (critic)
   int64_t lo_st[3], w_st[3];
   float* partial;                         // [G][N][P]
-  float* hist;                            // [G * N * 4 waves][L][64 lanes][4 HT] per-wave hidden-state scratch
+  float* hist;                            // [G * N * 4 waves][2 L (COOP + PADC: 3 L)][64 lanes][4 HT] per-wave h scratch
   float* wimg;                            // [N][3 * 16 HT][16 IT] input images (gru_wih_image_kernel)
   float* hacc;                            // [G * N * 4 waves][GruHeadAcc::NV][64] head-gradient sums
   float* himg;                            // [N][HeadImg::SIZE] padded head images (gru_images_kernel)
@@ -413,9 +414,23 @@ __device__ __forceinline__ bf16x8 whh_dh_frag(const bf16x8* whh_b, int T, int t,
 // (gru_preact_split: the 74 KB split W_hh image in LDS, the split W_ih image from L2); the scratch is
 // then 2 HW rows per wave (the step's gradient rows leave it in three passes), 155 KB in all.
 // LONGW (COOP): windows longer than kFlushSteps steps, the cooperative accumulators flushed every kFlushSteps
+//
+// PADC (COOP, D2D_GRU_PAD_COLLAPSE): the BPTT of the front-padding region once per wave instead of once per
+// tile.  A padding step j < pad has the same h_{j-1} (the padding table), the same x (the bias input) and
+// hence the same gates for every sample, so the backward through the padding region is one LINEAR map of
+// dh_{pad-1}, the same for every sample, and so are the weight-gradient rows it produces (dg (x) h_{j-1},
+// dg (x) x, dgh_n).  A tile's BPTT therefore stops at jlo (the smallest pad of the workgroup's four tiles
+// of the round: they step in lockstep), adds its dh_{jlo-1} into the wave's entry sums ent[jlo-1], and one
+// extra all-padding pass after the last round runs j = L-2 .. 0 once with dh += ent[j] at each step.
+// Exact in real arithmetic; in fp32 only the summation order of the padding rows' contributions changes.
+// Saves the padding steps' share of the BPTT: ~16 % at L = 64 (ep_len 200), ~60 % at L = 256.
+#ifndef D2D_GRU_PAD_COLLAPSE
+#define D2D_GRU_PAD_COLLAPSE 1
+#endif
 template <int HT, int IT, int KIND, bool SPLIT, bool COOP = false, bool LONGW = false>
 __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   constexpr int HW = 16 * HT, R3 = 3 * HW, RT = R3 + 4, SROWS = 2 * HW;
+  constexpr bool PADC = COOP && D2D_GRU_PAD_COLLAPSE != 0;
   static_assert(!COOP || (HT == 4 && SPLIT && D2D_GRU_DH_BF16), "COOP: H in (32, 64], the split step, bf16 dh");
   static_assert(COOP || !LONGW, "LONGW: the cooperative path");
   using SP = GruSplit<HT, IT>;
@@ -480,9 +495,15 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   const SwzOff<HW> oh(g, i);
   const XSigns<IT> xsg(a.ov, k);
   const size_t wave_id = (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 4 + wave;
-  // per wave: [0, L) the tile's h_j, [L, 2L) the front-padding table: h after j + 1 all-padding steps
-  float* hist = a.hist + wave_id * (size_t)2 * L * 64 * 4 * HT;
+  // per wave: [0, L) the tile's h_j, [L, 2L) the front-padding table: h after j + 1 all-padding steps,
+  // (PADC) [2L, 3L) the padding-region entry sums: ent[j] = sum of dh_j over the tiles whose BPTT stopped at j + 1
+  float* hist = a.hist + wave_id * (size_t)(PADC ? 3 : 2) * L * 64 * 4 * HT;
   float* ptab = hist + (size_t)L * 64 * 4 * HT;
+  float* ent = ptab + (size_t)L * 64 * 4 * HT;
+  if constexpr (PADC)
+    for (int j = 0; j < L; ++j)
+#pragma unroll
+      for (int t = 0; t < HT; ++t) reinterpret_cast<f32x4*>(ent + ((size_t)j * 64 + lane) * 4 * HT)[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float* hacc = a.hacc + wave_id * (size_t)GruHeadAcc<HT>::NV * 64;
   for (int v = 0; v < GruHeadAcc<HT>::NV; ++v) hacc[v * 64 + lane] = 0.f;
   using WA = GruWAcc<HT, IT>;
@@ -574,10 +595,14 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
   // COOP: block-uniform rounds (the waves' BPTT steps meet at barriers); a wave without a tile in the
   // last round runs an all-invalid tile (every sample masked: zero gradient rows) through the barriers
   const int rounds = (n_tiles + 4 * (int)gridDim.y - 1) / (4 * (int)gridDim.y);
-  for (int rnd = 0; COOP ? rnd < rounds : true; ++rnd) {
-    const int tile = (rnd * (int)gridDim.y + (int)blockIdx.y) * 4 + wave;  // wave-uniform
+  // PADC: round `rounds` is the padding-region pass (block-uniform, every wave)
+  auto pad_of = [&](int tl) { return L - min((tl < n_tiles ? tl / a.env_tiles : 0) % a.ep_len + 1, L); };
+  for (int rnd = 0; COOP ? rnd < rounds + (PADC ? 1 : 0) : true; ++rnd) {
+    const bool ppass = PADC && rnd == rounds;
+    const int tbase = (rnd * (int)gridDim.y + (int)blockIdx.y) * 4;
+    const int tile = tbase + wave;  // wave-uniform
     if (!COOP && tile >= n_tiles) break;
-    const bool active = tile < n_tiles;
+    const bool active = !ppass && tile < n_tiles;
     const int slot = active ? tile / a.env_tiles : 0;
     const int e0 = active ? (tile - slot * a.env_tiles) * 16 : 0;
     const int env = e0 + i;
@@ -585,10 +610,21 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     const int pos = slot % a.ep_len;
     const int S = min(pos + 1, L);
     const int lo = slot - S + 1;
-    const int pad = L - S;  // training windows: front-zero-padded to L (preprocess_input_for_rnn)
+    // training windows: front-zero-padded to L (preprocess_input_for_rnn); the padding pass: all padding
+    const int pad = ppass ? L : L - S;
+    // PADC: this round's BPTT stops at jlo, the smallest pad of the workgroup's four tiles (inactive tiles: any)
+    const int jlo = PADC && !ppass ? min(min(pad_of(tbase), pad_of(tbase + 1)), min(pad_of(tbase + 2), pad_of(tbase + 3)))
+                                   : 0;
     const GruIn in = active ? load_gru_in<KIND>(a, slot, env, k, ok) : GruIn{0u, 0.f, 0.f};
     auto row_of = [&](int j) { return ((size_t)(j < pad ? lo : lo + j - pad) * E + e0) * N + k; };
 
+    float gcur[HT][4];
+    if (ppass) {
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gcur[t][r] = 0.f;
+    } else {
     // ---- forward over the window; h_j (j < L - 1) to the wave's scratch
     // (steps j < pad: the padding table)
     float h[HT][4];
@@ -627,7 +663,6 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     }
 
     // ---- head forward + loss gradient w.r.t. the head outputs (COOP: the scratch is the wave's region)
-    float gcur[HT][4];
     auto head_phase = [&]() {
     f32x4 pre1[HT], lg;
     float y[HT][4];
@@ -721,6 +756,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     lds_order();
     };
     head_phase();
+    }  // !ppass
 
     // ---- backpropagation through time, j = L-1 .. 0 (gates recomputed from h_{j-1}); the step's
     // h_{j-1} and x tile are loaded one step ahead
@@ -737,8 +773,28 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       }
       load_x_raw<IT>(xb, a.ov, row_of(j), g, i, ok, j < pad);
     };
-    load_bstep(L - 1);
-    for (int j = L - 1; j >= 0; --j) {
+    // (PADC: down to jlo; the padding pass from L - 2, adding the entry sums, its dh_{j} prefetched with the step)
+    const int jtop = ppass ? L - 2 : L - 1;
+    f32x4 entn[PADC ? HT : 1];
+    auto load_ent = [&](int j) {
+#pragma unroll
+      for (int t = 0; t < HT; ++t) entn[t] = reinterpret_cast<const f32x4*>(ent + ((size_t)j * 64 + lane) * 4 * HT)[t];
+    };
+    if (jtop >= 0) {
+      load_bstep(jtop);
+      if (ppass) load_ent(jtop);
+    }
+    // two instances of the step loop: the tiles' (PP false: the loop of the kernel without PADC, bounds aside)
+    // and the padding pass's (PP true)
+    auto bptt = [&](auto pp_c) {
+    constexpr bool PP = decltype(pp_c)::value;
+    for (int j = jtop; j >= jlo; --j) {
+      if constexpr (PP) {
+#pragma unroll
+        for (int t = 0; t < HT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) gcur[t][r] += entn[t][r];
+      }
       float hp[HT][4];
 #pragma unroll
       for (int t = 0; t < HT; ++t)
@@ -746,7 +802,10 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
         for (int r = 0; r < 4; ++r) hp[t][r] = hpn[t][r];
       float x[IT][4];
       decode_x<IT>(x, xb, a.ov, xsg, g);
-      if (j > 0) load_bstep(j - 1);
+      if (j > jlo) {
+        load_bstep(j - 1);
+        if constexpr (PP) load_ent(j - 1);
+      }
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
 #if D2D_GRU_ABLATE == 4
@@ -935,6 +994,19 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
           if (((L - 1 - j) % kFlushSteps) == kFlushSteps - 1 && j > 0) coop_flush();  // wave-uniform
       }
 #endif
+    }
+    };
+    if (ppass) bptt(std::true_type{});
+    else bptt(std::false_type{});
+    if constexpr (PADC) {
+      if (!ppass && jlo > 0) {  // dh_{jlo-1} of this tile's samples (lane columns) into the entry sums
+        f32x4* e = reinterpret_cast<f32x4*>(ent + ((size_t)(jlo - 1) * 64 + lane) * 4 * HT);
+        f32x4 ev[HT];
+#pragma unroll
+        for (int t = 0; t < HT; ++t) ev[t] = e[t];
+#pragma unroll
+        for (int t = 0; t < HT; ++t) e[t] = ev[t] + f32x4{gcur[t][0], gcur[t][1], gcur[t][2], gcur[t][3]};
+      }
     }
     if constexpr (COOP) {
       __syncthreads();  // the regions' last readers are done before the next head phase
@@ -1483,7 +1555,8 @@ static GruWs gru_ws_layout(int64_t G, int64_t N, int64_t P, int64_t L, int htp, 
   GruWs w;
   w.partial = 0;
   w.hist = up(G * N * P);
-  w.wimg = w.hist + up(waves * 2 * L * 64 * 4 * htp);  // per wave: the tile's h history + the padding table
+  // per wave: the tile's h history + the padding table (+ COOP: the padding-region entry sums, PADC)
+  w.wimg = w.hist + up(waves * (coop && D2D_GRU_PAD_COLLAPSE ? 3 : 2) * L * 64 * 4 * htp);
   // fp32 input images [N][3 HW][16 itp] or the split ones [N][3 htp][CI][3 parts][64] 16-byte words
   const int64_t ci = (itp + 1) / 2;
   w.hacc = w.wimg + up(N * std::max<int64_t>(3 * HW * 16 * itp, 3 * htp * ci * 3 * 64 * 4));

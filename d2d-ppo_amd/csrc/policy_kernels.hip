@@ -180,6 +180,10 @@ __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* 
 // it could save at most (tools/gpu/fusion_bound.py)
 #define D2D_POLICY_ABLATE_NOREAD 0
 #endif
+#ifndef D2D_POLICY_ACTOR_WAVES
+// waves per SIMD of the actor-only record instantiation (137 VGPRs at 3; 4 needs <= 128)
+#define D2D_POLICY_ACTOR_WAVES 3
+#endif
 // KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even);
 // U8: the inputs are the env kernel's compact obs record (D2D_OBS_U8)
 template <int KC, int HT, int KIND, bool CRITIC, int MODE, bool U8>
@@ -187,7 +191,7 @@ template <int KC, int HT, int KIND, bool CRITIC, int MODE, bool U8>
 // actor alone on the record (137 VGPRs: test(), D2D-PPO,
 // and iPPO training rollouts whose values come from the first epoch's critic pass); H in (64, 128] -- the
 // learners' default hidden_size 128 -- or F + 1 > 32: one wave / SIMD with the doubled weight fragments)
-__global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 3) : 1) void policy_split_kernel(MlpArgs a) {
+__global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : D2D_POLICY_ACTOR_WAVES) : 1) void policy_split_kernel(MlpArgs a) {
   static_assert(HT % 2 == 0, "layer 2 consumes hidden tiles in pairs");
   // Philox step of the launch, read once before the obs pipeline starts (the optional device
   // offset of graph replays; a load inside the epilogue would add a wait to every tile pair)
