@@ -20,7 +20,6 @@
 #include <atomic>
 #include <algorithm>
 #include <cmath>
-#include <type_traits>
 
 #include "gru_common.h"
 #include "policy_epilogue.h"
@@ -773,27 +772,28 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       }
       load_x_raw<IT>(xb, a.ov, row_of(j), g, i, ok, j < pad);
     };
-    // (PADC: down to jlo; the padding pass from L - 2, adding the entry sums, its dh_{j} prefetched with the step)
+    // (PADC: down to jlo; the padding pass from L - 2, adding the entry sums, prefetched with the step.  One loop
+    // for both: a second instance of the step loop for the padding pass cost the tiles' loop spill reloads, so
+    // every step adds ef * ent row, ef = 0 and a fixed row of the padding table in the tiles' rounds)
     const int jtop = ppass ? L - 2 : L - 1;
+    const float ef = ppass ? 1.f : 0.f;
+    const float* entp = ppass ? ent : ptab;
+    const size_t est = ppass ? (size_t)64 * 4 * HT : 0;
     f32x4 entn[PADC ? HT : 1];
     auto load_ent = [&](int j) {
 #pragma unroll
-      for (int t = 0; t < HT; ++t) entn[t] = reinterpret_cast<const f32x4*>(ent + ((size_t)j * 64 + lane) * 4 * HT)[t];
+      for (int t = 0; t < HT; ++t) entn[t] = reinterpret_cast<const f32x4*>(entp + (size_t)j * est + (size_t)lane * 4 * HT)[t];
     };
     if (jtop >= 0) {
       load_bstep(jtop);
-      if (ppass) load_ent(jtop);
+      if constexpr (PADC) load_ent(jtop);
     }
-    // two instances of the step loop: the tiles' (PP false: the loop of the kernel without PADC, bounds aside)
-    // and the padding pass's (PP true)
-    auto bptt = [&](auto pp_c) {
-    constexpr bool PP = decltype(pp_c)::value;
     for (int j = jtop; j >= jlo; --j) {
-      if constexpr (PP) {
+      if constexpr (PADC) {
 #pragma unroll
         for (int t = 0; t < HT; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) gcur[t][r] += entn[t][r];
+          for (int r = 0; r < 4; ++r) gcur[t][r] = fmaf(ef, entn[t][r], gcur[t][r]);
       }
       float hp[HT][4];
 #pragma unroll
@@ -804,7 +804,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       decode_x<IT>(x, xb, a.ov, xsg, g);
       if (j > jlo) {
         load_bstep(j - 1);
-        if constexpr (PP) load_ent(j - 1);
+        if constexpr (PADC) load_ent(j - 1);
       }
       f32x4 rz[2 * HT], ni[HT], nh[HT];
       const int z = opaque_zero();
@@ -995,9 +995,6 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
       }
 #endif
     }
-    };
-    if (ppass) bptt(std::true_type{});
-    else bptt(std::false_type{});
     if constexpr (PADC) {
       if (!ppass && jlo > 0) {  // dh_{jlo-1} of this tile's samples (lane columns) into the entry sums
         f32x4* e = reinterpret_cast<f32x4*>(ent + ((size_t)(jlo - 1) * 64 + lane) * 4 * HT);
