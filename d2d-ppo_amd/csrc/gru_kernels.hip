@@ -774,10 +774,10 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
     };
     // (PADC: down to jlo; the padding pass from L - 2, adding the entry sums, prefetched with the step.  One loop
     // for both: a second instance of the step loop for the padding pass cost the tiles' loop spill reloads, so
-    // every step adds ef * ent row, ef = 0 and a fixed row of the padding table in the tiles' rounds)
+    // every step adds an entry row -- in the tiles' rounds always row L - 1, which is zeroed at the start and never
+    // written (entries go to rows <= L - 2): a cache-hot zero)
     const int jtop = ppass ? L - 2 : L - 1;
-    const float ef = ppass ? 1.f : 0.f;
-    const float* entp = ppass ? ent : ptab;
+    const float* entp = ppass ? ent : ent + (size_t)(L - 1) * 64 * 4 * HT;
     const size_t est = ppass ? (size_t)64 * 4 * HT : 0;
     f32x4 entn[PADC ? HT : 1];
     auto load_ent = [&](int j) {
@@ -793,7 +793,7 @@ __global__ __launch_bounds__(256, 1) void gru_grad_kernel(GruArgs a) {
 #pragma unroll
         for (int t = 0; t < HT; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) gcur[t][r] = fmaf(ef, entn[t][r], gcur[t][r]);
+          for (int r = 0; r < 4; ++r) gcur[t][r] += entn[t][r];
       }
       float hp[HT][4];
 #pragma unroll

@@ -180,7 +180,10 @@ def ref_loss_grads(p, obs, ep, L, kind, acts, logp_old, W, clip, beta, dtype):
         loss = -s.reshape(N, -1).mean(1) - beta * ent.reshape(N, -1).mean(1)
         stats = torch.stack([s.reshape(N, -1).sum(1), ent.reshape(N, -1).sum(1)], 1)
     loss.sum().backward()
-    return {k: v.grad for k, v in q.items()}, stats.detach(), out.detach()
+    # (history_len 1: h0 = 0 is the window's only hidden input, so W_hh never enters the graph -- its gradient
+    # is exactly zero)
+    return ({k: v.grad if v.grad is not None else torch.zeros_like(v) for k, v in q.items()}, stats.detach(),
+            out.detach())
 
 
 GRAD_CASES = [
@@ -193,6 +196,8 @@ GRAD_CASES = [
     ("sigmoid", 2, 46, 64, 16, 6, 8, 16, 18),       # run_ippo_combinatorial.py's 46 inputs: three input tiles
     (None, 2, 46, 64, 1, 6, 8, 16, 18),
     ("softmax", 2, 60, 32, 5, 4, 8, 16, 17),        # four input tiles
+    ("sigmoid", 2, 30, 64, 8, 1, 8, 16, 18),        # history_len 1: no padding steps at all (cooperative path)
+    (None, 2, 30, 64, 1, 1, 8, 16, 18),
 ]
 
 
