@@ -99,6 +99,7 @@ struct GruArgs {
   // ---- policy kernel
   MlpArgs ep;                             // epilogue view: ep.E = n_slots * E (slot-major samples)
   float* value_out;                       // kind 2: [N][n_slots * E]
+  float* ptab_g;                          // padded windows longer than the LDS table: [G][N][L - 1][HW] (or NULL)
   // ---- grad kernel
   float clip_lo, clip_hi, beta, scale, inv_A;
   int mask_bytes;
@@ -157,7 +158,11 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
   // of any tile's padding steps, so bitwise the same h -- and tiles start their window at step pad.
   __shared__ float ptab_s[kGruPadTab * HW];  // [step j][unit]: h after j + 1 padding steps
   const bool use_tab = a.padded && a.L - 1 <= kGruPadTab;
-  if (use_tab && wave == 0) {
+  // longer windows (xp_n_agents: history_len = N up to 256) keep the table in global memory, one per workgroup
+  // (a tile reads one row of it: h after its pad steps); without it every tile ran its pad steps itself
+  const bool use_gtab = a.padded && !use_tab && a.ptab_g;
+  float* gtab = use_gtab ? a.ptab_g + ((size_t)blockIdx.y * gridDim.x + k) * (size_t)(a.L - 1) * HW : nullptr;
+  if ((use_tab || use_gtab) && wave == 0) {
     float h[HT][4];
 #pragma unroll
     for (int t = 0; t < HT; ++t)
@@ -179,7 +184,7 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
 #pragma unroll
         for (int t = 0; t < HT; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) ptab_s[j * HW + 16 * t + 4 * g + r] = h[t][r];
+          for (int r = 0; r < 4; ++r) (use_tab ? ptab_s : gtab)[(size_t)j * HW + 16 * t + 4 * g + r] = h[t][r];
       }
     }
   }
@@ -197,12 +202,13 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
     const int S = min(pos + 1, a.L);
     const int lo = slot - S + 1;
     const int pad = a.padded ? a.L - S : 0;
-    const int j0 = use_tab ? pad : 0;  // the first step computed here (steps j < j0: the padding table)
+    const int j0 = use_tab || use_gtab ? pad : 0;  // the first step computed here (steps j < j0: the padding table)
     float h[HT][4];
+    const float* hrow = use_tab ? ptab_s : gtab;
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h[t][r] = j0 > 0 ? ptab_s[(j0 - 1) * HW + 16 * t + 4 * g + r] : 0.f;
+      for (int r = 0; r < 4; ++r) h[t][r] = j0 > 0 ? hrow[(size_t)(j0 - 1) * HW + 16 * t + 4 * g + r] : 0.f;
     // the window step's x tile is loaded one step ahead (its latency hides behind a step's MFMAs)
     float x[IT][4];
     XRaw<IT> xn;
@@ -1510,10 +1516,21 @@ extern "C" int d2d_policy_gru(const d2d_gru_desc* d, int32_t T, const void* obs,
   }
   dim3 grid(a.N, gy);
   const int ht = (a.H + 15) / 16;
+  // padded windows beyond the LDS padding table: a stream-ordered scratch table per workgroup (not while the
+  // stream is being captured: those launches run the pad steps per tile, the same arithmetic)
+  void* gtab = nullptr;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (a.padded && a.L - 1 > kGruPadTab && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+    const size_t bytes = sizeof(float) * (size_t)gy * a.N * (size_t)(a.L - 1) * 16 * (ht <= 1 ? 1 : ht <= 2 ? 2 : 4);
+    if (hipMallocAsync(&gtab, bytes, s) != hipSuccess) gtab = nullptr;
+  }
+  a.ptab_g = reinterpret_cast<float*>(gtab);
   if (ht <= 1) launch_policy_it<1>(a, grid, threads, s);
   else if (ht <= 2) launch_policy_it<2>(a, grid, threads, s);
   else launch_policy_it<4>(a, grid, threads, s);
-  D2D_CHECK_HIP(hipGetLastError());
+  const hipError_t le = hipGetLastError();
+  if (gtab) D2D_CHECK_HIP(hipFreeAsync(gtab, s));  // stream-ordered: released after the kernel
+  D2D_CHECK_HIP(le);
   return D2D_OK;
 }
 
