@@ -69,14 +69,75 @@ def config3_params(episode_length=200):
                 channel_switch=np.resize(cs8, (N, 8)))
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(n):
+    """`bench.py --gpus N` (N > 1) started without a launcher: start N fresh rank processes (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* in their env, one per GPU) and wait for them.  This parent never touches the GPU (no
+    HIP call before or after the fork: the children initialise their own devices); it forwards the ranks'
+    output, kills the remaining ranks when one fails (a rank left alone would block in its next collective) and
+    returns the worst child exit status."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n),
+                    "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port),
+                    "HSA_ENABLE_IPC_MODE_LEGACY": os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0")})
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+
+    def stop(signum, _frame):  # the launcher's own time limit: take the ranks down with it
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        sys.exit(128 + signum)
+
+    signal.signal(signal.SIGTERM, stop)
+    signal.signal(signal.SIGINT, stop)
+    rcs = [None] * n
+    failed_at = None
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+                if rcs[r] not in (None, 0) and failed_at is None:
+                    failed_at = time.monotonic()
+                    print(f"[bench] rank {r} exited with {rcs[r]}; stopping the other ranks", file=sys.stderr,
+                          flush=True)
+        if failed_at is not None and time.monotonic() - failed_at > 10:
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    p.kill()
+        time.sleep(0.2)
+    bad = [rc for rc in rcs if rc != 0]
+    return max(bad, key=abs) if bad else 0
+
+
 def setup_dist(n_gpus):
-    """One process per GPU over RCCL ("nccl").  Rehearsal switches for a 1-GPU box (never set by
-    the driver): D2D_BENCH_BACKEND=gloo and D2D_BENCH_SHARE_GPU=1 (every rank on cuda:0)."""
+    """One process per GPU over RCCL ("nccl").  The world comes from the launcher's env (WORLD_SIZE; bench.py
+    starts the ranks itself when run without one, self_launch) and must equal --gpus: a mismatch exits non-zero
+    instead of silently benchmarking another GPU count.  Rehearsal switches for a 1-GPU box (never set by the
+    driver): D2D_BENCH_BACKEND=gloo and D2D_BENCH_SHARE_GPU=1 (every rank on cuda:0).
+    Returns (rank, world, local, ranks_seen): ranks_seen = an all-reduce of one per rank over the group."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        print(f"[bench] WORLD_SIZE={world} but --gpus {n_gpus}: refusing to report a {world}-rank run as "
+              f"{n_gpus} GPUs", file=sys.stderr, flush=True)
+        sys.exit(2)
     if os.environ.get("D2D_BENCH_SHARE_GPU") == "1":
         local = 0
+    ranks_seen = 1
     if world > 1:
         torch.cuda.set_device(local)
         backend = os.environ.get("D2D_BENCH_BACKEND", "nccl")
@@ -84,9 +145,15 @@ def setup_dist(n_gpus):
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        one = torch.ones((1,), dtype=torch.int64, device=f"cuda:{local}" if backend == "nccl" else "cpu")
+        dist.all_reduce(one)
+        ranks_seen = int(one.item())
+        if ranks_seen != world:
+            print(f"[bench] all-reduce of ones saw {ranks_seen} ranks, WORLD_SIZE {world}", file=sys.stderr)
+            sys.exit(3)
     else:
         torch.cuda.set_device(0)
-    return rank, world, local
+    return rank, world, local, ranks_seen
 
 
 def barrier(world):
@@ -357,6 +424,7 @@ def ppo_leg(args, rank, world, local):
     lr._update_epoch(ro, upd)  # warm-up (allocator, hipBLASLt heuristics)
     torch.cuda.synchronize()
     barrier(world)
+    lr.phase_timer = PhaseTimer()
     t0 = time.perf_counter()
     P = args.ppo_epochs
     for _ in range(P):
@@ -364,12 +432,17 @@ def ppo_leg(args, rank, world, local):
     torch.cuda.synchronize()
     barrier(world)
     el = max_over_ranks(time.perf_counter() - t0, world)
+    # per-update phase split (HIP events at the learner's marks), max over ranks; "allreduce" is the bucketed
+    # gradient all-reduce (algorithms/data_parallel.py), absent at N = 1
+    phases = {k: max_over_ranks(v / P, world) for k, v in lr.phase_timer.totals_ms().items()}
+    lr.phase_timer = None
     N = params["n_agents"]
     samples = ro.T * E2 * world
     F, H, A = lr.policy.F, lr.policy.H, lr.policy.A
     out = {"updates_per_s": P / el, "ms_per_update": el / P * 1e3, "epochs": P,
            "batch": f"{E2} envs/GPU x {ro.T} slots x {N} agents (actor+critic, one Adam step each)",
-           "agent_samples_per_update": samples * N, "agent_samples_per_s": samples * N * P / el}
+           "agent_samples_per_update": samples * N, "agent_samples_per_s": samples * N * P / el,
+           "phase_ms_per_update": phases}
     if upd is None:
         out["path"] = "fused HIP update kernels (actor + critic gradients) + torch Adam"
         out["kernels"] = update_kernel_roofline(lr, ro, F, H, A, reps=P)
@@ -919,6 +992,9 @@ def main():
     ap.add_argument("--env-mode", default="both", choices=["both", "record", "fp32"],
                     help="obs output of the headline env steps (value = the first of record, fp32)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the ranks here, before anything touches the GPU
+        sys.exit(self_launch(args.gpus))
 
     params = config3_params(args.episode_length)
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
@@ -928,7 +1004,7 @@ def main():
         cpu = cpu_baseline_numpy(params, seconds=args.cpu_seconds)
         cpu["c_openmp"] = cpu_baseline_c(params, seconds=args.cpu_seconds)
 
-    rank, world, local = setup_dist(args.gpus)
+    rank, world, local, ranks_seen = setup_dist(args.gpus)
     from envs.combinatorial_env import CombinatorialEnv
 
     E = args.envs
@@ -1040,6 +1116,8 @@ def main():
             "value": env_steps_per_s,
             "unit": "env-steps/s",
             "n_gpus": world,
+            "ranks_seen": ranks_seen,
+            "dist_backend": dist.get_backend() if world > 1 else None,
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": t / K * 1e3,

@@ -1520,9 +1520,14 @@ extern "C" int d2d_policy_gru(const d2d_gru_desc* d, int32_t T, const void* obs,
   // stream is being captured: those launches run the pad steps per tile, the same arithmetic)
   void* gtab = nullptr;
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (a.padded && a.L - 1 > kGruPadTab && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
-    const size_t bytes = sizeof(float) * (size_t)gy * a.N * (size_t)(a.L - 1) * 16 * (ht <= 1 ? 1 : ht <= 2 ? 2 : 4);
-    if (hipMallocAsync(&gtab, bytes, s) != hipSuccess) gtab = nullptr;
+  if (a.padded && a.L - 1 > kGruPadTab) {
+    if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+      const size_t bytes = sizeof(float) * (size_t)gy * a.N * (size_t)(a.L - 1) * 16 * (ht <= 1 ? 1 : ht <= 2 ? 2 : 4);
+      if (hipMallocAsync(&gtab, bytes, s) != hipSuccess) gtab = nullptr;
+    }
+    // a failed query or allocation leaves HIP's sticky last error set: clear it, so the status checked after
+    // the launch is the launch's own (the fallback -- pad steps per tile -- is a valid launch)
+    if (!gtab) (void)hipGetLastError();
   }
   a.ptab_g = reinterpret_cast<float*>(gtab);
   if (ht <= 1) launch_policy_it<1>(a, grid, threads, s);

@@ -377,7 +377,9 @@ int d2d_ppo_critic_grad_values(const d2d_mlp_desc* desc, int32_t T, const void* 
 /* ---- D2D-PPO central critic, forward + the backward's per-sample glue (ABI 12) -------------------------------
  * The Value network over the whole state (d2d_ppo.py:62-98: linear1 [H][S], relu, linear2 [1][H]) for every sample
  * b of xb [B][ldx] (the rollout's states as exact bf16 integers, columns [S, ldx) zero, ldx a multiple of 8,
- * 16-byte aligned): values[b] = V(x_b); against ret [B] (the critic target, returns.mean(1), d2d_ppo.py:339) the
+ * 16-byte aligned; EVERY element of xb finite: the K loop reads whole 32-column chunks rounded up to its chunk
+ * group, so past column ldx it reads the next row's leading columns against zero W1 image columns, and a
+ * non-finite value there would turn 0 * x into NaN): values[b] = V(x_b); against ret [B] (the critic target, returns.mean(1), d2d_ppo.py:339) the
  * MSE loss's backward through linear2 / relu (d2d_ppo.py:440-446, value_loss.backward()): dpre_b = [pre_b > 0] w2
  * 2 (v_b - ret_b) / B as its three-way RNE bf16 split in dhm [B][3H] (parts h | m | l; dW1 = sum_b dpre_b x_b^T is
  * the caller's split-K GEMM), and per-workgroup sums partial [G][2H + 2] = db1 | dW2 | db2 | sum (v - ret)^2.

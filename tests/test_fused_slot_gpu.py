@@ -3,7 +3,10 @@ comb_policy_fused_kernel) against the two-launch slot it replaces (d2d_env_step,
 the loop body of create_rollouts, /root/reference/algorithms/ippo.py:293-330, whose parity with the reference
 the learner and env tests establish).  Bar: bit-exact -- the same record bytes, env state, rewards, actions
 and log-probs, in sampling and deterministic mode, on a ragged env count (not a multiple of the 32- or 64-env
-slice), and a whole iPPO training rollout with D2D_FUSED_SLOT on equal to the default rollout."""
+slice), and a whole iPPO training rollout with D2D_FUSED_SLOT on equal to the default rollout.  Oracle pin
+(test_fused_slot_matches_c_oracle_and_torch_policy): the fused launch against the C oracle env and the reference
+Policy in torch fp32 on the same Philox stream, not only against the two-launch HIP slot.  The row is a measured
+negative result (580 vs 252 us), off the product path (D2D_FUSED_SLOT defaults to 0)."""
 import pytest
 
 pytestmark = pytest.mark.gpu
@@ -119,3 +122,85 @@ def test_fused_slot_refuses_outside_prototype_scope():
         b64.step_policy_fused(b64.action_buffer(), rec64[0], None, desc2, False, b64.action_buffer(), logp)
     with pytest.raises(ValueError, match="obs_record"):  # an fp32-row output
         b64.step_policy_fused(b64.action_buffer(), b64.obs, None, desc2, False, b64.action_buffer(), logp)
+
+
+def _policy_probs_fp32(pp, obs):
+    """The reference Policy (ippo.py:54-71: linear1, relu, linear2, softmax) of every agent in torch fp32 on the
+    oracle's obs [E][N][F]: probs [N][E][A]."""
+    x = obs.transpose(0, 1)
+    h = torch.relu(torch.baddbmm(pp["b1"].unsqueeze(1), x, pp["w1"].transpose(1, 2)))
+    return torch.softmax(torch.baddbmm(pp["b2"].unsqueeze(1), h, pp["w2"].transpose(1, 2)), -1)
+
+
+@pytest.mark.parametrize("deterministic", [False, True], ids=["sample", "deterministic"])
+def test_fused_slot_matches_c_oracle_and_torch_policy(deterministic):
+    """Oracle pin of the fused slot (/root/reference/algorithms/ippo.py:293-330): over 6 fused
+    slots of a ragged 300-env batch, the C oracle env (oracle/c/d2d_oracle.c, the restatement of
+    CombinatorialEnv.step pinned to the reference's own fixtures) stepping the same actions at the same Philox
+    counters reproduces the fused launch's records (decoded obs) and rewards bit for bit; the reference Policy in
+    torch fp32 (softmax -> Bernoulli, ippo.py:54-71, 154-176) on the ORACLE's obs, with the Philox uniforms of
+    oracle/philox.py (stream 3 at the slot's rng_step), gives the fused launch's sampled actions (ties |u - p| <
+    1e-6 excluded) or deterministic actions (p > 0.5), and its log-probs within 1e-5 wherever every probability of
+    the (agent, env) lies in [1e-3, 1 - 1e-3] (1e-3 elsewhere: tests/test_policy_gpu.py's bar)."""
+    import numpy as np
+    import bench
+    from oracle import philox
+    from oracle.c_oracle import COracle
+    from d2dhip.record import set_format
+    from torch.distributions import Bernoulli
+    E, seed = 300, 9
+    lr = _learner(E, seed=seed)
+    b = lr.env.batch()
+    N, C = b.spec.N, b.spec.C
+    c = COracle("comb", bench.config3_params(200), n_envs=E, seed=seed, env_base=int(b.desc.env_base))
+    rec = b.record_buffer((2,))
+    assert b.rng_step == 0
+    b.reset(want_obs=True, out_obs=rec[0])
+    oc = c.reset(rng_step=0, want_state=False)
+    assert np.array_equal(rec[0].decode().cpu().numpy(), oc["obs"])
+    pp = {k: v.data for k, v in lr.policy.params.items()}
+    act = [b.action_buffer() for _ in range(2)]
+    logp = [torch.zeros((N, E), dtype=torch.float32, device="cuda:0") for _ in range(2)]
+    rew = torch.zeros(E, dtype=torch.int32, device="cuda:0")
+    lr._policy_slot(rec, 0, 0, not deterministic, act[0], logp[0], None, None, b)  # slot 0 (no env step before it)
+    desc = lr._mlp_desc(E, b.desc.env_base, critic=False)
+    desc.rng_offset = b.rng_off.data_ptr()
+    set_format(desc, rec[0])
+    pseed = lr._policy_seed()
+    envs = (int(b.desc.env_base) + np.arange(E)).astype(np.uint64)
+    agents = np.arange(N, dtype=np.uint64)
+
+    def bits_of(a):  # [E][N] uint8 masks -> [E][N][C]
+        return np.unpackbits(a.cpu().numpy().view(np.uint8).reshape(E, N, -1), axis=2, bitorder="little")[:, :, :C]
+
+    checked_sampled = 0
+    for t in range(6):
+        cur, nxt = t % 2, (t + 1) % 2
+        rs = b.rng_step
+        a_t = bits_of(act[cur])
+        b.step_policy_fused(act[cur], rec[nxt], rew, desc, deterministic, act[nxt], logp[nxt])
+        oc = c.step(a_t, rng_step=rs, want_state=False)
+        torch.cuda.synchronize()
+        assert np.array_equal(rec[nxt].decode().cpu().numpy(), oc["obs"]), f"record vs oracle obs, slot {t + 1}"
+        assert np.array_equal(rew.cpu().numpy(), oc["reward"]), f"reward vs oracle, slot {t}"
+        # the policy of slot t + 1 on the oracle's obs
+        probs = _policy_probs_fp32(pp, torch.from_numpy(oc["obs"]).to("cuda:0"))       # [N][E][C]
+        p = probs.double().cpu().numpy()
+        got = bits_of(act[nxt]).transpose(1, 0, 2)                                      # [N][E][C]
+        if deterministic:
+            near = np.abs(p - 0.5) < 1e-6
+            want = (p > 0.5).astype(np.uint8)
+        else:
+            r = philox.words(envs[None, :], agents[:, None], rs + 1, 3, 4 * ((C + 3) // 4), pseed)
+            u = (r[..., :C] >> np.uint64(8)).astype(np.float64) / 16777216.0
+            near = np.abs(u - p) < 1e-6
+            want = (u < p).astype(np.uint8)
+            checked_sampled += int((~near).sum())
+        assert np.array_equal(np.where(near, 0, got), np.where(near, 0, want)), f"actions, slot {t + 1}"
+        ref_lp = Bernoulli(probs=probs, validate_args=False).log_prob(
+            torch.from_numpy(got).to("cuda:0", torch.float32)).mean(-1)
+        well = ((probs > 1e-3) & (probs < 1 - 1e-3)).all(-1)
+        assert well.float().mean() > 0.5
+        torch.testing.assert_close(logp[nxt][well], ref_lp[well], rtol=0, atol=1e-5)
+        torch.testing.assert_close(logp[nxt], ref_lp, rtol=0, atol=1e-3)
+    assert deterministic or checked_sampled > 0.99 * 6 * N * E * C

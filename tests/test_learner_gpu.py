@@ -456,7 +456,8 @@ def test_rollout_graph_bound_to_its_batch():
 
 
 @pytest.mark.parametrize("case", ["comb12", "chsel16", "comb8", "comb16", "comb256", "chsel16-splitfwd",
-                                  "comb256-gemm", "chsel16-gemm", "comb256-h128", "comb256-h128-gemm", "comb8-h32"])
+                                  "comb256-gemm", "chsel16-gemm", "comb256-h128", "comb256-h128-gemm", "comb8-h32",
+                                  "comb16-h36", "comb8-h100", "chsel16-h20"])
 def test_d2d_central_critic_split_gemm_matches_fp32(case):
     """The central critic on the bf16 state operand (exact bf16 states x three-way split W1; dPre three-way
     split) == torch fp32 autograd of mse(Value(state), returns): values to 1e-5 relative; gradients against
@@ -466,7 +467,8 @@ def test_d2d_central_critic_split_gemm_matches_fp32(case):
     now also run on the split path -- configs[1] (S = 16 x 7 + 5 = 117, not a multiple of 8) and the
     sweep's 8 / 16 agents (S = 128 / 248), whose forward runs as one fp32 GEMM below
     CRITIC_F32_FWD_MAX_DIM (the "-splitfwd" case forces the split forward at S = 117).  Default: the fused HIP
-    forward + backward glue (d2d_central_critic_fwd, hidden 64 / 128 / 32); "-gemm" cases: the round-4 hipBLASLt
+    forward + backward glue (d2d_central_critic_fwd, hidden 64 / 128 / 32, and the ragged hidden sizes 36 / 100 / 20
+    whose last 16-unit tile is partial: masked b1 / w2 rows, zero image rows, the h0 < H store guard); "-gemm" cases: the round-4 hipBLASLt
     forward GEMM and dpre split kernel."""
     from algorithms.d2d_ppo import D2DPPO
     from envs.channel_selection_env import ChannelSelectionEnv

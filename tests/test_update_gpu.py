@@ -408,19 +408,25 @@ def test_grads_on_large_rollout_vs_float64(E):
     assert checked == 64 * 8
 
 
-def test_deferred_values_equal_rollout_values():
+@pytest.mark.parametrize("H", [64, 128])
+def test_deferred_values_equal_rollout_values(H):
     """iPPO training rollouts take their values from the first epoch's critic pass (d2d_ppo_critic_grad_values,
-    iPPO.defer_values): the same V(obs) as the rollout critic's forward (same weights; 1e-5), the same advantages
-    (1e-5), and that epoch's losses (1e-5) and post-Adam weights (2 % of lr) equal those of the epoch on the
-    per-slot values.  The deferred epoch runs the critic first; the two optimizers are independent."""
-    import copy
+    iPPO.defer_values): the deferred rollout (_rollout(defer_values=True): actor-only slots, zero-value returns)
+    on the same env draws and policy stream gives the same obs / actions / log-probs (bit-exact) and returns
+    (1e-5) as the per-slot-values rollout; its first epoch's critic pass writes the same V(obs) as the rollout
+    critic's forward (same weights; 1e-5), the same advantages (1e-5), and that epoch's losses (1e-5) and post-Adam
+    weights (2 % of lr) equal those of the epoch on the per-slot values.  H = 64 runs the hidden-on-rows critic
+    kernel, H = 128 the sample-on-rows one (its `values` write, update_kernels.hip)."""
     from algorithms.ippo import iPPO
-    (ref, dfr), ro, _ = _learner_pair(iPPO, "comb", E=96, N=6, H=64)
+    (ref, dfr), ro, _ = _learner_pair(iPPO, "comb", E=96, N=6, H=H)
     assert dfr._defer_values_ok()
-    ro2 = copy.copy(ro)
-    ro2.values = torch.zeros_like(ro.values)
-    ro2.adv_tne = None
-    ro2.values_pending = True
+    torch.manual_seed(1)  # _learner_pair's rollout seed: the same policy Philox stream
+    ro2 = dfr._rollout(96, defer_values=True)
+    assert ro2.values_pending and ro2.adv_tne is None
+    assert torch.equal(ro2.obs_f32, ro.obs_f32)
+    assert torch.equal(ro2.actions, ro.actions)
+    assert torch.equal(ro2.logp, ro.logp)
+    torch.testing.assert_close(ro2.ret_tne, ro.ret_tne, rtol=0, atol=1e-5)
     pl1, vl1 = ref._update_epoch(ro, None)
     pl2, vl2 = dfr._update_epoch(ro2, None)
     torch.testing.assert_close(ro2.values, ro.values, rtol=0, atol=1e-5)
