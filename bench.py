@@ -740,6 +740,17 @@ def d2denv_leg(args, rank, world, local):
     achieved = bytes_launch / (kern_ms / 1e3) / 1e9
     del env, b, act
     torch.cuda.empty_cache()
+    out = {"agents": N, "envs_per_gpu": args.envs, "obs_dim": s.F, "neighbourhood": "ring {k-1,k,k+1}",
+           "env_steps_per_s": args.envs * world * steps / wall,
+           "kernel": "d2d::single_kernel<2, false>", "kernel_avg_us": kern_ms * 1e3,
+           "bytes_per_launch": bytes_launch, "achieved_GBps": achieved, "hbm_frac": achieved / HBM_PEAK_GBS}
+    pmc, rel = load_profile_json("pmc_traffic_single.json")
+    if pmc and pmc.get("envs") == args.envs and pmc.get("agents") == N:
+        out["traffic"] = {"bytes_per_launch": pmc.get("bytes_per_launch"),
+                          "traffic_over_algorithmic": pmc.get("traffic_over_algorithmic"), "file": rel,
+                          "commit": pmc.get("commit")}
+    if args.d2denv_env_only:  # PMC passes: every single_kernel dispatch is a --envs launch
+        return out
     from algorithms.ippo import iPPO
     env = D2DEnv(**p, n_envs=4096, device=f"cuda:{local}", seed=32)
     env.shard(rank, world)
@@ -759,12 +770,8 @@ def d2denv_leg(args, rank, world, local):
     it(4)
     torch.cuda.synchronize()
     it_s = max_over_ranks(time.perf_counter() - t1, world)
-    out = {"agents": N, "envs_per_gpu": args.envs, "obs_dim": s.F, "neighbourhood": "ring {k-1,k,k+1}",
-           "env_steps_per_s": args.envs * world * steps / wall,
-           "kernel": "d2d::single_kernel<2, false>", "kernel_avg_us": kern_ms * 1e3,
-           "bytes_per_launch": bytes_launch, "achieved_GBps": achieved, "hbm_frac": achieved / HBM_PEAK_GBS,
-           "ippo_iteration_s_4096_envs": it_s, "fused_update": bool(lr._fused_update_ok()),
-           "ippo_env_steps_per_s_end_to_end": 4096 * world * args.episode_length / it_s}
+    out.update({"ippo_iteration_s_4096_envs": it_s, "fused_update": bool(lr._fused_update_ok()),
+                "ippo_env_steps_per_s_end_to_end": 4096 * world * args.episode_length / it_s})
     del env, lr
     torch.cuda.empty_cache()
     return out
@@ -984,6 +991,7 @@ def main():
     ap.add_argument("--gru-c5-agents", default="64,128,256", help="agent counts of the c5 GRU leg")
     ap.add_argument("--gru-envs", type=int, default=256, help="envs per GPU in the GRU update / iteration")
     ap.add_argument("--gru-slot-only", action="store_true", help="gru leg: the 65,536-env policy slot only (PMC passes)")
+    ap.add_argument("--d2denv-env-only", action="store_true", help="d2denv leg: the env steps only (PMC passes)")
     ap.add_argument("--rollout-steps", type=int, default=60)
     ap.add_argument("--ppo-envs", type=int, default=2048, help="envs per GPU in the PPO-update rollout")
     ap.add_argument("--ppo-epochs", type=int, default=6)

@@ -229,6 +229,24 @@ class BatchedLearnerBase(DataParallelMixin):
                             ptr(cp["w2"]) if cp else None, ptr(cp["b2"]) if cp else None,
                             self._policy_seed(), int(env_base))
 
+    gru_carry = os.environ.get("D2D_GRU_CARRY", "1") != "0"
+
+    def _gru_carry(self, b, role, params):
+        """The carried-state scratch of one GRU policy on env batch b (None when D2D_GRU_CARRY=0).  Kept with the
+        batch it serves (a captured rollout graph bakes in its address); dropped with the batch."""
+        if not self.gru_carry:
+            return None
+        from d2dhip import gru
+        cache = self.__dict__.setdefault("_gru_carries", {})
+        ent = cache.get(id(b))
+        if ent is None or ent[0] is not b:
+            ent = cache[id(b)] = (b, {})
+        n = gru.carry_floats(params, b.E, self.history_len, self.env.episode_length)
+        buf = ent[1].get(role)
+        if buf is None or buf.numel() < n:
+            buf = ent[1][role] = torch.empty((n,), dtype=torch.float32, device=b.device)
+        return buf
+
     def _policy_slot(self, obs_buf, t0, i, train, act_out, logp_out, val_out, tf, b):
         """Actions for slot i of every env (written to act_out [E][N]), log-probs [N][E], values [N][E]."""
         forced = None if (tf is None or tf["actions"] is None) else tf["actions"][i]
@@ -238,15 +256,20 @@ class BatchedLearnerBase(DataParallelMixin):
             from d2dhip import gru
             E, N = b.E, self.policy.N
             fz = None if forced is None else self._env_actions(forced).contiguous().view(1, E, N)
-            gru.policy({k: v.data for k, v in self.policy.params.items()}, obs_buf, self._gru_kind(),
+            # the slots of a wave run in order: while the episode position is below history_len the window extends
+            # the previous slot's, whose h the kernel carried (d2d_policy_gru_carry; bitwise the recompute)
+            pos = (i - t0) % self.env.episode_length
+            carry_in = 1 <= pos < self.history_len
+            pp = {k: v.data for k, v in self.policy.params.items()}
+            gru.policy(pp, obs_buf, self._gru_kind(),
                        self.history_len, self.env.episode_length, i, 1, padded=False, forced=fz,
                        rng_step=b.rng_step, deterministic=not train, seed=self._policy_seed(),
                        env_base=b.desc.env_base, rng_offset=b.rng_off.data_ptr(), actions_out=act_out.view(1, E, N),
-                       out=logp_out)
+                       out=logp_out, hcarry=self._gru_carry(b, "actor", pp), carry_in=carry_in)
             if val_out is not None:
-                crit = self.value
-                gru.policy({k: v.data for k, v in crit.params.items()}, obs_buf, None, self.history_len,
-                           self.env.episode_length, i, 1, padded=False, out=val_out)
+                cp = {k: v.data for k, v in self.value.params.items()}
+                gru.policy(cp, obs_buf, None, self.history_len, self.env.episode_length, i, 1, padded=False,
+                           out=val_out, hcarry=self._gru_carry(b, "critic", cp), carry_in=carry_in)
             return act_out
         if self._fused_ok() and (self.kind == "comb") == bool(self.combinatorial):
             from d2dhip import _lib
@@ -358,6 +381,9 @@ class BatchedLearnerBase(DataParallelMixin):
         graphs = self.__dict__.get("_rollout_graphs", {})
         for k in [k for k, G in graphs.items() if G["batch"] is b]:
             del graphs[k]
+        carries = self.__dict__.get("_gru_carries", {})
+        if id(b) in carries and carries[id(b)][0] is b:
+            del carries[id(b)]
 
     # ------------------------------------------------- rollout body (eager or captured)
     def _rollout_buffers(self, b, waves, want_values, want_state):

@@ -100,6 +100,8 @@ struct GruArgs {
   MlpArgs ep;                             // epilogue view: ep.E = n_slots * E (slot-major samples)
   float* value_out;                       // kind 2: [N][n_slots * E]
   float* ptab_g;                          // padded windows longer than the LDS table: [G][N][L - 1][HW] (or NULL)
+  float* hcarry;                          // one-slot unpadded launches: h after the window, [N][env_tiles][4 HT][64]
+  int carry_in;                           // 1: hcarry holds h after slot - 1's window (a prefix of this one)
   // ---- grad kernel
   float clip_lo, clip_hi, beta, scale, inv_A;
   int mask_bytes;
@@ -205,10 +207,17 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
     const int j0 = use_tab || use_gtab ? pad : 0;  // the first step computed here (steps j < j0: the padding table)
     float h[HT][4];
     const float* hrow = use_tab ? ptab_s : gtab;
+    // carried state (rollout / test windows, one slot per launch): while pos < L the window of slot s is the window
+    // of slot s - 1 plus obs_s, so h after slot s - 1's window (hcarry, written by the previous launch) enters the
+    // window's last step -- the same h the recompute reaches, hence bitwise the same step and head
+    float* hc = a.hcarry ? a.hcarry + ((size_t)k * a.env_tiles + (size_t)(e0 >> 4)) * (4 * HT * 64) + lane : nullptr;
+    const bool cin = hc && a.carry_in;
+    const int j1 = cin ? S - 1 : j0;
 #pragma unroll
     for (int t = 0; t < HT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) h[t][r] = j0 > 0 ? hrow[(size_t)(j0 - 1) * HW + 16 * t + 4 * g + r] : 0.f;
+      for (int r = 0; r < 4; ++r)
+        h[t][r] = cin ? hc[(4 * t + r) * 64] : j0 > 0 ? hrow[(size_t)(j0 - 1) * HW + 16 * t + 4 * g + r] : 0.f;
     // the window step's x tile is loaded one step ahead (its latency hides behind a step's MFMAs)
     float x[IT][4];
     XRaw<IT> xn;
@@ -217,8 +226,8 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
       const int row_slot = zero ? lo : lo + (j - pad);
       load_x_raw<IT>(xn, a.ov, ((size_t)row_slot * E + e0) * N + k, g, i, ok, zero);
     };
-    load_step(j0);
-    for (int j = j0; j < pad + S; ++j) {
+    load_step(j1);
+    for (int j = j1; j < pad + S; ++j) {
       decode_x<IT>(x, xn, a.ov, xsg, g);
       if (j + 1 < pad + S) load_step(j + 1);
       f32x4 rz[2 * HT], ni[HT], nh[HT];
@@ -230,6 +239,12 @@ __global__ __launch_bounds__(512, 1) void gru_policy_kernel(GruArgs a) {
         gru_preact<HT, IT, true>(wih_s + z, whh_s + z, oi, oh, x, h, bhn, rz, ni, nh, g, i, j == 0);
       }
       gru_gates<HT>(rz, ni, nh, h);
+    }
+    if (hc && pos + 1 < a.L) {  // the next slot's window extends this one: carry h (coalesced, one dword per lane)
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) hc[(4 * t + r) * 64] = h[t][r];
     }
     f32x4 pre1[HT], lg;
     float y[HT][4];
@@ -1479,9 +1494,42 @@ static GruArgs make_gru_args(const d2d_gru_desc* d, int T, const void* obs) {
   return a;
 }
 
+static int policy_gru(const d2d_gru_desc* d, int32_t T, const void* obs, int32_t slot0, int32_t n_slots,
+                      int32_t padded, const void* forced, uint32_t rng_step, int32_t deterministic, void* actions,
+                      float* out, float* hcarry, int32_t carry_in, void* stream);
+
+extern "C" int64_t d2d_gru_carry_floats(const d2d_gru_desc* d) {
+  if (!d || d->n_agents < 0 || d->n_envs < 0 || d->hidden < 1 || d->hidden > 64) return -1;
+  const int64_t ht = (d->hidden + 15) / 16;
+  return (int64_t)d->n_agents * ((d->n_envs + 15) / 16) * 4 * (ht <= 1 ? 1 : ht <= 2 ? 2 : 4) * 64;
+}
+
 extern "C" int d2d_policy_gru(const d2d_gru_desc* d, int32_t T, const void* obs, int32_t slot0, int32_t n_slots,
                               int32_t padded, const void* forced, uint32_t rng_step, int32_t deterministic,
                               void* actions, float* out, void* stream) {
+  return policy_gru(d, T, obs, slot0, n_slots, padded, forced, rng_step, deterministic, actions, out, nullptr, 0,
+                    stream);
+}
+
+extern "C" int d2d_policy_gru_carry(const d2d_gru_desc* d, int32_t T, const void* obs, int32_t slot,
+                                    const void* forced, uint32_t rng_step, int32_t deterministic, void* actions,
+                                    float* out, float* hcarry, int32_t carry_in, void* stream) {
+  if (!hcarry) { d2d_set_error("d2d_policy_gru_carry: NULL hcarry"); return D2D_EINVAL; }
+  if (d && d->episode_length > 0 && slot >= 0) {
+    const int pos = slot % d->episode_length;
+    if (carry_in && (pos < 1 || pos >= d->history_len)) {
+      d2d_set_error("d2d_policy_gru_carry: slot %d (episode position %d) does not extend the previous slot's window "
+                    "(history_len %d)", slot, pos, d->history_len);
+      return D2D_EINVAL;
+    }
+  }
+  return policy_gru(d, T, obs, slot, 1, 0, forced, rng_step, deterministic, actions, out, hcarry, carry_in ? 1 : 0,
+                    stream);
+}
+
+static int policy_gru(const d2d_gru_desc* d, int32_t T, const void* obs, int32_t slot0, int32_t n_slots,
+                      int32_t padded, const void* forced, uint32_t rng_step, int32_t deterministic, void* actions,
+                      float* out, float* hcarry, int32_t carry_in, void* stream) {
   int rc = check_gru_desc(d, obs);
   if (rc) return rc;
   if (!obs || !out || (d->kind != 2 && !actions)) { d2d_set_error("d2d_policy_gru: NULL buffer"); return D2D_EINVAL; }
@@ -1495,6 +1543,7 @@ extern "C" int d2d_policy_gru(const d2d_gru_desc* d, int32_t T, const void* obs,
   }
   GruArgs a = make_gru_args(d, T, obs);
   a.slot0 = slot0; a.n_slots = n_slots; a.padded = padded ? 1 : 0;
+  a.hcarry = hcarry; a.carry_in = carry_in;
   MlpArgs& ep = a.ep;
   ep.E = n_slots * a.E; ep.N = a.N; ep.F = a.F; ep.H = a.H; ep.A = a.A; ep.kind = d->kind == 0 ? 0 : 1;
   ep.deterministic = deterministic ? 1 : 0; ep.inv_A = a.inv_A; ep.rng_step = rng_step; ep.rng_off = d->rng_offset;

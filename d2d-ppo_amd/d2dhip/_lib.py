@@ -37,7 +37,7 @@ def refuse_ablation(what):
 
 D2D_ENV_COMBINATORIAL, D2D_ENV_CHANNEL_SELECTION, D2D_ENV_SINGLE = 0, 1, 2
 D2D_ARRIVAL_POISSON, D2D_ARRIVAL_SCHEDULED_BERNOULLI, D2D_ARRIVAL_NONE = 0, 1, 2
-ABI_VERSION = 13
+ABI_VERSION = 14
 D2D_OBS_F32, D2D_OBS_U8 = 0, 1
 D2D_OPT_NT_STORES = 1
 D2D_OPT_POLICY_F32_MFMA = 2
@@ -153,6 +153,9 @@ _SIGS = {
                                                _p, _p, _p, _p, _p, _p, _p, ctypes.c_int32, _p]),
     "d2d_policy_gru": (ctypes.c_int, [ctypes.POINTER(GruDesc), ctypes.c_int32, _p, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, _p, ctypes.c_uint32, ctypes.c_int32, _p, _p, _p]),
+    "d2d_gru_carry_floats": (ctypes.c_int64, [ctypes.POINTER(GruDesc)]),
+    "d2d_policy_gru_carry": (ctypes.c_int, [ctypes.POINTER(GruDesc), ctypes.c_int32, _p, ctypes.c_int32, _p,
+                                             ctypes.c_uint32, ctypes.c_int32, _p, _p, _p, ctypes.c_int32, _p]),
     "d2d_gru_grad_workspace": (ctypes.c_int64, [ctypes.POINTER(GruDesc), ctypes.c_int32]),
     "d2d_gru_grad": (ctypes.c_int, [ctypes.POINTER(GruDesc), ctypes.c_int32, _p, _p, _p, _p, _p, _p, ctypes.c_float,
                                      ctypes.c_float, ctypes.c_float, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p,

@@ -26,10 +26,23 @@ def desc(params, n_envs, kind, history_len, episode_length, seed=0, env_base=0, 
     return d
 
 
+def carry_floats(params, n_envs, history_len, episode_length):
+    """Floats of the carried-state scratch of one policy over n_envs envs (d2d_gru_carry_floats)."""
+    lib = _lib.require_gpu()
+    n = lib.d2d_gru_carry_floats(ctypes.byref(desc(params, n_envs, 2, history_len, episode_length)))
+    if n < 0:
+        raise ValueError("d2d_gru_carry_floats: unsupported shape")
+    return n
+
+
 def policy(params, obs, kind, history_len, episode_length, slot0, n_slots, padded=False, forced=None, rng_step=0,
-           deterministic=False, seed=0, env_base=0, rng_offset=None, actions_out=None, out=None):
+           deterministic=False, seed=0, env_base=0, rng_offset=None, actions_out=None, out=None, hcarry=None,
+           carry_in=False):
     """obs [T][E][N][F] (the rollout buffer: fp32, or the env kernel's ObsRecord).  kind 'sigmoid' / 'softmax' (actors): returns
-    (actions [n_slots][E][N], logp [N][n_slots * E]); kind None (value): returns values [N][n_slots * E]."""
+    (actions [n_slots][E][N], logp [N][n_slots * E]); kind None (value): returns values [N][n_slots * E].
+    hcarry (one unpadded slot per launch, slots in order: d2d_policy_gru_carry): float32 scratch of carry_floats()
+    elements holding h after the previous slot's window; carry_in: the previous launch on it was slot0 - 1 and
+    slot0's episode position is in [1, history_len - 1] (its window extends that one by one step)."""
     lib = _lib.require_gpu()
     T, E, N, F = obs.shape
     k = KIND[kind]
@@ -44,6 +57,18 @@ def policy(params, obs, kind, history_len, episode_length, slot0, n_slots, padde
         mb = 1 if (k == 1 or A <= 8) else 2 if A <= 16 else 4
         dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[mb]
         act = actions_out if actions_out is not None else torch.empty((n_slots, E, N), dtype=dt, device=dev)
+    if hcarry is not None:
+        if n_slots != 1 or padded:
+            raise ValueError("the carried state serves one unpadded slot per launch")
+        if hcarry.dtype != torch.float32 or hcarry.device != dev or hcarry.numel() < lib.d2d_gru_carry_floats(
+                ctypes.byref(d)):
+            raise ValueError("hcarry must be a float32 device tensor of d2d_gru_carry_floats elements")
+        rc = lib.d2d_policy_gru_carry(ctypes.byref(d), T, optr, int(slot0), None if forced is None else forced.data_ptr(),
+                                      int(rng_step) & 0xFFFFFFFF, 1 if deterministic else 0,
+                                      None if act is None else act.data_ptr(), out.data_ptr(), hcarry.data_ptr(),
+                                      1 if carry_in else 0, _lib.stream_ptr())
+        _lib.check(rc, "d2d_policy_gru_carry")
+        return (act, out) if k != 2 else out
     rc = lib.d2d_policy_gru(ctypes.byref(d), T, optr, int(slot0), int(n_slots), 1 if padded else 0,
                             None if forced is None else forced.data_ptr(), int(rng_step) & 0xFFFFFFFF,
                             1 if deterministic else 0, None if act is None else act.data_ptr(), out.data_ptr(),

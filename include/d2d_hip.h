@@ -43,13 +43,14 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 13  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
+#define D2D_ABI_VERSION 14  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
                               6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_states_to_bf16_exact,
                               d2d_critic_dpre_split; 8: d2d_gae_scan_moments, d2d_normalize_pair;
                               9: d2d_gae_scan_moments without outputs, d2d_gae_scan_normalized;
                               10: d2d_states_to_bf16_padded, d2d_critic_dpre_split3;
                               11: D2D_OPT_CRITIC_GRAD_ROWS; 12: d2d_ppo_critic_grad_values, d2d_central_critic_*;
-                              13: d2d_comb_policy_fused_step, D2D_OPT_FUSED_SLICE, d2d_env_out.state_bf16 */
+                              13: d2d_comb_policy_fused_step, D2D_OPT_FUSED_SLICE, d2d_env_out.state_bf16;
+                              14: d2d_policy_gru_carry, d2d_gru_carry_floats */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -419,6 +420,20 @@ typedef struct d2d_gru_desc {
 int d2d_policy_gru(const d2d_gru_desc* desc, int32_t T, const void* obs, int32_t slot0, int32_t n_slots,
                    int32_t padded, const void* forced, uint32_t rng_step, int32_t deterministic, void* actions,
                    float* out, void* stream);
+
+/* d2d_policy_gru for ONE unpadded slot (rollout / test windows, ippo.py:302-304, 362-364) with a carried hidden state
+ * (ABI 14).  While the slot's episode position p = slot % episode_length is below history_len, its window is the
+ * previous slot's window plus obs[slot] (both start at the episode's first slot; h0 = 0), so a rollout that runs its
+ * slots in order need not recompute the window: hcarry (d2d_gru_carry_floats(desc) floats of device scratch owned by
+ * the caller, one per (policy, env batch)) holds h after the previous slot's window, carry_in != 0 says so, and the
+ * launch runs the window's last step only.  Every launch whose next window extends its own (p + 1 < history_len)
+ * writes h after its window to hcarry.  carry_in requires p in [1, history_len - 1] (else D2D_EINVAL) and the
+ * previous launch on hcarry to have been slot - 1 of the same buffer, batch and weights (the caller's sequence).
+ * Actions, log-probs and values are bitwise those of d2d_policy_gru (the same steps on the same h). */
+int64_t d2d_gru_carry_floats(const d2d_gru_desc* desc);
+int d2d_policy_gru_carry(const d2d_gru_desc* desc, int32_t T, const void* obs, int32_t slot, const void* forced,
+                         uint32_t rng_step, int32_t deterministic, void* actions, float* out, float* hcarry,
+                         int32_t carry_in, void* stream);
 
 /* PPO.train_step's evaluate + loss + backward for GRU policies (ippo.py:178-217, d2d_ppo.py:183-216) and
  * the iPPO GRU critic's MSE (ippo.py:210-216) over every sample of the buffer (training windows, padded):

@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     for fn in fns:
         assert hasattr(lib, fn), fn
         assert fn in d2dhip.EXPORTED, f"{fn} has no ctypes signature"
-    assert lib.d2d_abi_version() == 13
+    assert lib.d2d_abi_version() == 14
     assert [lib.d2d_mask_bytes(c) for c in (1, 8, 9, 16, 17, 32)] == [1, 1, 2, 2, 4, 4]
     assert [lib.d2d_buffer_words(d) for d in (1, 4, 5, 8, 12, 14, 16, 17, 32)] == [1, 1, 2, 2, 3, 4, 4, 8, 8]
     assert lib.d2d_colstats_workspace(1000, 64) >= 64

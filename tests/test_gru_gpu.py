@@ -616,3 +616,72 @@ def xp_grads_check(kind, grad_input, E, check=True, cfg=None):
         tol = torch.maximum(1e-5 * s64c.abs() + 1e-4, 4 * (s32c - s64c).abs())
         assert bool(((got_s - s64c).abs() <= tol).all()), (col, ((got_s - s64c).abs() / tol).max().item())
     del well
+
+
+@pytest.mark.parametrize("case", [CASES[0], CASES[1], CASES[2], CASES[4], CASES[6]],
+                         ids=lambda c: f"{c[0]}-N{c[1]}-F{c[2]}-H{c[3]}-A{c[4]}-L{c[5]}-ep{c[6]}")
+@pytest.mark.parametrize("deterministic", [False, True], ids=["sample", "deterministic"])
+def test_gru_carried_state_equals_recompute(case, deterministic, policy_impl):
+    """d2d_policy_gru_carry (ABI 14): a rollout's slots in order, each launch carrying h into the
+    next while the window is a prefix extension (episode position < history_len, ippo.py:302-304), give bitwise the
+    actions / log-probs / values of the per-slot recompute from h0 = 0 -- across episode boundaries, windows longer
+    than the episode (L > ep_len) and past history_len, where the window slides and the launch recomputes."""
+    from d2dhip import gru
+    kind, N, F, H, A, L, ep, T, E = case
+    p, dims = make_net(N, F, H, A, seed=H + A + 1)
+    obs = make_obs(T, E, N, F, dims, seed=9, frac=kind == "softmax").to("cuda").contiguous()
+    pd = {k: v.to("cuda").contiguous() for k, v in p.items()}
+    hc = torch.full((gru.carry_floats(pd, E, L, ep),), float("nan"), device="cuda")
+    kw = dict(seed=77, env_base=5, deterministic=deterministic)
+    for t in range(T):
+        pos = t % ep
+        if kind is None:
+            v0 = gru.policy(pd, obs, None, L, ep, t, 1)
+            v1 = gru.policy(pd, obs, None, L, ep, t, 1, hcarry=hc, carry_in=1 <= pos < L)
+            assert torch.equal(v0, v1), f"value, slot {t}"
+        else:
+            a0, l0 = gru.policy(pd, obs, kind, L, ep, t, 1, rng_step=3 + t, **kw)
+            a1, l1 = gru.policy(pd, obs, kind, L, ep, t, 1, rng_step=3 + t, hcarry=hc, carry_in=1 <= pos < L, **kw)
+            assert torch.equal(a0, a1), f"actions, slot {t}"
+            assert torch.equal(l0, l1), f"log-probs, slot {t}"
+
+
+def test_gru_carry_refuses_a_window_that_does_not_extend():
+    from d2dhip import gru
+    from d2dhip._lib import D2DHipError
+    p, dims = make_net(2, 12, 16, 4, seed=1)
+    pd = {k: v.to("cuda").contiguous() for k, v in p.items()}
+    obs = make_obs(8, 16, 2, 12, dims, seed=1).to("cuda").contiguous()
+    hc = torch.zeros((gru.carry_floats(pd, 16, 3, 8),), device="cuda")
+    for slot in (0, 3, 8):  # an episode's first slot; positions >= history_len (3)
+        with pytest.raises(D2DHipError):
+            gru.policy(pd, obs, "softmax", 3, 8, slot, 1, hcarry=hc, carry_in=True)
+    with pytest.raises(ValueError):
+        gru.policy(pd, obs, "softmax", 3, 8, 1, 2, hcarry=hc, carry_in=True)
+
+
+@pytest.mark.parametrize("graph", [True, False], ids=["graph", "eager"])
+def test_gru_rollout_carry_c5_256_agents(graph):
+    """configs[4] as xp_n_agents.py writes its learner (D2D-PPO, GRU H = 64, history_len = N = 256 > the 200-slot
+    episode: every rollout window is an episode prefix, xp_n_agents.py:98-112): the training rollout with the carried
+    state (the default) equals the recompute (D2D_GRU_CARRY=0) bit for bit -- records, actions, log-probs, rewards."""
+    from algorithms.d2d_ppo import D2DPPO
+    from envs.combinatorial_env import CombinatorialEnv
+    N, E = 256, 32
+    out = []
+    for carry in (False, True):
+        p5 = dict(n_agents=N, n_channels=8, deadlines=np.full(N, 7), lbdas=np.full(N, 1 / 14), period=None,
+                  arrival_probs=None, offsets=None, episode_length=200, traffic_model="aperiodic",
+                  periodic_devices=[], channel_switch=np.ones((N, 8)) * 0.8)
+        env = CombinatorialEnv(**p5, n_envs=E, device="cuda", seed=61)
+        torch.manual_seed(7)
+        lr = D2DPPO(env, hidden_size=64, gamma=0.4, policy_lr=3e-4, value_lr=1e-3, beta_entropy=0.01, device="cuda",
+                    useRNN=True, combinatorial=True, history_len=N, early_stopping=False)
+        assert lr._gru_ok()
+        lr.gru_carry = carry
+        lr.graph_rollout = graph
+        ro = lr._rollout(E)
+        torch.cuda.synchronize()
+        out.append((ro.obs.data.clone(), ro.actions.clone(), ro.logp.clone(), ro.rewards.clone()))
+    for x, y, name in zip(out[0], out[1], ("record", "actions", "logp", "rewards")):
+        assert torch.equal(x, y), name
