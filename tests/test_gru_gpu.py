@@ -648,15 +648,14 @@ def test_gru_carried_state_equals_recompute(case, deterministic, policy_impl):
 
 def test_gru_carry_refuses_a_window_that_does_not_extend():
     from d2dhip import gru
-    from d2dhip._lib import D2DHipError
     p, dims = make_net(2, 12, 16, 4, seed=1)
     pd = {k: v.to("cuda").contiguous() for k, v in p.items()}
     obs = make_obs(8, 16, 2, 12, dims, seed=1).to("cuda").contiguous()
     hc = torch.zeros((gru.carry_floats(pd, 16, 3, 8),), device="cuda")
     for slot in (0, 3, 8):  # an episode's first slot; positions >= history_len (3)
-        with pytest.raises(D2DHipError):
+        with pytest.raises(ValueError, match="does not extend"):  # D2D_EINVAL from d2d_policy_gru_carry
             gru.policy(pd, obs, "softmax", 3, 8, slot, 1, hcarry=hc, carry_in=True)
-    with pytest.raises(ValueError):
+    with pytest.raises(ValueError, match="one unpadded slot"):
         gru.policy(pd, obs, "softmax", 3, 8, 1, 2, hcarry=hc, carry_in=True)
 
 

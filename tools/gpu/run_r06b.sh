@@ -2,7 +2,7 @@
 # usage (GPU box): bash tools/gpu/run_r06b.sh <commit>
 R="$GRAFT_REPO_ROOT"; cd "$R" || exit 9
 O="$R/gpurun_out/r06b"; mkdir -p "$O"
-timeout -k 10 600 python3 -u -m pytest tests/test_gru_gpu.py -k "carr" tests/test_fused_slot_gpu.py -m gpu -v \
+timeout -k 10 600 python3 -u -m pytest tests/test_gru_gpu.py tests/test_fused_slot_gpu.py -k "carr or fused_slot" -m gpu -v \
   --timeout 300 --timeout-method thread -p no:cacheprovider > "$O/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed" "$O/pytest_gpu.log" | tail -3
 [ $rc -eq 0 ] || exit $rc
