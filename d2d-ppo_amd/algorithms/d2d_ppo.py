@@ -417,8 +417,12 @@ class D2DPPO(BatchedLearnerBase):
             with torch.no_grad():
                 sums = part.sum(0)                                                      # db1 | dW2 | db2 | sum d^2
                 value_loss = sums[2 * H + 1] / v.numel()
-                g = self._dw1_gemm_bm(dhm, ro.state_bf16)[:, :l1.weight.shape[1]]       # [3H][S]
-                grads = {l1.weight: (g[2 * H:] + g[H:2 * H]) + g[:H], l1.bias: sums[:H], l2.weight: sums[H:2 * H],
+                if self.critic_dw1_hip:
+                    gw1 = self._dw1_hip(dhm, ro.state_bf16, H, l1.weight.shape[1])              # [H][S]
+                else:
+                    g = self._dw1_gemm_bm(dhm, ro.state_bf16)[:, :l1.weight.shape[1]]   # [3H][S]
+                    gw1 = (g[2 * H:] + g[H:2 * H]) + g[:H]
+                grads = {l1.weight: gw1, l1.bias: sums[:H], l2.weight: sums[H:2 * H],
                          l2.bias: sums[2 * H:2 * H + 1]}
                 for prm, gr in grads.items():
                     prm.grad = gr.reshape(prm.shape).contiguous()
@@ -450,6 +454,25 @@ class D2DPPO(BatchedLearnerBase):
             for prm, gr in grads.items():
                 prm.grad = gr.reshape(prm.shape).contiguous()
         return value_loss
+
+    # round 6: dW1 from the fused forward's dhm on the hand-written bf16 MFMA kernel (d2d_central_critic_dw1: the three
+    # parts accumulated in one accumulator, no [3H][S] partial products, no hipBLASLt); D2D_CRITIC_DW1_HIP=0 keeps the
+    # split-K bmm (A/B)
+    critic_dw1_hip = os.environ.get("D2D_CRITIC_DW1_HIP", "1") != "0"
+
+    def _dw1_hip(self, dhm, xb, H, S):
+        """dW1 = sum_b dpre_b x_b^T [H][S] fp32 from dpre's parts dhm [B][3H] and the bf16 operand xb [B][ldx]."""
+        from d2dhip import _lib
+        lib = _lib.require_gpu()
+        B, ldx = xb.shape[0], xb.shape[1]
+        n = int(lib.d2d_central_critic_dw1_workspace(H, B, S, ldx))
+        ws = getattr(self, "_dw1_ws", None)
+        if ws is None or ws.numel() < max(n, 1) or ws.device != xb.device:
+            ws = self._dw1_ws = torch.empty((max(n, 1),), dtype=torch.float32, device=xb.device)
+        out = torch.empty((H, S), dtype=torch.float32, device=xb.device)
+        _lib.check(lib.d2d_central_critic_dw1(H, B, S, ldx, xb.data_ptr(), dhm.data_ptr(), ws.data_ptr(), ws.numel(),
+                                              out.data_ptr(), _lib.stream_ptr()), "d2d_central_critic_dw1")
+        return out
 
     @staticmethod
     def _dw1_gemm_bm(dhm, xb):

@@ -68,6 +68,13 @@ __device__ __forceinline__ uint32_t rne_pk(float a, float b) {
   return __builtin_bit_cast(uint32_t, v);
 }
 __device__ __forceinline__ float bf_lo(uint32_t p) { return __uint_as_float(p << 16); }
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+// two transposing LDS reads (four bf16 each) as one MFMA operand
+__device__ __forceinline__ bf16x8 cat_tr16(v4i16 a, v4i16 b) {
+  const uint2 x = __builtin_bit_cast(uint2, a), y = __builtin_bit_cast(uint2, b);
+  const u32x4v v = {x.x, x.y, y.x, y.y};
+  return __builtin_bit_cast(bf16x8, v);
+}
 __device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 0xFFFF0000u); }
 
 #ifndef D2D_CRITIC_WAVES
@@ -362,6 +369,171 @@ __global__ __launch_bounds__(64 * D2D_CRITIC_WAVES, 8 / D2D_CRITIC_WAVES) void c
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// dW1 = sum_b dpre_b x_b^T (d2d_ppo.py:440-446, value_loss.backward() into linear1.weight) on v_mfma_f32_16x16x32_bf16:
+// A = dpre's three RNE parts [B][3H] (the forward's dhm, sample-major), B = the bf16 state operand xb [B][ldx]; the
+// three parts accumulate into ONE accumulator (the part index is a further k-slot), so the kernel emits dW1 itself
+// rather than [3H][S] partial products summed afterwards (the hipBLASLt split-K bmm of rounds 4-5).
+// Both operands are sample-major and the contraction runs over samples, so every K step of 32 samples goes through
+// LDS: the rows of xb's column block and of dhm are copied in (16-byte / 8-byte coalesced loads, prefetched into
+// registers one step ahead, double-buffered images) and read back with ds_read_b64_tr_b16, which delivers 4 samples
+// of one column per lane -- the A fragment of a hidden unit and the B fragment of a state feature.  k-slot order of
+// lane group g: samples 4g .. 4g + 3, then 16 + 4g .. 16 + 4g + 3 (the same for both operands).  Image rows are
+// padded by 32 bytes so that the two 16-lane groups of a 32-lane half read 8 distinct 8-bank slots (conflict-free).
+// Mapping: a workgroup (4 waves) owns a column block of 64 NF features (wave w: feature tiles w NF .. w NF + NF - 1,
+// every hidden tile) and a contiguous range of K steps; its fp32 partial [H][S] goes to the workspace and
+// critic_dw1_reduce_kernel sums the KS partials in fixed order (deterministic, no atomics).  XCD-aware order: the
+// column blocks of one K range are consecutive on one XCD, so they share its dhm rows in that XCD's L2.
+constexpr int kDw1Ws = 512;  // workgroups per launch (2 per CU), a multiple of the 8 XCDs
+
+template <int HT, int NF>
+struct Dw1Cfg {
+  static constexpr int WC = 4 * NF * 16;          // columns per workgroup
+  static constexpr int XS = WC + 16;              // x image row stride (bf16): +32 bytes
+  static constexpr int DS = 3 * 16 * HT + 16;     // dhm image row stride (bf16)
+  static constexpr int XCH = 32 * WC / 8 / 256;   // 16-byte x chunks per thread per K step
+};
+
+struct Dw1Args {
+  int H, S, CB, KS, steps_per;
+  int64_t B, ldx;
+  const uint16_t* xb;
+  const uint16_t* dhm;
+  float* partial;  // [KS][H][S]
+};
+
+template <int HT, int NF>
+__global__ __launch_bounds__(256, 2) void critic_dw1_kernel(Dw1Args a) {
+  using C = Dw1Cfg<HT, NF>;
+  typedef __attribute__((address_space(3))) v4i16* lds_v4i16;
+  __shared__ __attribute__((aligned(16))) uint16_t xim[2][32 * C::XS];
+  __shared__ __attribute__((aligned(16))) uint16_t dim_[2][32 * C::DS];
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, i = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-aware: workgroup id -> (xcd, local); a K range's CB column blocks run consecutively on one XCD
+  const int id = blockIdx.x, per = (int)gridDim.x / 8;
+  const int xcd = id % 8, local = id / 8;
+  const int cb = local % a.CB, kc = xcd * (per / a.CB) + local / a.CB;
+  const int H = a.H, H3 = 3 * H;
+  const int64_t steps_total = (a.B + 31) / 32;
+  const int64_t st0 = (int64_t)kc * a.steps_per;
+  const int64_t st1 = std::min<int64_t>(st0 + a.steps_per, steps_total);
+  const int nsteps = (int)std::max<int64_t>(0, st1 - st0);
+  const int64_t kb = st0 * 32;  // first sample
+  const int col0 = cb * C::WC;
+  // range-checked descriptors from the workgroup's first sample (rows past B read 0)
+  const int64_t xrest = (a.B - kb) * a.ldx * 2 - 2 * (int64_t)col0;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.xb + (xrest > 0 ? kb * a.ldx + col0 : 0)), 0,
+      xrest <= 0 ? 0u : xrest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)xrest, 0x00020000);
+  const int64_t drest = (a.B - kb) * H3 * 2;
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t*>(a.dhm + (drest > 0 ? kb * H3 : 0)), 0,
+      drest <= 0 ? 0u : drest > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)drest, 0x00020000);
+  // dhm's pad columns (units H .. 16 HT - 1 of each part) are never written by the copies: zero them once
+  for (int e = tid; e < 2 * 32 * C::DS; e += 256) (&dim_[0][0])[e] = 0;
+  // per-thread copy plan, offsets computed once: x chunk j = row rx, 16-byte column chunk cx of the block; dhm 8-byte
+  // chunk q of the 32 x (3H / 4) grid of a step (part p = 4c / H, unit h), placed in its part's 16 HT-unit slot
+  constexpr int CPR = C::WC / 8;       // 16-byte chunks per x row
+  constexpr int NDM = 3 * HT / 2;      // 8-byte dhm chunks per thread at most (H = 16 HT)
+  uint32_t xg[C::XCH], xl[C::XCH], dg[NDM], dl[NDM];
+#pragma unroll
+  for (int j = 0; j < C::XCH; ++j) {
+    const int c = tid + 256 * j, rx = c / CPR, cx = c % CPR;
+    xg[j] = (uint32_t)(((int64_t)rx * a.ldx + 8 * cx) * 2);
+    xl[j] = (uint32_t)(rx * C::XS + 8 * cx);
+  }
+  const int DQ = H3 / 4;               // 8-byte dhm chunks per row
+  const int nq = 32 * DQ;
+#pragma unroll
+  for (int j = 0; j < NDM; ++j) {
+    const int q = min(tid + 256 * j, nq - 1);  // (threads past the grid repeat its last chunk: same value, same place)
+    const int r = q / DQ, c = q - r * DQ;
+    const int p = (4 * c) / H, h = 4 * c - p * H;
+    dg[j] = (uint32_t)((r * H3 + 4 * c) * 2);
+    dl[j] = (uint32_t)(r * C::DS + p * 16 * HT + h);
+  }
+  const uint32_t xstep = (uint32_t)(32 * a.ldx * 2), dstep = (uint32_t)(32 * H3 * 2);
+  u32x4v xv[C::XCH];
+  uint2 dv[NDM];
+  auto load = [&](int step) {
+    const uint32_t xb0 = (uint32_t)step * xstep, db0 = (uint32_t)step * dstep;
+#pragma unroll
+    for (int j = 0; j < C::XCH; ++j) xv[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, xb0 + xg[j], 0, 0);
+#pragma unroll
+    for (int j = 0; j < NDM; ++j) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(dr, db0 + dg[j], 0, 0);
+      dv[j] = make_uint2(v[0], v[1]);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < C::XCH; ++j) *reinterpret_cast<u32x4v*>(&xim[buf][xl[j]]) = xv[j];
+#pragma unroll
+    for (int j = 0; j < NDM; ++j) *reinterpret_cast<uint2*>(&dim_[buf][dl[j]]) = dv[j];
+  };
+  f32x4 acc[HT][NF];
+#pragma unroll
+  for (int t = 0; t < HT; ++t)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) acc[t][f] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // the zeroed pads before any copy lands
+  if (nsteps > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  const int ra = 4 * g + (i >> 2), ca = 4 * (i & 3);  // this lane's row / column offset of a transposing read
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nsteps) load(s + 1);
+    const uint16_t* X = xim[buf];
+    const uint16_t* D = dim_[buf];
+    bf16x8 bx[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const int col = (wave * NF + f) * 16 + ca;
+      bx[f] = cat_tr16(__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(&X[ra * C::XS + col])),
+                       __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(&X[(16 + ra) * C::XS + col])));
+    }
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int p = 2; p >= 0; --p) {  // smallest part first
+        const int col = p * 16 * HT + 16 * t + ca;
+        const bf16x8 ad = cat_tr16(__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(&D[ra * C::DS + col])),
+                                   __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16)(&D[(16 + ra) * C::DS + col])));
+#pragma unroll
+        for (int f = 0; f < NF; ++f) acc[t][f] = mfma_bf16(ad, bx[f], acc[t][f]);
+      }
+    if (s + 1 < nsteps) store(buf ^ 1);  // buffer buf ^ 1 was last read in step s - 1, before the last barrier
+    __syncthreads();
+  }
+  // the partial: lane (g, i) of tile (t, f) holds hidden 16 t + 4 g + r, feature col0 + (wave NF + f) 16 + i
+  float* out = a.partial + (size_t)kc * H * a.S;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    const int sc = col0 + (wave * NF + f) * 16 + i;
+#pragma unroll
+    for (int t = 0; t < HT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int h = 16 * t + 4 * g + r;
+        if (h < H && sc < a.S) out[(size_t)h * a.S + sc] = acc[t][f][r];
+      }
+  }
+}
+
+// dW1[h][s] = sum over the KS partials, in index order
+__global__ __launch_bounds__(256) void critic_dw1_reduce_kernel(int64_t n, int KS, const float* __restrict__ partial,
+                                                                float* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  float v = 0.f;
+  for (int k = 0; k < KS; ++k) v += partial[(size_t)k * n + e];
+  out[e] = v;
+}
+
 }  // namespace d2d
 
 using namespace d2d;
@@ -417,6 +589,60 @@ extern "C" int d2d_central_critic_fwd(int32_t H, int64_t B, int32_t S, int64_t l
     hipLaunchKernelGGL(critic_w1_image_kernel<8>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
     hipLaunchKernelGGL((critic_fwd_kernel<8, 2, 1>), dim3(G), dim3(64 * D2D_CRITIC_WAVES), 0, s, a);
   }
+  D2D_CHECK_HIP(hipGetLastError());
+  return D2D_OK;
+}
+
+// ---- dW1 (ABI 14)
+static int dw1_nf(int ht) { return ht <= 4 ? 4 : 2; }
+// K ranges: a multiple of 8 (the XCD-aware mapping), kDw1Ws workgroups in all where the column blocks allow, and a
+// workgroup's rows within the buffer descriptors' 2 GB offset range
+static void dw1_plan(int H, int64_t B, int S, int64_t ldx, int& CB, int& KS, int& steps_per) {
+  const int ht = critic_ht(H);
+  const int wc = 64 * dw1_nf(ht);
+  CB = (S + wc - 1) / wc;
+  KS = std::max(8, (kDw1Ws / std::max(CB, 1)) / 8 * 8);
+  const int64_t steps = (B + 31) / 32;
+  for (;;) {
+    steps_per = (int)std::max<int64_t>(1, (steps + KS - 1) / KS);
+    if ((int64_t)steps_per * 32 * std::max<int64_t>(ldx, 3 * H) * 2 < 0x7FFFFFFF || KS >= (1 << 20)) break;
+    KS *= 2;
+  }
+}
+
+extern "C" int64_t d2d_central_critic_dw1_workspace(int32_t H, int64_t B, int32_t S, int64_t ldx) {
+  if (critic_ht(H) == 0 || H % 4 || B < 0 || S < 1 || ldx < S) return -1;
+  int CB, KS, sp;
+  dw1_plan(H, B, S, ldx, CB, KS, sp);
+  return (int64_t)KS * H * S;
+}
+
+extern "C" int d2d_central_critic_dw1(int32_t H, int64_t B, int32_t S, int64_t ldx, const uint16_t* xb,
+                                      const uint16_t* dhm, float* workspace, int64_t workspace_floats, float* dw1,
+                                      void* stream) {
+  const int ht = critic_ht(H);
+  if (ht == 0 || H % 4) { d2d_set_error("d2d_central_critic_dw1: hidden=%d (a multiple of 4 in [4, 128])", H); return D2D_EUNSUPPORTED; }
+  if (B < 0 || S < 1 || ldx < S || (ldx & 7) || !dw1 || (B > 0 && (!xb || !dhm || !workspace)) ||
+      (reinterpret_cast<uintptr_t>(xb) & 15) || (reinterpret_cast<uintptr_t>(dhm) & 7) ||
+      workspace_floats < d2d_central_critic_dw1_workspace(H, B, S, ldx)) {
+    d2d_set_error("d2d_central_critic_dw1: bad arguments (ldx a multiple of 8 >= S, 16-byte aligned operand, 8-byte "
+                  "aligned dhm, workspace of d2d_central_critic_dw1_workspace floats)");
+    return D2D_EINVAL;
+  }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (B == 0) {
+    D2D_CHECK_HIP(hipMemsetAsync(dw1, 0, sizeof(float) * (size_t)H * S, s));
+    return D2D_OK;
+  }
+  Dw1Args a{};
+  dw1_plan(H, B, S, ldx, a.CB, a.KS, a.steps_per);
+  a.H = H; a.S = S; a.B = B; a.ldx = ldx; a.xb = xb; a.dhm = dhm; a.partial = workspace;
+  const dim3 grid((unsigned)(a.CB * a.KS));
+  if (ht == 2) hipLaunchKernelGGL((critic_dw1_kernel<2, 4>), grid, dim3(256), 0, s, a);
+  else if (ht == 4) hipLaunchKernelGGL((critic_dw1_kernel<4, 4>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((critic_dw1_kernel<8, 2>), grid, dim3(256), 0, s, a);
+  const int64_t n = (int64_t)H * S;
+  hipLaunchKernelGGL(critic_dw1_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, a.KS, workspace, dw1);
   D2D_CHECK_HIP(hipGetLastError());
   return D2D_OK;
 }

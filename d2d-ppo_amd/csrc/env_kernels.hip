@@ -861,6 +861,9 @@ __global__ __launch_bounds__(kMaxAgents) void chsel_kernel(EnvArgs a) {
 //   F = sum d + N + 1); state = [concat_k B'[k,:d_k], H', ack] (204-205).
 // Counters: sel_quality = channel_errors, sel_count = n_collisions.
 // =====================================================================
+#ifndef D2D_SINGLE_FLAT
+#define D2D_SINGLE_FLAT 0  // 1: obs emitted flat over the block's range (A/B)
+#endif
 template <int DW, bool LARGE>
 __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -1009,7 +1012,41 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
       for (int le = 0; le < nenv; ++le) st_stream(o + (size_t)le * env_stride, value(le, word, shift), nt);
     }
   };
+#if D2D_SINGLE_FLAT
+  // flat obs emission: the block's obs range [nenv][N][F] is contiguous, so every lane stores float4 number
+  // tid, tid + blockDim, ... of it (all lanes busy, each wave-store one contiguous 1 KB); the column's gather code
+  // is read per float4 (L1 / L2-resident table)
+  if (a.obs && nenv > 0 && ((N * F) & 3) == 0 && (reinterpret_cast<uintptr_t>(a.obs) & 15) == 0) {
+    const int c4 = (N * F) >> 2, total = nenv * c4;
+    const int step = blockDim.x, dle = step / c4, dr = step - dle * c4;
+    int le = threadIdx.x / c4, r4 = threadIdx.x - le * c4;
+    float4* o = reinterpret_cast<float4*>(a.obs + (size_t)env0 * N * F);
+    for (int idx = threadIdx.x; idx < total; idx += step) {
+      const int4 c = reinterpret_cast<const int4*>(a.gather)[r4];
+      int w0, w1, w2, w3, s0, s1, s2, s3;
+      decode(c.x, w0, s0);
+      decode(c.y, w1, s1);
+      decode(c.z, w2, s2);
+      decode(c.w, w3, s3);
+      const float4 v = make_float4(value(le, w0, s0), value(le, w1, s1), value(le, w2, s2), value(le, w3, s3));
+      if (nt) {
+        __builtin_nontemporal_store(v.x, &o[idx].x);
+        __builtin_nontemporal_store(v.y, &o[idx].y);
+        __builtin_nontemporal_store(v.z, &o[idx].z);
+        __builtin_nontemporal_store(v.w, &o[idx].w);
+      } else {
+        o[idx] = v;
+      }
+      le += dle;
+      r4 += dr;
+      if (r4 >= c4) { r4 -= c4; ++le; }
+    }
+  } else if (a.obs && nenv > 0) {
+    emit(a.obs + (size_t)env0 * N * F, (size_t)N * F, a.gather, N * F);
+  }
+#else
   if (a.obs && nenv > 0) emit(a.obs + (size_t)env0 * N * F, (size_t)N * F, a.gather, N * F);
+#endif
   if (a.state && nenv > 0)
     emit(a.state + (size_t)env0 * a.state_stride, (size_t)a.state_stride, a.gather + (size_t)N * F, a.S);
 }

@@ -151,6 +151,9 @@ _SIGS = {
     "d2d_central_critic_image_bytes": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32]),
     "d2d_central_critic_fwd": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, _p, _p, _p,
                                                _p, _p, _p, _p, _p, _p, _p, ctypes.c_int32, _p]),
+    "d2d_central_critic_dw1_workspace": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64]),
+    "d2d_central_critic_dw1": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, _p, _p, _p,
+                                               ctypes.c_int64, _p, _p]),
     "d2d_policy_gru": (ctypes.c_int, [ctypes.POINTER(GruDesc), ctypes.c_int32, _p, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, _p, ctypes.c_uint32, ctypes.c_int32, _p, _p, _p]),
     "d2d_gru_carry_floats": (ctypes.c_int64, [ctypes.POINTER(GruDesc)]),

@@ -50,7 +50,7 @@ extern "C" {
                               10: d2d_states_to_bf16_padded, d2d_critic_dpre_split3;
                               11: D2D_OPT_CRITIC_GRAD_ROWS; 12: d2d_ppo_critic_grad_values, d2d_central_critic_*;
                               13: d2d_comb_policy_fused_step, D2D_OPT_FUSED_SLICE, d2d_env_out.state_bf16;
-                              14: d2d_policy_gru_carry, d2d_gru_carry_floats */
+                              14: d2d_policy_gru_carry, d2d_gru_carry_floats, d2d_central_critic_dw1 */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -391,6 +391,16 @@ int64_t d2d_central_critic_image_bytes(int32_t hidden, int32_t S);
 int d2d_central_critic_fwd(int32_t hidden, int64_t B, int32_t S, int64_t ldx, const uint16_t* xb, const float* w1,
                            const float* b1, const float* w2, const float* b2, const float* ret, void* w1img,
                            float* values, uint16_t* dhm, float* partial, int32_t G, void* stream);
+
+/* dW1 = sum_b dpre_b x_b^T of the same critic (d2d_ppo.py:440-446: value_loss.backward() into linear1.weight) from
+ * d2d_central_critic_fwd's dhm [B][3H] (the three RNE parts of dpre, all accumulated: the result is dW1 itself) and
+ * the operand xb [B][ldx] (as d2d_central_critic_fwd: bf16, columns [S, ldx) zero, every element finite, 16-byte
+ * aligned), on bf16 MFMAs through LDS (critic_kernels.hip; ABI 14, replacing the hipBLASLt split-K bmm of rounds 4-5).
+ * dw1: [H][S] fp32 (overwritten).  workspace: d2d_central_critic_dw1_workspace(H, B, S, ldx) floats of device scratch
+ * (the per-K-range partials, summed in fixed order: deterministic).  H a multiple of 4 in [4, 128]. */
+int64_t d2d_central_critic_dw1_workspace(int32_t hidden, int64_t B, int32_t S, int64_t ldx);
+int d2d_central_critic_dw1(int32_t hidden, int64_t B, int32_t S, int64_t ldx, const uint16_t* xb, const uint16_t* dhm,
+                           float* workspace, int64_t workspace_floats, float* dw1, void* stream);
 
 /* ---- GRU window policies (the reference's RNN module, algorithms/ippo.py:14-51 == d2d_ppo.py:24-59) ----
  * Per agent: torch.nn.GRU(F, H) weights w_ih [N][3H][F], w_hh [N][3H][H], b_ih, b_hh [N][3H] (gate order
