@@ -529,9 +529,17 @@ __global__ __launch_bounds__(256) void critic_dw1_reduce_kernel(int64_t n, int K
                                                                 float* __restrict__ out) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e >= n) return;
-  float v = 0.f;
-  for (int k = 0; k < KS; ++k) v += partial[(size_t)k * n + e];
-  out[e] = v;
+  // four interleaved chains (k mod 4), combined in a fixed order: independent loads in flight, deterministic
+  float v0 = 0.f, v1 = 0.f, v2 = 0.f, v3 = 0.f;
+  int k = 0;
+  for (; k + 4 <= KS; k += 4) {
+    v0 += partial[(size_t)k * n + e];
+    v1 += partial[(size_t)(k + 1) * n + e];
+    v2 += partial[(size_t)(k + 2) * n + e];
+    v3 += partial[(size_t)(k + 3) * n + e];
+  }
+  for (; k < KS; ++k) v0 += partial[(size_t)k * n + e];
+  out[e] = (v0 + v1) + (v2 + v3);
 }
 
 }  // namespace d2d
@@ -594,12 +602,14 @@ extern "C" int d2d_central_critic_fwd(int32_t H, int64_t B, int32_t S, int64_t l
 }
 
 // ---- dW1 (ABI 14)
-static int dw1_nf(int ht) { return ht <= 4 ? 4 : 2; }
+// feature tiles per wave: 4 (256 columns per workgroup) unless the state is narrower than 160 columns (configs[1]'s
+// S = 117, the sweep's 8 agents: 128) or the hidden tiles are 8 (register budget)
+static int dw1_nf(int ht, int S) { return ht <= 4 && S > 160 ? 4 : 2; }
 // K ranges: a multiple of 8 (the XCD-aware mapping), kDw1Ws workgroups in all where the column blocks allow, and a
 // workgroup's rows within the buffer descriptors' 2 GB offset range
 static void dw1_plan(int H, int64_t B, int S, int64_t ldx, int& CB, int& KS, int& steps_per) {
   const int ht = critic_ht(H);
-  const int wc = 64 * dw1_nf(ht);
+  const int wc = 64 * dw1_nf(ht, S);
   CB = (S + wc - 1) / wc;
   KS = std::max(8, (kDw1Ws / std::max(CB, 1)) / 8 * 8);
   const int64_t steps = (B + 31) / 32;
@@ -638,9 +648,16 @@ extern "C" int d2d_central_critic_dw1(int32_t H, int64_t B, int32_t S, int64_t l
   dw1_plan(H, B, S, ldx, a.CB, a.KS, a.steps_per);
   a.H = H; a.S = S; a.B = B; a.ldx = ldx; a.xb = xb; a.dhm = dhm; a.partial = workspace;
   const dim3 grid((unsigned)(a.CB * a.KS));
-  if (ht == 2) hipLaunchKernelGGL((critic_dw1_kernel<2, 4>), grid, dim3(256), 0, s, a);
-  else if (ht == 4) hipLaunchKernelGGL((critic_dw1_kernel<4, 4>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((critic_dw1_kernel<8, 2>), grid, dim3(256), 0, s, a);
+  const int nf = dw1_nf(ht, S);
+  if (ht == 2) {
+    if (nf == 4) hipLaunchKernelGGL((critic_dw1_kernel<2, 4>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((critic_dw1_kernel<2, 2>), grid, dim3(256), 0, s, a);
+  } else if (ht == 4) {
+    if (nf == 4) hipLaunchKernelGGL((critic_dw1_kernel<4, 4>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((critic_dw1_kernel<4, 2>), grid, dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((critic_dw1_kernel<8, 2>), grid, dim3(256), 0, s, a);
+  }
   const int64_t n = (int64_t)H * S;
   hipLaunchKernelGGL(critic_dw1_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, a.KS, workspace, dw1);
   D2D_CHECK_HIP(hipGetLastError());

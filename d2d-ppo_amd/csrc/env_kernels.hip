@@ -861,9 +861,6 @@ __global__ __launch_bounds__(kMaxAgents) void chsel_kernel(EnvArgs a) {
 //   F = sum d + N + 1); state = [concat_k B'[k,:d_k], H', ack] (204-205).
 // Counters: sel_quality = channel_errors, sel_count = n_collisions.
 // =====================================================================
-#ifndef D2D_SINGLE_FLAT
-#define D2D_SINGLE_FLAT 0  // 1: obs emitted flat over the block's range (A/B)
-#endif
 template <int DW, bool LARGE>
 __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -875,6 +872,11 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
   const uint64_t genv = a.env_base + (uint64_t)L.env;
   const bool env_ok = L.env < a.E;
 
+  // this lane's first obs gather codes (four columns), issued before the step so that their L2 latency hides behind
+  // it instead of opening the emission phase (the obs emission below: column quad r4 = threadIdx.x first)
+  int4 c_first = make_int4(0, 0, 0, 0);
+  const bool have_first = a.obs && (int)threadIdx.x < ((N * F) >> 2);
+  if (have_first) c_first = reinterpret_cast<const int4*>(a.gather)[threadIdx.x];
   Row<DW> b;
 #pragma unroll
   for (int i = 0; i < DW; ++i) b.w[i] = 0;
@@ -979,11 +981,11 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
     if (word >= 0) return (float)((rows0[le * NW + word] >> shift) & 0xFFu);
     return word == -1 ? (float)cnt0[le * 4 + 2] : 0.f;
   };
-  auto emit = [&](float* base, size_t env_stride, const int* codes, int cols) {
+  auto emit = [&](float* base, size_t env_stride, const int* codes, int cols, int4 first, bool pre) {
     const bool vec = (cols & 3) == 0 && (env_stride & 3) == 0 && (reinterpret_cast<uintptr_t>(base) & 15) == 0;
     if (vec) {  // 16-byte stores: four columns per lane
       for (int r4 = threadIdx.x; r4 < (cols >> 2); r4 += blockDim.x) {
-        const int4 c = reinterpret_cast<const int4*>(codes)[r4];
+        const int4 c = pre && r4 == (int)threadIdx.x ? first : reinterpret_cast<const int4*>(codes)[r4];
         int w0, w1, w2, w3, s0, s1, s2, s3;
         decode(c.x, w0, s0);
         decode(c.y, w1, s1);
@@ -1012,43 +1014,10 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
       for (int le = 0; le < nenv; ++le) st_stream(o + (size_t)le * env_stride, value(le, word, shift), nt);
     }
   };
-#if D2D_SINGLE_FLAT
-  // flat obs emission: the block's obs range [nenv][N][F] is contiguous, so every lane stores float4 number
-  // tid, tid + blockDim, ... of it (all lanes busy, each wave-store one contiguous 1 KB); the column's gather code
-  // is read per float4 (L1 / L2-resident table)
-  if (a.obs && nenv > 0 && ((N * F) & 3) == 0 && (reinterpret_cast<uintptr_t>(a.obs) & 15) == 0) {
-    const int c4 = (N * F) >> 2, total = nenv * c4;
-    const int step = blockDim.x, dle = step / c4, dr = step - dle * c4;
-    int le = threadIdx.x / c4, r4 = threadIdx.x - le * c4;
-    float4* o = reinterpret_cast<float4*>(a.obs + (size_t)env0 * N * F);
-    for (int idx = threadIdx.x; idx < total; idx += step) {
-      const int4 c = reinterpret_cast<const int4*>(a.gather)[r4];
-      int w0, w1, w2, w3, s0, s1, s2, s3;
-      decode(c.x, w0, s0);
-      decode(c.y, w1, s1);
-      decode(c.z, w2, s2);
-      decode(c.w, w3, s3);
-      const float4 v = make_float4(value(le, w0, s0), value(le, w1, s1), value(le, w2, s2), value(le, w3, s3));
-      if (nt) {
-        __builtin_nontemporal_store(v.x, &o[idx].x);
-        __builtin_nontemporal_store(v.y, &o[idx].y);
-        __builtin_nontemporal_store(v.z, &o[idx].z);
-        __builtin_nontemporal_store(v.w, &o[idx].w);
-      } else {
-        o[idx] = v;
-      }
-      le += dle;
-      r4 += dr;
-      if (r4 >= c4) { r4 -= c4; ++le; }
-    }
-  } else if (a.obs && nenv > 0) {
-    emit(a.obs + (size_t)env0 * N * F, (size_t)N * F, a.gather, N * F);
-  }
-#else
-  if (a.obs && nenv > 0) emit(a.obs + (size_t)env0 * N * F, (size_t)N * F, a.gather, N * F);
-#endif
+  if (a.obs && nenv > 0) emit(a.obs + (size_t)env0 * N * F, (size_t)N * F, a.gather, N * F, c_first, have_first);
   if (a.state && nenv > 0)
-    emit(a.state + (size_t)env0 * a.state_stride, (size_t)a.state_stride, a.gather + (size_t)N * F, a.S);
+    emit(a.state + (size_t)env0 * a.state_stride, (size_t)a.state_stride, a.gather + (size_t)N * F, a.S,
+         make_int4(0, 0, 0, 0), false);
 }
 
 // =====================================================================
