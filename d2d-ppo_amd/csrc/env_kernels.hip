@@ -861,55 +861,37 @@ __global__ __launch_bounds__(kMaxAgents) void chsel_kernel(EnvArgs a) {
 //   F = sum d + N + 1); state = [concat_k B'[k,:d_k], H', ack] (204-205).
 // Counters: sel_quality = channel_errors, sel_count = n_collisions.
 // =====================================================================
-// A block runs its env groups gi = blockIdx.x, blockIdx.x + gridDim.x, ... (D2D_SINGLE_ITERS groups per block): the
-// next group's state rows are loaded before the current group's obs emission, so the step's reads overlap the
-// emission's stores instead of every resident block reading, then every block writing, in lockstep (one group
-// per block measured exactly the sum of the two phases: 51 + 80 us at 64 agents x 65,536 envs,
-// tools/gpu/single_probe.py).
-#ifndef D2D_SINGLE_ITERS
-#define D2D_SINGLE_ITERS 4
-#endif
-template <int DW>
-struct SingleIn {
-  Row<DW> b;
-  uint32_t h, act, rc, dc;
-};
 template <int DW, bool LARGE>
 __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  const Lane L = lane_geometry<LARGE>(a);
   const int N = a.N, F = a.F;
-  const int epb0 = LARGE ? 1 : (int)blockDim.x / a.seg;
-  const int ngroups = (a.E + epb0 - 1) / epb0;
-  const Lane L0 = lane_geometry<LARGE>(a, blockIdx.x);
-  int* cnt = reinterpret_cast<int*>(lds) + L0.local_env * 4;
-  uint32_t* rows = reinterpret_cast<uint32_t*>(lds) + a.cnt_words + (size_t)L0.local_env * N * (DW + 1);
-  d2d_agent_entry ag{};
-  if (L0.k < N) ag = a.agents[L0.k];  // the lane's agent: the same in every group
-  auto fetch = [&](int gi, SingleIn<DW>& in) {
-    const Lane Lf = lane_geometry<LARGE>(a, gi);
-    const size_t rowf = (size_t)Lf.env * N + Lf.k;
-#pragma unroll
-    for (int i = 0; i < DW; ++i) in.b.w[i] = 0;
-    in.h = 1; in.act = 0; in.rc = 0; in.dc = 0;
-    if (Lf.active && !a.reset) {
-      load_row<DW>(in.b, a.buf + rowf * DW);
-      in.h = reinterpret_cast<const uint8_t*>(a.chan)[rowf] & 1u;
-      in.act = reinterpret_cast<const uint8_t*>(a.actions)[rowf];
-      in.rc = a.recv[rowf];
-      in.dc = a.disc[rowf];
-    }
-  };
-  SingleIn<DW> cur;
-  fetch(blockIdx.x, cur);
-  for (int gi = blockIdx.x; gi < ngroups; gi += gridDim.x) {
-  const Lane L = lane_geometry<LARGE>(a, gi);
-  SingleIn<DW> nxt = cur;
-  if (gi + (int)gridDim.x < ngroups) fetch(gi + gridDim.x, nxt);
+  int* cnt = reinterpret_cast<int*>(lds) + L.local_env * 4;
+  uint32_t* rows = reinterpret_cast<uint32_t*>(lds) + a.cnt_words + (size_t)L.local_env * N * (DW + 1);
   const size_t row = (size_t)L.env * N + L.k;
   const uint64_t genv = a.env_base + (uint64_t)L.env;
   const bool env_ok = L.env < a.E;
-  Row<DW> b = cur.b;
-  uint32_t h = cur.h, act = cur.act, rc = cur.rc, dc = cur.dc;
+
+  // this lane's first obs gather codes (four columns), issued before the step so that their L2 latency hides behind
+  // it instead of opening the emission phase (the obs emission below: column quad r4 = threadIdx.x first)
+  int4 c_first = make_int4(0, 0, 0, 0);
+  const bool have_first = a.obs && (int)threadIdx.x < ((N * F) >> 2);
+  if (have_first) c_first = reinterpret_cast<const int4*>(a.gather)[threadIdx.x];
+  Row<DW> b;
+#pragma unroll
+  for (int i = 0; i < DW; ++i) b.w[i] = 0;
+  uint32_t h = 1, act = 0, rc = 0, dc = 0;
+  d2d_agent_entry ag{};
+  if (L.active) {
+    ag = a.agents[L.k];
+    if (!a.reset) {
+      load_row<DW>(b, a.buf + row * DW);
+      h = reinterpret_cast<const uint8_t*>(a.chan)[row] & 1u;
+      act = reinterpret_cast<const uint8_t*>(a.actions)[row];
+      rc = a.recv[row];
+      dc = a.disc[row];
+    }
+  }
   if (LARGE) {
     if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
     __syncthreads();
@@ -978,7 +960,7 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
   if (L.k == 0) cnt[2] = ackv;
   __syncthreads();
   const int epb = L.envs_per_block;
-  const int env0 = LARGE ? gi : gi * epb;
+  const int env0 = LARGE ? blockIdx.x : blockIdx.x * epb;
   const int nenv = min(epb, a.E - env0);
   const bool nt = a.flags & 1u;
   const uint32_t* rows0 = reinterpret_cast<const uint32_t*>(lds) + a.cnt_words;
@@ -999,11 +981,11 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
     if (word >= 0) return (float)((rows0[le * NW + word] >> shift) & 0xFFu);
     return word == -1 ? (float)cnt0[le * 4 + 2] : 0.f;
   };
-  auto emit = [&](float* base, size_t env_stride, const int* codes, int cols) {
+  auto emit = [&](float* base, size_t env_stride, const int* codes, int cols, int4 first, bool pre) {
     const bool vec = (cols & 3) == 0 && (env_stride & 3) == 0 && (reinterpret_cast<uintptr_t>(base) & 15) == 0;
     if (vec) {  // 16-byte stores: four columns per lane
       for (int r4 = threadIdx.x; r4 < (cols >> 2); r4 += blockDim.x) {
-        const int4 c = reinterpret_cast<const int4*>(codes)[r4];
+        const int4 c = pre && r4 == (int)threadIdx.x ? first : reinterpret_cast<const int4*>(codes)[r4];
         int w0, w1, w2, w3, s0, s1, s2, s3;
         decode(c.x, w0, s0);
         decode(c.y, w1, s1);
@@ -1032,12 +1014,10 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
       for (int le = 0; le < nenv; ++le) st_stream(o + (size_t)le * env_stride, value(le, word, shift), nt);
     }
   };
-  if (a.obs && nenv > 0) emit(a.obs + (size_t)env0 * N * F, (size_t)N * F, a.gather, N * F);
+  if (a.obs && nenv > 0) emit(a.obs + (size_t)env0 * N * F, (size_t)N * F, a.gather, N * F, c_first, have_first);
   if (a.state && nenv > 0)
-    emit(a.state + (size_t)env0 * a.state_stride, (size_t)a.state_stride, a.gather + (size_t)N * F, a.S);
-  cur = nxt;
-  __syncthreads();  // the next group's LDS rows / counts overwrite this group's
-  }
+    emit(a.state + (size_t)env0 * a.state_stride, (size_t)a.state_stride, a.gather + (size_t)N * F, a.S,
+         make_int4(0, 0, 0, 0), false);
 }
 
 // =====================================================================
@@ -1175,9 +1155,7 @@ template <typename K>
 int launch(K kernel, const EnvArgs& a, int block, hipStream_t s, int kind) {
   const bool large = a.N > kWave;
   const int epb = large ? 1 : block / a.seg;
-  const int groups = (a.E + epb - 1) / epb;
-  // single_kernel loops over D2D_SINGLE_ITERS env groups per block (its reads of the next group overlap its stores)
-  const int grid = kind == D2D_ENV_SINGLE ? (groups + D2D_SINGLE_ITERS - 1) / D2D_SINGLE_ITERS : groups;
+  const int grid = (a.E + epb - 1) / epb;
   if (grid == 0) return D2D_OK;
   const size_t lds = lds_need(a, block, kind);
   int rc = set_lds(kernel, lds);
