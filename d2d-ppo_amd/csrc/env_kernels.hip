@@ -872,11 +872,6 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
   const uint64_t genv = a.env_base + (uint64_t)L.env;
   const bool env_ok = L.env < a.E;
 
-  // this lane's first obs gather codes (four columns), issued before the step so that their L2 latency hides behind
-  // it instead of opening the emission phase (the obs emission below: column quad r4 = threadIdx.x first)
-  int4 c_first = make_int4(0, 0, 0, 0);
-  const bool have_first = a.obs && (int)threadIdx.x < ((N * F) >> 2);
-  if (have_first) c_first = reinterpret_cast<const int4*>(a.gather)[threadIdx.x];
   Row<DW> b;
 #pragma unroll
   for (int i = 0; i < DW; ++i) b.w[i] = 0;
@@ -981,11 +976,11 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
     if (word >= 0) return (float)((rows0[le * NW + word] >> shift) & 0xFFu);
     return word == -1 ? (float)cnt0[le * 4 + 2] : 0.f;
   };
-  auto emit = [&](float* base, size_t env_stride, const int* codes, int cols, int4 first, bool pre) {
+  auto emit = [&](float* base, size_t env_stride, const int* codes, int cols) {
     const bool vec = (cols & 3) == 0 && (env_stride & 3) == 0 && (reinterpret_cast<uintptr_t>(base) & 15) == 0;
     if (vec) {  // 16-byte stores: four columns per lane
       for (int r4 = threadIdx.x; r4 < (cols >> 2); r4 += blockDim.x) {
-        const int4 c = pre && r4 == (int)threadIdx.x ? first : reinterpret_cast<const int4*>(codes)[r4];
+        const int4 c = reinterpret_cast<const int4*>(codes)[r4];
         int w0, w1, w2, w3, s0, s1, s2, s3;
         decode(c.x, w0, s0);
         decode(c.y, w1, s1);
@@ -1014,10 +1009,9 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
       for (int le = 0; le < nenv; ++le) st_stream(o + (size_t)le * env_stride, value(le, word, shift), nt);
     }
   };
-  if (a.obs && nenv > 0) emit(a.obs + (size_t)env0 * N * F, (size_t)N * F, a.gather, N * F, c_first, have_first);
+  if (a.obs && nenv > 0) emit(a.obs + (size_t)env0 * N * F, (size_t)N * F, a.gather, N * F);
   if (a.state && nenv > 0)
-    emit(a.state + (size_t)env0 * a.state_stride, (size_t)a.state_stride, a.gather + (size_t)N * F, a.S,
-         make_int4(0, 0, 0, 0), false);
+    emit(a.state + (size_t)env0 * a.state_stride, (size_t)a.state_stride, a.gather + (size_t)N * F, a.S);
 }
 
 // =====================================================================
