@@ -714,36 +714,47 @@ def d2denv_leg(args, rank, world, local):
     b = env.batch()
     s = b.spec
     act = b.action_buffer()
-    b.reset(want_obs=True)
-    for _ in range(10):
-        b.sample_actions(0.05, out=act)
-        b.step(act, want_obs=True)
-    steps = 100
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        if b.timestep >= env.episode_length:
-            b.reset(want_obs=True)
-        b.sample_actions(0.05, out=act)
-        evs[i][0].record()
-        b.step(act, want_obs=True)
-        evs[i][1].record()
-    torch.cuda.synchronize()
-    wall = max_over_ranks(time.perf_counter() - t0, world)
-    kern_ms = max_over_ranks(float(np.mean([a.elapsed_time(bb) for a, bb in evs])), world)
-    # algorithmic bytes of one launch: per agent row r+w (buffers 4*DW, channel 1, received 4, discarded 4),
-    # the action byte and the obs row; per env the reward and the two counters (r+w)
-    per_agent = 2 * (4 * s.DW + 1 + 8) + 1 + 4 * s.F
-    per_env = 4 + 16
-    bytes_launch = (per_agent * N + per_env) * b.E
-    achieved = bytes_launch / (kern_ms / 1e3) / 1e9
-    del env, b, act
+    from d2dhip._lib import record_bytes
+    rec = b.record_buffer(())
+
+    def run(record):
+        out_obs = rec if record else None
+        b.reset(want_obs=True, out_obs=out_obs)
+        for _ in range(10):
+            b.sample_actions(0.05, out=act)
+            b.step(act, want_obs=True, out_obs=out_obs)
+        steps = 100
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            if b.timestep >= env.episode_length:
+                b.reset(want_obs=True, out_obs=out_obs)
+            b.sample_actions(0.05, out=act)
+            evs[i][0].record()
+            b.step(act, want_obs=True, out_obs=out_obs)
+            evs[i][1].record()
+        torch.cuda.synchronize()
+        wall = max_over_ranks(time.perf_counter() - t0, world)
+        kern_ms = max_over_ranks(float(np.mean([a.elapsed_time(bb) for a, bb in evs])), world)
+        # algorithmic bytes of one launch: per agent row r+w (buffers 4*DW, channel 1, received 4, discarded 4),
+        # the action byte and the obs row (fp32: 4F; the record: record_bytes(F)); per env the reward and the two
+        # counters (r+w)
+        per_agent = 2 * (4 * s.DW + 1 + 8) + 1 + (record_bytes(s.F) if record else 4 * s.F)
+        per_env = 4 + 16
+        bytes_launch = (per_agent * N + per_env) * b.E
+        achieved = bytes_launch / (kern_ms / 1e3) / 1e9
+        return {"env_steps_per_s": args.envs * world * steps / wall, "kernel_avg_us": kern_ms * 1e3,
+                "bytes_per_launch": bytes_launch, "achieved_GBps": achieved, "hbm_frac": achieved / HBM_PEAK_GBS}
+
+    f32 = run(False)
+    recd = run(True)
+    del env, b, act, rec
     torch.cuda.empty_cache()
     out = {"agents": N, "envs_per_gpu": args.envs, "obs_dim": s.F, "neighbourhood": "ring {k-1,k,k+1}",
-           "env_steps_per_s": args.envs * world * steps / wall,
-           "kernel": "d2d::single_kernel<2, false>", "kernel_avg_us": kern_ms * 1e3,
-           "bytes_per_launch": bytes_launch, "achieved_GBps": achieved, "hbm_frac": achieved / HBM_PEAK_GBS}
+           "kernel": "d2d::single_kernel<2, false>", **f32,
+           "record": dict(recd, what="the same steps emitting the compact obs record the learners consume (ABI 14: "
+                                     f"{record_bytes(s.F)} B per agent-step instead of {4 * s.F} B of fp32 rows)")}
     pmc, rel = load_profile_json("pmc_traffic_single.json")
     if pmc and pmc.get("envs") == args.envs and pmc.get("agents") == N:
         out["traffic"] = {"bytes_per_launch": pmc.get("bytes_per_launch"),

@@ -160,7 +160,12 @@ class BatchedLearnerBase(DataParallelMixin):
     obs_record = os.environ.get("D2D_OBS_RECORD", "1") != "0"
 
     def _record_ok(self):
-        return (self.obs_record and self.kind == "comb" and bool(self.combinatorial)
+        # the combinatorial env's record, and since round 6 the D2DEnv's (categorical learners; record rows of at most
+        # 64 bytes -- the update kernels' F + 1 <= 64 -- and 64 agents, the ring / small neighbourhoods of the drivers)
+        s = self.env.spec if self.kind == "single" else None
+        env_ok = ((self.kind == "comb" and bool(self.combinatorial))
+                  or (self.kind == "single" and not self.combinatorial and s.N <= 64 and _lib_record_bytes(s.F) <= 64))
+        return (self.obs_record and env_ok
                 and (self._gru_ok() or (not self.useRNN and self._fused_ok())) and self._fused_update_ok())
 
     def _fused_update_ok(self):

@@ -871,6 +871,17 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
   const size_t row = (size_t)L.env * N + L.k;
   const uint64_t genv = a.env_base + (uint64_t)L.env;
   const bool env_ok = L.env < a.E;
+  // compact record (ABI 14): the agents' gather codes staged in LDS, one row of rec_bytes + 4 codes per agent (the pad
+  // keeps the 16-byte reads of 8 consecutive agents on distinct banks): columns < F the obs codes, column F the
+  // layer-1 bias input (-3: the byte 1), past it -2 (0)
+  const int CS = a.rec_bytes + 4;
+  int* codes_s = reinterpret_cast<int*>(lds) + a.cnt_words + (size_t)L.envs_per_block * N * (DW + 1);
+  if (a.rec) {
+    for (int idx = threadIdx.x; idx < N * CS; idx += blockDim.x) {
+      const int j = idx / CS, c = idx - j * CS;
+      codes_s[idx] = c < F ? a.gather[(size_t)j * F + c] : c == F ? -3 : -2;
+    }
+  }
 
   Row<DW> b;
 #pragma unroll
@@ -1012,6 +1023,32 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
   if (a.obs && nenv > 0) emit(a.obs + (size_t)env0 * N * F, (size_t)N * F, a.gather, N * F);
   if (a.state && nenv > 0)
     emit(a.state + (size_t)env0 * a.state_stride, (size_t)a.state_stride, a.gather + (size_t)N * F, a.S);
+  if (a.rec && L.active) {
+    // the lane's own record row [env][agent][rec_bytes]: byte c = obs column c (uint8 buffer counts and channel
+    // bits, the int8 ack), byte F = 1, zeros past it -- 32 bytes per agent-step instead of 4 F of fp32 rows
+    const int le = L.local_env;
+    const int* cj = codes_s + L.k * CS;
+    const uint32_t ackb = (uint32_t)cnt0[le * 4 + 2] & 0xFFu;
+    auto byte_at = [&](int code) -> uint32_t {
+      if (code >= 0) {
+        const int j = code >> 6, q = code & 63;
+        const int word = j * (DW + 1) + (q == 32 ? DW : (q >> 2));
+        const int shift = q == 32 ? 0 : (q & 3) * 8;
+        return (rows0[le * NW + word] >> shift) & 0xFFu;
+      }
+      return code == -1 ? ackb : code == -3 ? 1u : 0u;
+    };
+    uint4* dst = reinterpret_cast<uint4*>(a.rec + row * (size_t)a.rec_bytes);
+    for (int p16 = 0; p16 < (a.rec_bytes >> 4); ++p16) {
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int4 c4 = *reinterpret_cast<const int4*>(cj + 16 * p16 + 4 * q);
+        w[q] = byte_at(c4.x) | (byte_at(c4.y) << 8) | (byte_at(c4.z) << 16) | (byte_at(c4.w) << 24);
+      }
+      st_rec(dst + p16, w[0], w[1], w[2], w[3], nt);
+    }
+  }
 }
 
 // =====================================================================
@@ -1130,7 +1167,8 @@ size_t lds_need(const EnvArgs& a, int block, int kind) {
   const bool comb = kind == D2D_ENV_COMBINATORIAL;
   if (kind == D2D_ENV_SINGLE) {
     const int epb = large ? 1 : block / a.seg;
-    return sizeof(float) * ((size_t)a.cnt_words + (size_t)epb * a.N * (a.D <= 4 ? 2 : a.D <= 8 ? 3 : a.D <= 12 ? 4 : a.D <= 16 ? 5 : 9));
+    return sizeof(float) * ((size_t)a.cnt_words + (size_t)epb * a.N * (a.D <= 4 ? 2 : a.D <= 8 ? 3 : a.D <= 12 ? 4 : a.D <= 16 ? 5 : 9) +
+                            (a.rec ? (size_t)a.N * (a.rec_bytes + 4) : 0));
   }
   if (comb) {
     const int nwaves = block / kWave;
@@ -1231,7 +1269,9 @@ int env_args(const d2d_env_desc* d, const d2d_env_state* st, const void* actions
     }
   }
   a.rec_bytes = D2D_RECORD_BYTES(a.F);
-  if (a.rec && !comb) { d2d_set_error("obs_record is implemented for the combinatorial env only"); return D2D_EUNSUPPORTED; }
+  if (a.rec && !comb && d->env_kind != D2D_ENV_SINGLE) {
+    d2d_set_error("obs_record is implemented for the combinatorial env and the D2DEnv only"); return D2D_EUNSUPPORTED;
+  }
   if (a.rec && (reinterpret_cast<uintptr_t>(a.rec) & 15)) { d2d_set_error("obs_record must be 16-byte aligned"); return D2D_EINVAL; }
   draw_mask(d, reset ? 0 : t, a.draw);
   a.flags = store_flags();

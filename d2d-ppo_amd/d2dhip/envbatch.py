@@ -58,10 +58,11 @@ class EnvBatch:
         self._ack = None
         self._success = None
         self._record = None
-        # int8-column masks of the compact obs record (combinatorial env only)
-        self._signed_host = signed_masks(s).view(np.int32) if s.kind == COMB else None
-        self.signed = torch.from_numpy(self._signed_host).to(dev) if s.kind == COMB else None
-        self.gather = torch.from_numpy(spec.gather_map(self.lib)).to(dev) if s.kind == SINGLE else None
+        # int8-column masks of the compact obs record (combinatorial env; D2DEnv from its gather codes)
+        gather_host = spec.gather_map(self.lib) if s.kind == SINGLE else None
+        self._signed_host = (signed_masks(s, gather_host).view(np.int32) if s.kind in (COMB, SINGLE) else None)
+        self.signed = torch.from_numpy(self._signed_host).to(dev) if self._signed_host is not None else None
+        self.gather = torch.from_numpy(gather_host).to(dev) if s.kind == SINGLE else None
         # device word added to rng_step by every kernel of this batch (and by the learner's policy
         # kernel): 0 for eager calls, set before replaying a captured rollout graph
         self.rng_off = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -99,7 +100,7 @@ class EnvBatch:
 
     @property
     def record(self):
-        """Persistent compact obs record [E][N][R] (ObsRecord, combinatorial env only)."""
+        """Persistent compact obs record [E][N][R] (ObsRecord; combinatorial env and D2DEnv)."""
         if self._record is None:
             self._record = self.record_buffer(())
         return self._record
@@ -107,7 +108,7 @@ class EnvBatch:
     def record_buffer(self, lead):
         """A zeroed ObsRecord [*lead][E][N][R] for rollout buffers (slice [t] per step)."""
         if self.signed is None:
-            raise NotImplementedError("the compact obs record exists for the combinatorial env only")
+            raise NotImplementedError("the compact obs record exists for the combinatorial env and the D2DEnv only")
         r = ObsRecord.empty(tuple(lead) + (self.E,), self.spec, self.signed, self.device)
         r._host = self._signed_host
         return r

@@ -1,7 +1,8 @@
 """The compact obs record (C ABI D2D_OBS_U8, include/d2d_hip.h d2d_env_out.obs_record).
 
 The combinatorial env's observation (combinatorial_env.py:199-206) is made of packet counts (uint8
-buffer cells), channel bits and ACKs in {-1, 0, 1}: every value is an integer that fits one byte.
+buffer cells), channel bits and ACKs in {-1, 0, 1}: every value is an integer that fits one byte.  So is the
+D2DEnv's (envs/env.py:89-95: the neighbours' buffers and channel bits, the last feedback in {-1, 0, 1}; ABI 14).
 The env kernel can write each obs row as bytes, padded to 32 per chunk of 32 network inputs, and
 the policy / update / GRU kernels read it instead of the fp32 rows: 32 bytes per (env, agent) slot
 instead of 4 * obs_dim (120 at the c3 headline config).  The decoded values are the same floats,
@@ -16,11 +17,21 @@ import torch
 from . import _lib
 
 
-def signed_masks(spec):
-    """uint32 [N][R / 32] int8-column masks of a combinatorial EnvSpec: agent k's ACK columns
-    [w_k + C, w_k + 2C) (obs layout of combinatorial_env.py:199-206)."""
+def signed_masks(spec, gather=None):
+    """uint32 [N][R / 32] int8-column masks of an EnvSpec's record: combinatorial env, agent k's ACK columns
+    [w_k + C, w_k + 2C) (obs layout of combinatorial_env.py:199-206); D2DEnv (kind 'single', ABI 14), the column
+    of the agent's last feedback (env.py:94; gather code -1 of d2d_env_single_gather_map, `gather` = the host codes)."""
+    if spec.kind == "single":
+        if gather is None:
+            raise ValueError("the D2DEnv record's masks need the env's gather codes")
+        R = _lib.record_bytes(spec.F)
+        codes = np.asarray(gather)[: spec.N * spec.F].reshape(spec.N, spec.F)
+        m = np.zeros((spec.N, R // 32), dtype=np.uint64)
+        for k, col in zip(*np.nonzero(codes == -1)):
+            m[k, col // 32] |= np.uint64(1) << np.uint64(col % 32)
+        return m.astype(np.uint32)
     if spec.kind != "comb":
-        raise NotImplementedError("the compact obs record exists for the combinatorial env only")
+        raise NotImplementedError("the compact obs record exists for the combinatorial env and the D2DEnv only")
     R = _lib.record_bytes(spec.F)
     m = np.zeros((spec.N, R // 32), dtype=np.uint64)
     for k in range(spec.N):

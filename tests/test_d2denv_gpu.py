@@ -7,7 +7,8 @@
 2. Philox production mode == the numpy oracle (oracle/env_oracle.py "single")
    bit for bit, incl. N > 64 (one env per workgroup) and full neighbourhoods;
 3. the reference-API path (n_envs = 1 numpy structures, counters);
-4. the learners run on it (iPPO and D2D-PPO, one iteration + test()).
+4. the learners run on it (iPPO and D2D-PPO, one iteration + test());
+5. the compact obs record (ABI 14) decodes to the fp32 obs bit for bit.
 Bit-exact for every integer output; obs / state exact after the fp32 cast.
 """
 import glob
@@ -142,6 +143,68 @@ def test_philox_large_agent_counts(N, full):
     params = dict(n_agents=N, deadlines=d, lbdas=np.full(N, 0.05), episode_length=8, channel_switch=0.3,
                   neighbourhoods=nb)
     _philox_case(params, E=5, steps=8, seed=7, p_act=0.02)
+
+
+def _record_case(params, E, steps, seed, p_act=0.05):
+    """Two identical batches, one emitting fp32 obs rows and one the compact record (ABI 14): the decoded record is
+    the fp32 obs bit for bit at every reset and step, and the env states stay identical."""
+    from envs.env import D2DEnv  # noqa: F401
+    envs = [make(params, n_envs=E, device="cuda", seed=seed) for _ in range(2)]
+    ba, bb = envs[0].batch(), envs[1].batch()
+    rec = bb.record_buffer(())
+    L = int(params["episode_length"])
+    act = ba.action_buffer()
+    for t in range(steps):
+        if t % L == 0:
+            ra = ba.reset(want_obs=True)
+            bb.reset(want_obs=True, out_obs=rec)
+            assert torch.equal(rec.decode(), ra["obs"]), ("reset", t)
+        ba.sample_actions(p_act, out=act)
+        bb.rng_step += 1  # (the sampler's draw on the other batch)
+        ra = ba.step(act, want_obs=True)
+        bb.step(act, out_obs=rec)
+        torch.cuda.synchronize()
+        assert torch.equal(rec.decode(), ra["obs"]), t
+        for x, y in ((ba.buffers, bb.buffers), (ba.channels, bb.channels), (ba.received, bb.received),
+                     (ba.discarded, bb.discarded), (ba.reward, bb.reward)):
+            assert torch.equal(x, y), t
+    # the row's bias byte (column F) and zeros past it
+    R = rec.data.shape[-1]
+    F = ba.spec.F
+    assert torch.all(rec.data[..., F] == 1) and (R == F + 1 or torch.all(rec.data[..., F + 1:] == 0))
+
+
+@pytest.mark.parametrize("name", fixtures())
+def test_record_equals_fp32_obs(name):
+    """The D2DEnv compact record (single_kernel, ABI 14): 32 bytes per agent-step for the learners instead of 4 F of
+    fp32 rows, decoded bit-exactly to the obs the reference's env.py:89-95 layout gives (the fp32 rows are pinned to
+    the reference traces by test_replay_matches_reference)."""
+    z = np.load(os.path.join(GOLDEN, f"d2denv_{name}.npz"))
+    params = load_params(z)
+    params["episode_length"] = 7
+    _record_case(params, E=133, steps=15, seed=99)
+
+
+@pytest.mark.parametrize("N", [64, 65, 200])
+def test_record_ring_agent_counts(N):
+    d = np.array([3, 5, 7] * (N // 3) + [4] * (N % 3))
+    nb = [[(k - 1) % N, k, (k + 1) % N] for k in range(N)]
+    params = dict(n_agents=N, deadlines=d, lbdas=np.full(N, 0.1), episode_length=6, channel_switch=0.3,
+                  neighbourhoods=nb)
+    _record_case(params, E=37 if N > 64 else 1001, steps=13, seed=5, p_act=0.1)
+
+
+def test_record_too_wide_is_refused():
+    """Full neighbourhoods of 96 agents: the record's gather codes do not fit the workgroup's LDS -- refused loudly
+    (the learners keep fp32 rows there: _record_ok)."""
+    N = 96
+    params = dict(n_agents=N, deadlines=np.full(N, 7), lbdas=np.full(N, 0.1), episode_length=6, channel_switch=0.3,
+                  neighbourhoods=[list(range(N)) for _ in range(N)])
+    env = make(params, n_envs=4, device="cuda", seed=1)
+    b = env.batch()
+    rec = b.record_buffer(())
+    with pytest.raises(NotImplementedError, match="LDS"):
+        b.reset(want_obs=True, out_obs=rec)
 
 
 def test_reference_api_structures():
