@@ -877,9 +877,15 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
   const int CS = a.rec_bytes + 4;
   int* codes_s = reinterpret_cast<int*>(lds) + a.cnt_words + (size_t)L.envs_per_block * N * (DW + 1);
   if (a.rec) {
+    // pre-decoded: a row byte as (LDS word of the block's row image) | (bit shift << 16), else -1 ack / -2 zero / -3 one
     for (int idx = threadIdx.x; idx < N * CS; idx += blockDim.x) {
       const int j = idx / CS, c = idx - j * CS;
-      codes_s[idx] = c < F ? a.gather[(size_t)j * F + c] : c == F ? -3 : -2;
+      int code = c < F ? a.gather[(size_t)j * F + c] : c == F ? -3 : -2;
+      if (code >= 0) {
+        const int jj = code >> 6, q = code & 63;
+        code = (jj * (DW + 1) + (q == 32 ? DW : (q >> 2))) | ((q == 32 ? 0 : (q & 3) * 8) << 16);
+      }
+      codes_s[idx] = code;
     }
   }
 
@@ -1029,13 +1035,9 @@ __global__ __launch_bounds__(kMaxAgents) void single_kernel(EnvArgs a) {
     const int le = L.local_env;
     const int* cj = codes_s + L.k * CS;
     const uint32_t ackb = (uint32_t)cnt0[le * 4 + 2] & 0xFFu;
+    const uint32_t* rle = rows0 + le * NW;
     auto byte_at = [&](int code) -> uint32_t {
-      if (code >= 0) {
-        const int j = code >> 6, q = code & 63;
-        const int word = j * (DW + 1) + (q == 32 ? DW : (q >> 2));
-        const int shift = q == 32 ? 0 : (q & 3) * 8;
-        return (rows0[le * NW + word] >> shift) & 0xFFu;
-      }
+      if (code >= 0) return (rle[code & 0xFFFF] >> (code >> 16)) & 0xFFu;
       return code == -1 ? ackb : code == -3 ? 1u : 0u;
     };
     uint4* dst = reinterpret_cast<uint4*>(a.rec + row * (size_t)a.rec_bytes);

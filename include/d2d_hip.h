@@ -50,7 +50,7 @@ extern "C" {
                               10: d2d_states_to_bf16_padded, d2d_critic_dpre_split3;
                               11: D2D_OPT_CRITIC_GRAD_ROWS; 12: d2d_ppo_critic_grad_values, d2d_central_critic_*;
                               13: d2d_comb_policy_fused_step, D2D_OPT_FUSED_SLICE, d2d_env_out.state_bf16;
-                              14: d2d_policy_gru_carry, d2d_gru_carry_floats, d2d_central_critic_dw1 */
+                              14: d2d_policy_gru_carry, d2d_gru_carry_floats, d2d_central_critic_dw1, single obs_record */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -119,11 +119,13 @@ typedef struct d2d_env_out {  /* any field may be NULL */
     int32_t* reward;    /* [E]  |successful users| (single: the ack); broadcast to all agents by the host */
     void* ack;          /* comb int8 [E][C] in {-1,0,1}; chsel double [E][C+1]; single int8 [E] */
     uint8_t* success;   /* [E][N] 1 if agent k delivered a packet this slot */
-    /* comb only: the compact obs record [E][N][D2D_RECORD_BYTES(obs_dim)] (16-byte aligned), the obs
-     * row above one byte per column: packet counts and channel bits as uint8, the acks (columns
-     * [w_k + C, w_k + 2C)) as int8, then byte obs_dim = 1 (the networks' layer-1 bias input) and
-     * zeros.  Every obs value of this env is an integer in those ranges, so the record is exact;
-     * consumers take it with obs_format = D2D_OBS_U8. */
+    /* comb and (ABI 14) single: the compact obs record [E][N][D2D_RECORD_BYTES(obs_dim)] (16-byte aligned),
+     * the obs row above one byte per column: packet counts and channel bits as uint8, the acks (comb: columns
+     * [w_k + C, w_k + 2C); single: the last-feedback column, gather code -1) as int8, then byte obs_dim = 1
+     * (the networks' layer-1 bias input) and zeros.  Every obs value of these envs is an integer in those
+     * ranges, so the record is exact; consumers take it with obs_format = D2D_OBS_U8.  single: the agents'
+     * gather codes are staged in LDS (N * (record bytes + 4) * 4 bytes beside the rows; D2D_EUNSUPPORTED past
+     * 160 KiB, e.g. full neighbourhoods of ~96 agents). */
     uint8_t* obs_record;
     /* comb only (ABI v13): the state row as bf16 -- exact, every state value is an integer in [-1, 255] -- for
      * the D2D central critic's operand: env e's row at state_bf16 + e * state_bf16_ld (elements; a multiple of
