@@ -231,50 +231,24 @@ class D2DPPO(BatchedLearnerBase):
         cycle = np.arange(self.n_agents)
         np.random.shuffle(cycle)
         cycle = self._sync_perm(cycle)
-        T, E, N = ro.T, ro.E, self.n_agents
-        # first epoch on this rollout: the epoch-start actors ARE the rollout's, and the policy kernel's forced
-        # log-probs equal the sampled ones bit for bit, so every ratio is exactly 1 and the chain is A for every
-        # agent (no forced pass needed).  Not for GRU policies: their training windows are padded, the rollout's
-        # were not (Q5)
-        shortcut = not self.useRNN and self._actors_unchanged_since(ro)
-        side = self._side_stream()
-        logp_new = None
-        if not shortcut and side is not None:
-            # the forced log-prob pass (VALU-bound policy kernel) depends on the actors only: it runs on a side stream
-            # beside the central critic's forward (HBM-bound) and GAE, joined before the chain
-            main = torch.cuda.current_stream()
-            side.wait_stream(main)
-            with torch.cuda.stream(side), torch.no_grad():
-                logp_new = self._logp_forced(ro)
-            logp_new.record_stream(main)
         crit = self._critic_split_forward(ro)
         values = crit[0] if crit is not None else self.value_network(ro.state_seq).squeeze()
         self._phase("critic_fwd")
         v_te = values.detach().view(ro.E, ro.T).t().unsqueeze(2).contiguous()
         adv, _ = self._gae(ro.rewards, v_te, ro.dones, normalize_adv=True, normalize_ret=False)
         self._phase("gae")
+        T, E, N = ro.T, ro.E, self.n_agents
         A = adv[:, :, 0].reshape(-1)                                                   # [T*E]
         with torch.no_grad():
-            if shortcut:
+            if not self.useRNN and self._actors_unchanged_since(ro):
+                # first epoch on this rollout: the epoch-start actors ARE the rollout's, and the
+                # policy kernel's forced log-probs equal the sampled ones bit for bit, so every
+                # ratio is exactly 1 and the chain is A for every agent (no forced pass needed).
+                # Not for GRU policies: their training windows are padded, the rollout's were not (Q5)
                 M = A.expand(N, T * E)
             else:
-                if logp_new is None:
-                    logp_new = self._logp_forced(ro)
-                else:
-                    torch.cuda.current_stream().wait_stream(side)
-                M = self._chain_dev(A, logp_new, ro.logp, cycle, T, E)                # [N][T*E]
+                M = self._chain_dev(A, self._logp_forced(ro), ro.logp, cycle, T, E)     # [N][T*E]
         self._phase("chain")
-        # the central critic's backward (dW1: HBM-bound) needs the forward's dpre parts only: on the side stream beside
-        # the actor-gradient kernel (MFMA / VALU-bound), joined before the critic's all-reduce and Adam step
-        crit_side = crit is not None and side is not None
-        if crit_side:
-            side.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(side):
-                value_loss = self._critic_split_backward(ro, crit)
-            # (tensors made on the side stream and read on the main one: their blocks are not reused by the side
-            # stream's allocator before the main stream's reads)
-            for t in [prm.grad for prm in self.value_network.parameters()] + [value_loss]:
-                t.record_stream(torch.cuda.current_stream())
         pp = self.policy.params
         kind = "comb" if self.combinatorial else "chsel"
         beta = float(self.beta_entropy)
@@ -295,9 +269,7 @@ class D2DPPO(BatchedLearnerBase):
         self.policy_optimizer.step()
         self._phase("adam")
         ploss = -(sa[:, 0] + beta * sa[:, 1]) / (T * E)
-        if crit_side:
-            torch.cuda.current_stream().wait_stream(side)
-        elif crit is not None:
+        if crit is not None:
             value_loss = self._critic_split_backward(ro, crit)
         else:
             value_loss = F.mse_loss(values, ro.ret_mean, reduction='mean')
@@ -311,19 +283,6 @@ class D2DPPO(BatchedLearnerBase):
         self._phase("adam")
         pl = ploss.detach().cpu().numpy()
         return [float(pl[i]) for i in cycle], value_loss.detach()
-
-    # round 6: independent pieces of an epoch on a second HIP stream (the forced log-prob pass beside the critic's
-    # forward, the critic's backward beside the actor-gradient kernel); D2D_OVERLAP=0 keeps one stream (A/B).  Every
-    # kernel sees the same inputs either way, so the results are bitwise the same.
-    overlap_streams = os.environ.get("D2D_OVERLAP", "1") != "0"
-
-    def _side_stream(self):
-        if not self.overlap_streams or not torch.cuda.is_available() or torch.device(self.device).type != "cuda":
-            return None
-        st = self.__dict__.get("_side")
-        if st is None:
-            st = self._side = torch.cuda.Stream(device=self.device)
-        return st
 
     def _actors_unchanged_since(self, ro):
         snap = getattr(ro, "policy_snapshot", None)

@@ -442,24 +442,3 @@ def test_deferred_values_equal_rollout_values(H):
     assert not ro2.values_pending
     dfr._update_epoch(ro2, None)
 
-
-@pytest.mark.parametrize("kind,N,H", [("c5", 16, 64), ("chsel", 6, 32), ("c5", 256, 64)])
-def test_d2d_side_stream_epochs_equal_one_stream(kind, N, H):
-    """D2D-PPO epochs with the forced log-prob pass and the central critic's backward on a side stream
-    (D2DPPO.overlap_streams, round 6) give bitwise the epochs of the one-stream order: the same kernels on the same
-    inputs.  Three epochs (the first takes the ratio-1 shortcut, the next two run the forced pass)."""
-    from algorithms.d2d_ppo import D2DPPO
-    (a, b), ro, copy = _learner_pair(D2DPPO, kind, E=64 if N > 64 else 96, N=N, H=H)
-    a.overlap_streams, b.overlap_streams = True, False
-    for ep in range(3):
-        np.random.seed(11 + ep)
-        pa, va = a._update_epoch(ro, a._update_state(ro))
-        np.random.seed(11 + ep)
-        pb, vb = b._update_epoch(ro, b._update_state(ro))
-        torch.cuda.synchronize()
-        assert pa == pb, ep
-        assert torch.equal(va, vb), ep
-        for (na, x), (nb, y) in zip(a.value_network.named_parameters(), b.value_network.named_parameters()):
-            assert torch.equal(x.grad, y.grad) and torch.equal(x.data, y.data), (ep, na)
-        for x, y in zip(a.policy.parameters(), b.policy.parameters()):
-            assert torch.equal(x.data, y.data), ep
