@@ -13,49 +13,7 @@
 #define D2D_POLICY_L2_F32 0
 #endif
 
-#ifndef D2D_POLICY_SPLIT_DOT2
-// 1: the per-tile three-way split of relu(H^T) for layer 2 takes its residuals v - part on v_dot2c_f32_bf16
-// (part.lo * -1 + part.hi * 0 + v: one VALU, exact -- v minus its 8-bit truncation is representable) instead of
-// v_and + v_sub; the parts are bitwise the truncation split's (mlp_common.h split3), 7 instead of 11 VALU per pair
-#define D2D_POLICY_SPLIT_DOT2 1
-#endif
-
 namespace d2d {
-
-#if D2D_POLICY_SPLIT_DOT2
-typedef __bf16 pol_bf16x2 __attribute__((ext_vector_type(2)));
-// the bf16 pairs (-1, 0) / (0, -1) from SGPRs: the compiler's inline-constant encoding of 0x0000BF80 is not read
-// by the hardware as that pair (update_kernels.hip, tools/gpu/probe/dot2_probe.hip)
-__device__ __forceinline__ uint32_t pol_neg1_lo() {
-  uint32_t c;
-  asm("s_mov_b32 %0, 0x0000bf80" : "=s"(c));
-  return c;
-}
-__device__ __forceinline__ uint32_t pol_neg1_hi() {
-  uint32_t c;
-  asm("s_mov_b32 %0, 0xbf800000" : "=s"(c));
-  return c;
-}
-// exact three-way truncation split of 8 finite floats (bitwise split3's parts)
-__device__ __forceinline__ Parts split3_dot(const float (&v)[8]) {
-  const uint32_t nlo = pol_neg1_lo(), nhi = pol_neg1_hi();
-  auto res = [](uint32_t part, uint32_t neg, float x) {
-    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(pol_bf16x2, part), __builtin_bit_cast(pol_bf16x2, neg), x,
-                                           false);
-  };
-  uint32_t H[4], M[4], L[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const float a = v[2 * p], b = v[2 * p + 1];
-    H[p] = pack_hi(a, b);
-    const float ar = res(H[p], nlo, a), br = res(H[p], nhi, b);
-    M[p] = pack_hi(ar, br);
-    const float al = res(M[p], nlo, ar), bl = res(M[p], nhi, br);
-    L[p] = pack_hi(al, bl);
-  }
-  return {as_frag(H), as_frag(M), as_frag(L)};
-}
-#endif
 
 // x[c][j] <- slot, then input F := 1.0 (layer-1 bias input) and inputs past F := 0
 template <int KC>
@@ -255,11 +213,7 @@ struct SplitNet {
         hvals[r] = relu(ha[2 * c2i][r]);
         hvals[4 + r] = relu(ha[2 * c2i + 1][r]);
       }
-#if D2D_POLICY_SPLIT_DOT2
-      lg = mfma_split(w2p[c2i], split3_dot(hvals), false, lg);
-#else
       lg = mfma_split(w2p[c2i], split3(hvals), false, lg);
-#endif
     }
 #endif
     // ---- critic layer 2 (64 -> 1) on VALU
