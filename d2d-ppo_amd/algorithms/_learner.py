@@ -699,16 +699,6 @@ class BatchedLearnerBase(DataParallelMixin):
     # ------------------------------------------------------------ phase marks
     phase_timer = None  # bench.py installs one to split an iteration into phases (stream events)
 
-    # round 6: the stacked learners' Adam as torch's fused kernel (one launch per step over all of a network's stacked
-    # tensors instead of the multi-tensor foreach sequence); the same update formula, D2D_FUSED_ADAM=0 keeps foreach
-    fused_adam = os.environ.get("D2D_FUSED_ADAM", "1") != "0"
-
-    def _adam(self, params, lr):
-        params = list(params)
-        if self.fused_adam and all(p.is_cuda for p in params):
-            return torch.optim.Adam(params, lr=lr, fused=True)
-        return torch.optim.Adam(params, lr=lr)
-
     def _phase(self, name):
         """Attribute the GPU time since the previous mark to `name` (no-op unless timed)."""
         t = self.phase_timer

@@ -135,11 +135,11 @@ class D2DPPO(BatchedLearnerBase):
         # The value network is at the BS (d2d_ppo.py:264-267)
         self.value_network = Value(self.env.state_space.shape[0], hidden_size)
         self.value_network = self.value_network.to(self.device)
-        self.value_optimizer = self._adam(self.value_network.parameters(), value_lr)
+        self.value_optimizer = torch.optim.Adam(self.value_network.parameters(), lr=value_lr)
         in_dims = [env.observation_space[k].shape[0] for k in range(self.n_agents)]
         self.policy = StackedNets([a.policy_network for a in self.agents], in_dims,
                                   "rnn" if useRNN else "mlp", self.device, act=self._policy_act())
-        self.policy_optimizer = self._adam(self.policy.parameters(), policy_lr)
+        self.policy_optimizer = torch.optim.Adam(self.policy.parameters(), lr=policy_lr)
         self._setup_data_parallel(self.policy.parameters() + list(self.value_network.parameters()))
 
     # ------------------------------------------------------------ rollouts

@@ -161,8 +161,8 @@ class iPPO(BatchedLearnerBase):
         self.policy = StackedNets([a.policy_network for a in self.agents], in_dims, kind, self.device,
                                   act=self._policy_act())
         self.value = StackedNets([a.value_network for a in self.agents], in_dims, kind, self.device, act=None)
-        self.policy_optimizer = self._adam(self.policy.parameters(), policy_lr)
-        self.value_optimizer = self._adam(self.value.parameters(), value_lr)
+        self.policy_optimizer = torch.optim.Adam(self.policy.parameters(), lr=policy_lr)
+        self.value_optimizer = torch.optim.Adam(self.value.parameters(), lr=value_lr)
         self._setup_data_parallel(self.policy.parameters() + self.value.parameters())
 
     # ------------------------------------------------------------ rollouts
