@@ -28,9 +28,9 @@ for leg in rollout ppo gru_slot gru; do
   cp "$R/gpurun_out/pmcl_r06/pmc_mfma_$leg.json" "$O/pmc_mfma_$leg.json"
   cp "$(ls "$R/gpurun_out/pmcl_r06/$leg/stats/"*kernel_stats.csv | head -1)" "$O/${leg}_kernel_stats.csv"
 done
-rm -rf "$R/gpurun_out/pmcl_r06"
-exit 0
 bash "$R/tools/gpu/profile_single.sh" r06z "$COMMIT" > "$O/profile_single.log" 2>&1
 rc=$?; echo "single traffic rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cp "$R/gpurun_out/prof_r06z/pmc_traffic_single.json" "$O/pmc_traffic_single.json"
 cp "$(ls "$R"/gpurun_out/prof_r06z/stats/*kernel_stats.csv | head -1)" "$O/single_kernel_stats.csv"
+rm -rf "$R/gpurun_out/pmcl_r06" "$R/gpurun_out/prof_r06z"
+exit 0
