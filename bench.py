@@ -960,9 +960,12 @@ def gru_c5_leg(args, rank, world, local):
         lr._update_epoch(ro, upd)     # epoch 1 (its forced log-prob pass included: no first-epoch shortcut on GRU)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
-        lr._update_epoch(ro, upd)     # epoch 2
+        lr.phase_timer = PhaseTimer()
+        lr._update_epoch(ro, upd)     # epoch 2 (with its phase split: the forced pass is in "chain")
         torch.cuda.synchronize()
         t3 = time.perf_counter()
+        ep_phases = {k: max_over_ranks(v, world) for k, v in lr.phase_timer.totals_ms().items()}
+        lr.phase_timer = None
         barrier(world)
         if rank == 0:
             print(f"[bench gru_c5] N={N}: rollout {t1 - t0:.2f} s, epochs {t2 - t1:.2f} / {t3 - t2:.2f} s",
@@ -973,7 +976,7 @@ def gru_c5_leg(args, rank, world, local):
         samples = ro.T * E * world * N
         sweep.append({"agents": N, "history_len": N, "envs_per_gpu": E, "gru_kernels": gru_ok,
                       "rollout_s": roll, "rollout_env_steps_per_s": E * world * ro.T / roll,
-                      "epoch_s": ep, "first_epoch_s": ep1, "agent_samples_per_epoch": samples,
+                      "epoch_s": ep, "epoch_phase_ms": ep_phases, "first_epoch_s": ep1, "agent_samples_per_epoch": samples,
                       "update_agent_samples_per_s": samples / ep,
                       "iteration_s": roll + ep1 + 4 * ep,
                       "iteration_env_steps_per_s_end_to_end": E * world * ro.T / (roll + ep1 + 4 * ep)})
