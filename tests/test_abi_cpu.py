@@ -107,6 +107,58 @@ def test_library_validates_arguments_without_gpu():
     assert lib.d2d_set_option(_lib.D2D_OPT_FUSED_SLICE, 0) == 0
 
 
+def test_abi14_argument_checks():
+    """ABI 14's entry points refuse bad arguments before any HIP call (runs on a GPU-less host): the carried GRU
+    state (d2d_policy_gru_carry: a NULL scratch, a slot whose window does not extend the previous one) and the
+    central critic's dW1 (d2d_central_critic_dw1: hidden, ldx, alignment, workspace size)."""
+    import ctypes
+    import d2dhip
+    from d2dhip import _lib
+    lib = d2dhip.load()
+    w = ctypes.c_void_p(16)
+    g = _lib.GruDesc(2, 32, 12, 16, 4, 1, 3, 8, w, w, w, w, w, w, w, w, 0, 0, None, _lib.D2D_OBS_F32, 0, None)
+    n = lib.d2d_gru_carry_floats(ctypes.byref(g))
+    assert n == 2 * 2 * 4 * 1 * 64  # [N][env tiles][4 HT][64]
+    assert lib.d2d_policy_gru_carry(ctypes.byref(g), 8, w, 1, None, 0, 0, w, w, None, 1, None) == -1
+    assert b"NULL hcarry" in lib.d2d_last_error()
+    for slot in (0, 3, 8, 11):  # episode positions 0, 3, 0, 3 with history_len 3
+        assert lib.d2d_policy_gru_carry(ctypes.byref(g), 16, w, slot, None, 0, 0, w, w, w, 1, None) == -1
+        assert b"does not extend" in lib.d2d_last_error()
+    assert lib.d2d_central_critic_dw1_workspace(62, 10, 100, 104) == -1
+    assert lib.d2d_central_critic_dw1_workspace(64, 10, 100, 96) == -1
+    ws = lib.d2d_central_critic_dw1_workspace(64, 819200, 3848, 3848)
+    assert ws > 0 and ws % (64 * 3848) == 0 and (ws // (64 * 3848)) % 8 == 0  # KS partials, a multiple of the 8 XCDs
+    assert lib.d2d_central_critic_dw1(62, 64, 100, 104, w, w, w, 10 ** 6, w, None) == -2
+    assert lib.d2d_central_critic_dw1(64, 64, 100, 100, w, w, w, 10 ** 6, w, None) == -1  # ldx not a multiple of 8
+    assert lib.d2d_central_critic_dw1(64, 64, 100, 104, ctypes.c_void_p(24), w, w, 10 ** 6, w, None) == -1  # misaligned
+    assert lib.d2d_central_critic_dw1(64, 64, 100, 104, w, w, w, 1, w, None) == -1  # workspace too small
+    assert b"d2d_central_critic_dw1_workspace" in lib.d2d_last_error()
+
+
+def test_d2denv_record_signed_masks():
+    """The D2DEnv's record masks (ABI 14): exactly the last-feedback column of each agent's obs row (gather code -1
+    of d2d_env_single_gather_map, env.py:94), wherever the neighbourhood puts it."""
+    import d2dhip
+    from d2dhip.record import signed_masks
+    from d2dhip.spec import EnvSpec
+    from envs.env import D2DEnv
+    lib = d2dhip.load()
+    N = 5
+    nb = [[0, 1], [1], [0, 1, 2, 3, 4], [3, 4], [4]]
+    env = D2DEnv(n_agents=N, deadlines=np.array([3, 5, 4, 2, 6]), lbdas=np.full(N, 0.2), episode_length=10,
+                 neighbourhoods=nb, n_envs=2, device="cpu", seed=1)
+    s = env.spec
+    codes = s.gather_map(lib)
+    m = signed_masks(s, codes)
+    assert m.shape == (N, 32 * ((s.F + 32) // 32) // 32)
+    for k in range(N):
+        cols = [c for c in range(32 * m.shape[1]) if (int(m[k, c // 32]) >> (c % 32)) & 1]
+        length = sum(int(s.d[j]) + 1 for j in nb[k]) + 1  # buffers + channel bits of the neighbours, then the ack
+        assert cols == [length - 1], (k, cols)
+    with pytest.raises(ValueError):
+        signed_masks(s)  # the D2DEnv masks need its gather codes
+
+
 def test_record_signed_masks_and_decode():
     """The int8-column masks mark exactly the ACK columns [w_k + C, w_k + 2C) of every agent's row
     (combinatorial_env.py:199-206), and ObsRecord.decode maps bytes back to the fp32 obs values."""
