@@ -198,7 +198,8 @@ class BatchedLearnerBase(DataParallelMixin):
         if self.useRNN:
             from d2dhip import gru
             _, lp = gru.policy({k: v.data for k, v in self.policy.params.items()}, ro.obs, self._gru_kind(),
-                               self.history_len, ro.L, 0, ro.T, padded=True, forced=ro.actions)
+                               self.history_len, ro.L, 0, ro.T, padded=True, forced=ro.actions,
+                               want_actions=False)
             return lp
         from d2dhip import _lib
         lib = _lib.require_gpu()
@@ -206,10 +207,10 @@ class BatchedLearnerBase(DataParallelMixin):
         desc = self._mlp_desc(TE, 0)
         desc.v1 = desc.c1 = desc.v2 = desc.c2 = None
         logp = torch.empty((N, TE), dtype=torch.float32, device=self.device)
-        scratch = torch.empty_like(ro.actions)
         optr = set_format(desc, ro.obs)
-        rc = lib.d2d_policy_mlp_step(desc, optr, ro.actions.data_ptr(), 0, 0, scratch.data_ptr(),
-                                     logp.data_ptr(), None, _lib.stream_ptr())
+        # actions = NULL (ABI 15): forced mode stores only the log-probs (the actions are the input)
+        rc = lib.d2d_policy_mlp_step(desc, optr, ro.actions.data_ptr(), 0, 0, None, logp.data_ptr(), None,
+                                     _lib.stream_ptr())
         _lib.check(rc, "d2d_policy_mlp_step (forced)")
         return logp
 

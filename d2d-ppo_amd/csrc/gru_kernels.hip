@@ -1532,7 +1532,8 @@ static int policy_gru(const d2d_gru_desc* d, int32_t T, const void* obs, int32_t
                       float* out, float* hcarry, int32_t carry_in, void* stream) {
   int rc = check_gru_desc(d, obs);
   if (rc) return rc;
-  if (!obs || !out || (d->kind != 2 && !actions)) { d2d_set_error("d2d_policy_gru: NULL buffer"); return D2D_EINVAL; }
+  // actions may be NULL in forced mode (the log-probs of given actions: nothing else to write)
+  if (!obs || !out || (d->kind != 2 && !actions && !forced)) { d2d_set_error("d2d_policy_gru: NULL buffer"); return D2D_EINVAL; }
   if (T < 1 || slot0 < 0 || n_slots < 0 || slot0 + n_slots > T) {
     d2d_set_error("d2d_policy_gru: slots [%d, %d) outside the %d-slot buffer", slot0, slot0 + n_slots, T);
     return D2D_EINVAL;

@@ -28,9 +28,17 @@ template <bool HALF = false>
 __device__ __forceinline__ float group_sum(float v) {
   return uf(group_reduce<HALF>(fu(v), [](uint32_t a, uint32_t b) { return fu(uf(a) + uf(b)); }));
 }
+// max of two floats as one v_max_f32: fmaxf under the IEEE mode first quiets each operand with a canonicalizing
+// v_max_f32 x, x, x (the compiler cannot prove an MFMA result or a lane swap canonical) -- three VALU instead of one.
+// The same value for every non-NaN input; a NaN in stays a NaN out.
+__device__ __forceinline__ float fmax_raw(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 template <bool HALF = false>
 __device__ __forceinline__ float group_max(float v) {
-  return uf(group_reduce<HALF>(fu(v), [](uint32_t a, uint32_t b) { return fu(fmaxf(uf(a), uf(b))); }));
+  return uf(group_reduce<HALF>(fu(v), [](uint32_t a, uint32_t b) { return fu(fmax_raw(uf(a), uf(b))); }));
 }
 template <bool HALF = false>
 __device__ __forceinline__ uint32_t group_or(uint32_t v) {

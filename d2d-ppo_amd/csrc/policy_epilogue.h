@@ -100,11 +100,13 @@ __device__ __forceinline__ u32x4 policy_rng_block(const MlpArgs& a, int env, boo
 // RNG (sample mode): the lane's Philox block drawn ahead by the caller and passed in `rpre` -- the split
 // kernel draws it before its tile MFMAs so that the ten dependent rounds (20 v_mad_u64_u32) fill the MFMA issue
 // gaps instead of running as a serial chain after them; the same counter and key, so the same words.
+// AF != 0: the action count as a compile-time constant (a.A == AF; the split kernel's A = 8 instantiation, the
+// combinatorial envs' 8 channels): no per-action range selects
 template <int KIND, bool CRITIC, bool HALF = false, int MODE = kModeRuntime, bool PRE = false, bool SIGMOID = false,
-          bool RNG = false>
+          bool RNG = false, int AF = 0>
 __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, float value, int env, bool env_ok,
                                                 int k, int g, uint32_t rng, uint32_t fpre = 0, u32x4 rpre = {}) {
-  const int N = a.N, A = a.A;
+  const int N = a.N, A = AF ? AF : a.A;
   constexpr bool critic = CRITIC;
   const int ga = HALF ? (g & 1) : g;
   const bool forced = MODE == kModeRuntime ? a.forced != nullptr : MODE == kModeForced;
@@ -118,10 +120,10 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
       p[r] = (4 * ga + r < A) ? __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-lg[r])) : 0.f;
   } else {
     // ---- softmax over the A actions of env i (lane group g holds actions 4g..4g+3)
-    float mx = -INFINITY;
+    float mx = 4 * ga < A ? lg[0] : -INFINITY;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (4 * ga + r < A) mx = fmaxf(mx, lg[r]);
+    for (int r = 1; r < 4; ++r)
+      if (4 * ga + r < A) mx = fmax_raw(mx, lg[r]);
     mx = group_max<HALF>(mx);
     float ex[4], sum = 0.f;
 #pragma unroll
@@ -166,7 +168,7 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
       lsum += act < A ? l : 0.f;
     }
     lsum = group_sum<HALF>(lsum);
-    lp = lsum * a.inv_A;  // log_prob(action).mean(-1)
+    lp = lsum * (AF ? 1.f / (float)AF : a.inv_A);  // log_prob(action).mean(-1)
     out_bits = group_or<HALF>(out_bits);
   } else {
     // ---- Categorical over A ids (channel selection): Categorical(probs) renormalises, log of
@@ -226,10 +228,13 @@ __device__ __forceinline__ void policy_epilogue(const MlpArgs& a, f32x4 lg, floa
     out_id = chosen;
   }
   if (env_ok && ga == 0) {
-    if constexpr (KIND == 0) {
-      store_mask(a.act_out, cell, a.mask_bytes, out_bits);
-    } else {
-      reinterpret_cast<unsigned char*>(a.act_out)[cell] = (unsigned char)out_id;
+    // forced mode with act_out NULL: the actions are the caller's input, nothing to store
+    if (!forced || a.act_out) {
+      if constexpr (KIND == 0) {
+        store_mask(a.act_out, cell, a.mask_bytes, out_bits);
+      } else {
+        reinterpret_cast<unsigned char*>(a.act_out)[cell] = (unsigned char)out_id;
+      }
     }
     a.logp_out[(size_t)k * a.E + env] = lp;
     if (critic && a.value_out) a.value_out[(size_t)k * a.E + env] = value;

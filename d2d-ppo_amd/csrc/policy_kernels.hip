@@ -180,13 +180,19 @@ __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* 
 // it could save at most (tools/gpu/fusion_bound.py)
 #define D2D_POLICY_ABLATE_NOREAD 0
 #endif
+#ifndef D2D_POLICY_ABLATE_FORCED_DMA
+// != 0 only in timing variants (tools/gpu/run_r06o.sh): forced mode without the forced-word DMA (every forced mask
+// reads as 0) -- what the forced words' DMA and extraction cost
+#define D2D_POLICY_ABLATE_FORCED_DMA 0
+#endif
 #ifndef D2D_POLICY_ACTOR_WAVES
 // waves per SIMD of the actor-only record instantiation (137 VGPRs at 3; 4 needs <= 128)
 #define D2D_POLICY_ACTOR_WAVES 3
 #endif
 // KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even);
 // U8: the inputs are the env kernel's compact obs record (D2D_OBS_U8)
-template <int KC, int HT, int KIND, bool CRITIC, int MODE, bool U8>
+// AF: the action count as a compile-time constant (0: a.A at run time; 8: the combinatorial envs' 8 channels)
+template <int KC, int HT, int KIND, bool CRITIC, int MODE, bool U8, int AF = 0>
 // (H <= 64, F + 1 <= 32: 2 waves / SIMD with the iPPO critic or on fp32 rows (their DMA ring is 48 KB), 3 for the
 // actor alone on the record (137 VGPRs: test(), D2D-PPO,
 // and iPPO training rollouts whose values come from the first epoch's critic pass); H in (64, 128] -- the
@@ -202,7 +208,7 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
   int k, by;
   xcd_block(k, by);  // k = agent, by = env chunk
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (SGPR)
-  const int N = a.N, F = a.F, A = a.A;
+  const int N = a.N, F = a.F, A = AF ? AF : a.A;
   const int tiles = a.envs_per_wave / 16;
   const int wave_env0 = (by * (blockDim.x >> 6) + wave) * a.envs_per_wave;
 
@@ -222,7 +228,7 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
   // register load inside the tile loop drains the ring with vmcnt(0) and a wave can run any number of
   // tiles (one resident round).  Paired epilogue (A <= 8, one byte per cell) only; otherwise the DMA is
   // aimed outside the buffer (no traffic) and the epilogue loads its masks itself.
-  constexpr int FD = MODE == kModeForced ? 1 : 0;
+  constexpr int FD = (MODE == kModeForced && !D2D_POLICY_ABLATE_FORCED_DMA) ? 1 : 0;
   __shared__ uint32_t fring[4][FD ? RING : 1][64];
   const int64_t fbytes = MODE == kModeForced ? ((int64_t)a.E * N * a.mask_bytes + 3) / 4 * 4 : 0;
   const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -252,8 +258,9 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
             rsrc, (__attribute__((address_space(3))) void*)&ring[wave][t % RING][c][j][0], 4,
             vo + (U8 ? 32 * c + 4 * j : 4 * (32 * c + j)), 0, 0, 0);
     if constexpr (FD) {
+      // 32-bit cell offsets: policy_mlp_args caps the forced buffer at 2 GiB
       const int env = wave_env0 + t * 16 + i;
-      const uint32_t fo = (t < tiles && g == 0 && A <= 8 && env < a.E) ? (uint32_t)(((size_t)env * N + k) & ~(size_t)3)
+      const uint32_t fo = (t < tiles && g == 0 && A <= 8 && env < a.E) ? ((uint32_t)env * (uint32_t)N + (uint32_t)k) & ~3u
                                                                        : 0x80000000u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(frsrc, (__attribute__((address_space(3))) void*)&fring[wave][t % RING][0],
                                                4, fo, 0, 0, 0);
@@ -285,7 +292,7 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
     if constexpr (FD) {
       const int envc = g < 2 ? env0 : env1;
       const uint32_t w = fring[wave][(g < 2 ? tt : tt + 1) % RING][i];
-      fpre = (w >> (8 * (uint32_t)(((size_t)(envc < a.E ? envc : 0) * N + k) & 3))) & 0xFFu;
+      fpre = (w >> (8 * (((uint32_t)(envc < a.E ? envc : 0) * (uint32_t)N + (uint32_t)k) & 3u))) & 0xFFu;
     }
     // the paired epilogue's Philox block, drawn here: inside the scheduling region of the tiles' MFMAs (the
     // barrier below would otherwise keep it behind them as a serial chain of ten dependent rounds)
@@ -315,7 +322,7 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
 #pragma unroll
       for (int r = 0; r < 4; ++r) lgc[r] = uf(__builtin_amdgcn_permlane32_swap(fu(lg0[r]), fu(lg1[r]), false, false)[0]);
       const int envc = g < 2 ? env0 : env1;
-      policy_epilogue<KIND, CRITIC, true, MODE, MODE == kModeForced, false, MODE == kModeSample && D2D_POLICY_RNG_EARLY>(
+      policy_epilogue<KIND, CRITIC, true, MODE, MODE == kModeForced, false, MODE == kModeSample && D2D_POLICY_RNG_EARLY, AF>(
           a, lgc, g < 2 ? v0 : v1, envc, envc < a.E, k, g, rng, fpre, rpre);
     } else {
       policy_epilogue<KIND, CRITIC, false, MODE>(a, lg0, v0, env0, env0 < a.E, k, g, rng);
@@ -396,11 +403,22 @@ static void launch_one(const MlpArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(K, grid, dim3(256), 0, s, x);
 }
 
+template <int KC, int HT, int KIND, bool CRITIC, bool U8, int AF>
+static void launch_split_af(const MlpArgs& a, hipStream_t s) {
+  if (a.forced) launch_one<policy_split_kernel<KC, HT, KIND, CRITIC, kModeForced, U8, AF>>(a, s);
+  else if (a.deterministic) launch_one<policy_split_kernel<KC, HT, KIND, CRITIC, kModeDeterministic, U8, AF>>(a, s);
+  else launch_one<policy_split_kernel<KC, HT, KIND, CRITIC, kModeSample, U8, AF>>(a, s);
+}
+#ifndef D2D_POLICY_AFIX
+// 1: the record kernels of the combinatorial actor at A = 8 (the benched 8 channels) with the action count compile-time
+#define D2D_POLICY_AFIX 1
+#endif
 template <int KC, int HT, int KIND, bool CRITIC, bool U8>
 static void launch_split_fmt(const MlpArgs& a, hipStream_t s) {
-  if (a.forced) launch_one<policy_split_kernel<KC, HT, KIND, CRITIC, kModeForced, U8>>(a, s);
-  else if (a.deterministic) launch_one<policy_split_kernel<KC, HT, KIND, CRITIC, kModeDeterministic, U8>>(a, s);
-  else launch_one<policy_split_kernel<KC, HT, KIND, CRITIC, kModeSample, U8>>(a, s);
+  if constexpr (KIND == 0 && U8 && D2D_POLICY_AFIX) {
+    if (a.A == 8) return launch_split_af<KC, HT, KIND, CRITIC, U8, 8>(a, s);
+  }
+  launch_split_af<KC, HT, KIND, CRITIC, U8, 0>(a, s);
 }
 
 template <int KC, int HT, int KIND, bool CRITIC, bool U8>
@@ -441,7 +459,8 @@ static int launch_policy_split(const MlpArgs& a, hipStream_t s) {
 // env_kernels.hip d2d_comb_policy_fused_step)
 int d2d::policy_mlp_args(const d2d_mlp_desc* d, const void* obs, const void* forced, uint32_t rng_step,
                          int32_t deterministic, void* actions, float* logp, float* value, MlpArgs& a) {
-  if (!d || !obs || !actions || !logp || !d->w1 || !d->b1 || !d->w2 || !d->b2) {
+  // actions may be NULL in forced mode only (the log-probs of given actions: nothing else to write)
+  if (!d || !obs || (!actions && !forced) || !logp || !d->w1 || !d->b1 || !d->w2 || !d->b2) {
     d2d_set_error("d2d_policy_mlp_step: NULL argument");
     return D2D_EINVAL;
   }

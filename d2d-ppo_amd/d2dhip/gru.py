@@ -37,12 +37,13 @@ def carry_floats(params, n_envs, history_len, episode_length):
 
 def policy(params, obs, kind, history_len, episode_length, slot0, n_slots, padded=False, forced=None, rng_step=0,
            deterministic=False, seed=0, env_base=0, rng_offset=None, actions_out=None, out=None, hcarry=None,
-           carry_in=False):
+           carry_in=False, want_actions=True):
     """obs [T][E][N][F] (the rollout buffer: fp32, or the env kernel's ObsRecord).  kind 'sigmoid' / 'softmax' (actors): returns
     (actions [n_slots][E][N], logp [N][n_slots * E]); kind None (value): returns values [N][n_slots * E].
     hcarry (one unpadded slot per launch, slots in order: d2d_policy_gru_carry): float32 scratch of carry_floats()
     elements holding h after the previous slot's window; carry_in: the previous launch on it was slot0 - 1 and
-    slot0's episode position is in [1, history_len - 1] (its window extends that one by one step)."""
+    slot0's episode position is in [1, history_len - 1] (its window extends that one by one step).
+    want_actions=False with forced: actions = NULL to the C ABI (only the log-probs are stored; returns (None, logp))."""
     lib = _lib.require_gpu()
     T, E, N, F = obs.shape
     k = KIND[kind]
@@ -52,7 +53,7 @@ def policy(params, obs, kind, history_len, episode_length, slot0, n_slots, padde
     if out is None:
         out = torch.empty((N, n_slots * E), dtype=torch.float32, device=dev)
     act = None
-    if k != 2:
+    if k != 2 and (want_actions or forced is None):
         A = params["w2"].shape[1]
         mb = 1 if (k == 1 or A <= 8) else 2 if A <= 16 else 4
         dt = {1: torch.uint8, 2: torch.int16, 4: torch.int32}[mb]

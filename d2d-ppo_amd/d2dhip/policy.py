@@ -6,10 +6,11 @@ from .record import set_format
 
 
 def policy_mlp_step(actor, obs, kind, critic=None, forced=None, rng_step=0, deterministic=False, seed=0,
-                    env_base=0, actions=None, logp=None, value=None, want_value=True):
+                    env_base=0, actions=None, logp=None, value=None, want_value=True, want_actions=True):
     """actor/critic: dicts of agent-stacked fp32 tensors w1 [N][H][F], b1 [N][H], w2 [N][A][H], b2 [N][A]
     (critic: A = 1).  obs [E][N][F] fp32, or the env kernel's ObsRecord of that shape.  kind 'comb' (Bernoulli, masks out) or 'chsel' (Categorical, ids out).
-    want_value=False with critic weights passes value = NULL to the C ABI (valid usage: the value is skipped).
+    want_value=False with critic weights passes value = NULL to the C ABI (valid usage: the value is skipped);
+    want_actions=False with forced passes actions = NULL (only the log-probs are stored; actions returned as None).
     Returns (actions [E][N], logp [N][E], value [N][E] or None)."""
     lib = _lib.require_gpu()
     N, H, F = actor["w1"].shape
@@ -20,7 +21,8 @@ def policy_mlp_step(actor, obs, kind, critic=None, forced=None, rng_step=0, dete
     for t in list(actor.values()) + (list(critic.values()) if critic else []):
         assert t.dtype == torch.float32 and t.is_contiguous() and t.device == dev
     k = 0 if kind == "comb" else 1
-    if actions is None:
+    store_actions = want_actions or forced is None
+    if actions is None and store_actions:
         if k == 0:
             dt = torch.uint8 if A <= 8 else torch.int16
             actions = torch.zeros((E, N), dtype=dt, device=dev)
@@ -37,7 +39,8 @@ def policy_mlp_step(actor, obs, kind, critic=None, forced=None, rng_step=0, dete
                         int(env_base))
     optr = set_format(desc, obs)
     rc = lib.d2d_policy_mlp_step(desc, optr, None if forced is None else forced.contiguous().data_ptr(),
-                                 int(rng_step), 1 if deterministic else 0, actions.data_ptr(), logp.data_ptr(),
+                                 int(rng_step), 1 if deterministic else 0,
+                                 actions.data_ptr() if store_actions else None, logp.data_ptr(),
                                  None if value is None else value.data_ptr(), _lib.stream_ptr())
     _lib.check(rc, "d2d_policy_mlp_step")
-    return actions, logp, (value if critic is not None and want_value else None)
+    return (actions if store_actions else None), logp, (value if critic is not None and want_value else None)

@@ -43,14 +43,15 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 14  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
+#define D2D_ABI_VERSION 15  /* 4: GRU entry points; 5: compact obs record (obs_record, obs_format);
                               6: d2d_env_desc.poisson_cdf; 7: d2d_f32_to_bf16_exact, d2d_states_to_bf16_exact,
                               d2d_critic_dpre_split; 8: d2d_gae_scan_moments, d2d_normalize_pair;
                               9: d2d_gae_scan_moments without outputs, d2d_gae_scan_normalized;
                               10: d2d_states_to_bf16_padded, d2d_critic_dpre_split3;
                               11: D2D_OPT_CRITIC_GRAD_ROWS; 12: d2d_ppo_critic_grad_values, d2d_central_critic_*;
                               13: d2d_comb_policy_fused_step, D2D_OPT_FUSED_SLICE, d2d_env_out.state_bf16;
-                              14: d2d_policy_gru_carry, d2d_gru_carry_floats, d2d_central_critic_dw1, single obs_record */
+                              14: d2d_policy_gru_carry, d2d_gru_carry_floats, d2d_central_critic_dw1, single obs_record;
+                              15: actions = NULL in forced mode (d2d_policy_mlp_step, d2d_policy_gru) */
 
 enum { D2D_ENV_COMBINATORIAL = 0, D2D_ENV_CHANNEL_SELECTION = 1, D2D_ENV_SINGLE = 2 };
 enum { D2D_ARRIVAL_POISSON = 0, D2D_ARRIVAL_SCHEDULED_BERNOULLI = 1, D2D_ARRIVAL_NONE = 2 };
@@ -303,7 +304,8 @@ int d2d_happo_chain(int32_t n_agents, int32_t T, int32_t E, const float* adv, co
  *         channel masks [E][N] (d2d_mask_bytes(A) bytes), logp = mean_c log_prob;
  * kind 1: softmax -> Categorical over A = C+1 ids, actions = uint8 [E][N].
  * obs [E][N][F] (the env kernel's layout); logp, value [N][E].  forced != NULL
- * evaluates the given actions instead of sampling; deterministic = argmax / p > 0.5.
+ * evaluates the given actions instead of sampling; actions may then be NULL (ABI 15: only logp is written --
+ * D2D-PPO's epoch-start log-prob pass).  deterministic = argmax / p > 0.5.
  * Sampling uses Philox stream 3 at (env_base + env, agent, rng_step).
  * Shapes: obs_dim <= 64, n_out <= 16, hidden <= 64, or hidden <= 128 when obs_dim + 1 <= 32 (the
  * learners' default hidden_size 128 on the reference envs; one wave per SIMD there), else D2D_EUNSUPPORTED;

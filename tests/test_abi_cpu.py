@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
     for fn in fns:
         assert hasattr(lib, fn), fn
         assert fn in d2dhip.EXPORTED, f"{fn} has no ctypes signature"
-    assert lib.d2d_abi_version() == 14
+    assert lib.d2d_abi_version() == 15
     assert [lib.d2d_mask_bytes(c) for c in (1, 8, 9, 16, 17, 32)] == [1, 1, 2, 2, 4, 4]
     assert [lib.d2d_buffer_words(d) for d in (1, 4, 5, 8, 12, 14, 16, 17, 32)] == [1, 1, 2, 2, 3, 4, 4, 8, 8]
     assert lib.d2d_colstats_workspace(1000, 64) >= 64
@@ -70,6 +70,9 @@ def test_library_validates_arguments_without_gpu():
     md.obs_signed = w
     assert lib.d2d_policy_mlp_step(ctypes.byref(md), ctypes.c_void_p(24), None, 0, 0, w, w, None, None) == -1
     assert b"aligned" in lib.d2d_last_error()
+    # ABI 15: actions may be NULL in forced mode only
+    assert lib.d2d_policy_mlp_step(ctypes.byref(md), w, None, 0, 0, None, w, None, None) == -1
+    assert b"NULL" in lib.d2d_last_error()
     # the record is a combinatorial-env output only
     dsc = _lib.EnvDesc(1, 4, 3, 7, 11, 0, 0, 1, 0, 0, w, w, w, w, w, None, None, w)
     st = _lib.EnvState(w, w, w, w, w, w)

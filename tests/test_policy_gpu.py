@@ -152,7 +152,7 @@ def test_sampling_uses_philox_stream3(kind, F, H, A, in_dims):
     torch.testing.assert_close(lp, lp2, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("kind,F,H,A,in_dims", [CASES[0], CASES[4], CASES[3]])
+@pytest.mark.parametrize("kind,F,H,A,in_dims", [CASES[0], CASES[4], CASES[3], CASES[2]])
 def test_forced_full_waves_equal_sampled_logp(kind, F, H, A, in_dims):
     """Batches large enough for many tiles per wave (one resident round: the forced bytes travel through the
     obs DMA ring, several hundred tile pairs per wave) with a ragged tail: the forced evaluation of sampled actions
@@ -167,6 +167,11 @@ def test_forced_full_waves_equal_sampled_logp(kind, F, H, A, in_dims):
     acts2, lp2, _ = policy_mlp_step(actor, obs, kind, None, forced=acts)
     assert torch.equal(acts2, acts)
     torch.testing.assert_close(lp2, lp, rtol=0, atol=0)
+    # ABI 15: the same log-probs with actions = NULL (D2D-PPO's epoch-start pass; A > 8 and the Categorical ids
+    # through the epilogue's own load, A <= 8 through the DMA ring)
+    none3, lp3, _ = policy_mlp_step(actor, obs, kind, None, forced=acts, want_actions=False)
+    assert none3 is None
+    torch.testing.assert_close(lp3, lp, rtol=0, atol=0)
     probs, _ = torch_ref(actor, None, obs)
     if kind == "comb":
         bits = torch.stack([(acts.long() >> j) & 1 for j in range(A)], -1).transpose(0, 1).float()  # [N][E][A]
