@@ -36,10 +36,10 @@ __device__ __forceinline__ f32x4 ppo_dz(const Args& a, f32x4 z, uint32_t act, fl
 #pragma unroll
     for (int r = 0; r < 4; ++r) p[r] = valid[r] ? __builtin_amdgcn_rcpf(1.f + __expf(-z[r])) : 0.f;
   } else {
-    float mx = -INFINITY;
+    float mx = valid[0] ? z[0] : -INFINITY;
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (valid[r]) mx = fmaxf(mx, z[r]);
+    for (int r = 1; r < 4; ++r)
+      if (valid[r]) mx = fmax_raw(mx, z[r]);  // one v_max_f32 each (mlp_common.h)
     mx = group_max<HALF>(mx);
     float ex[4], sum = 0.f;
 #pragma unroll
