@@ -185,6 +185,11 @@ __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* 
 // reads as 0) -- what the forced words' DMA and extraction cost
 #define D2D_POLICY_ABLATE_FORCED_DMA 0
 #endif
+#ifndef D2D_POLICY_FORCED_PAIR
+// 1: one forced-word DMA per tile PAIR (lanes of group 0 bring tile t's words, group 1 tile t + 1's) instead of one per
+// tile (group 0 only)
+#define D2D_POLICY_FORCED_PAIR 1
+#endif
 #ifndef D2D_POLICY_ACTOR_WAVES
 // waves per SIMD of the actor-only record instantiation (137 VGPRs at 3; 4 needs <= 128)
 #define D2D_POLICY_ACTOR_WAVES 3
@@ -229,7 +234,9 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
   // tiles (one resident round).  Paired epilogue (A <= 8, one byte per cell) only; otherwise the DMA is
   // aimed outside the buffer (no traffic) and the epilogue loads its masks itself.
   constexpr int FD = (MODE == kModeForced && !D2D_POLICY_ABLATE_FORCED_DMA) ? 1 : 0;
-  __shared__ uint32_t fring[4][FD ? RING : 1][64];
+  constexpr bool FP = D2D_POLICY_FORCED_PAIR != 0;           // one forced DMA per tile pair
+  constexpr int FSLOTS = FD ? (FP ? RING / 2 : RING) : 1;     // forced-word ring slots
+  __shared__ uint32_t fring[4][FSLOTS][64];
   const int64_t fbytes = MODE == kModeForced ? ((int64_t)a.E * N * a.mask_bytes + 3) / 4 * 4 : 0;
   const __amdgpu_buffer_rsrc_t frsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<void*>(MODE == kModeForced ? a.forced : (const void*)a.act_out), 0,
@@ -245,7 +252,7 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
   // int8 byte masks of this lane's record words (agent k, columns 32c + 8g + 4h + r)
   uint32_t sm[KC][2] = {};
   if constexpr (U8) record_sign_masks<KC>(sm, a.sgn, k, g);
-  auto issue = [&](int t) {
+  auto issue = [&](int t, bool even) {
     // look-ahead tiles past this wave's last are still issued (the counted waits need a fixed
     // DMA count) but aimed outside the descriptor's range: no memory traffic, zeros
     const uint32_t vo = (t < tiles && !D2D_POLICY_ABLATE_NOREAD) ? (uint32_t)((t * 16 + i) * N * RB) + (U8 ? 8 : 32) * g
@@ -258,12 +265,17 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
             rsrc, (__attribute__((address_space(3))) void*)&ring[wave][t % RING][c][j][0], 4,
             vo + (U8 ? 32 * c + 4 * j : 4 * (32 * c + j)), 0, 0, 0);
     if constexpr (FD) {
-      // 32-bit cell offsets: policy_mlp_args caps the forced buffer at 2 GiB
-      const int env = wave_env0 + t * 16 + i;
-      const uint32_t fo = (t < tiles && g == 0 && A <= 8 && env < a.E) ? ((uint32_t)env * (uint32_t)N + (uint32_t)k) & ~3u
-                                                                       : 0x80000000u;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(frsrc, (__attribute__((address_space(3))) void*)&fring[wave][t % RING][0],
-                                               4, fo, 0, 0, 0);
+      // 32-bit cell offsets: policy_mlp_args caps the forced buffer at 2 GiB.  FP: issued with the even tile of a pair
+      // (wave-uniform branch), lane group 0 bringing tile t's words and group 1 tile t + 1's
+      if (!FP || even) {
+        const int tf = FP ? t + (g & 1) : t;
+        const int env = wave_env0 + tf * 16 + i;
+        const uint32_t fo = (tf < tiles && (FP ? g < 2 : g == 0) && A <= 8 && env < a.E)
+                                ? ((uint32_t)env * (uint32_t)N + (uint32_t)k) & ~3u
+                                : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            frsrc, (__attribute__((address_space(3))) void*)&fring[wave][(FP ? t >> 1 : t) % FSLOTS][0], 4, fo, 0, 0, 0);
+      }
     }
   };
   // layers 1-2 of one tile -> (pre-scaled) logits lg and critic value
@@ -279,11 +291,11 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
   // the DMA count between a tile's issue and its wait is fixed: RING - 2 tiles of KC * DPC DMAs
   // (anything else issued in between -- the stores -- only makes the counted wait stricter)
   static_assert(RING >= 4 && RING % 2 == 0, "two tiles per iteration");
-  for (int t = 0; t < RING - 2; ++t) issue(t);
+  for (int t = 0; t < RING - 2; ++t) issue(t, (t & 1) == 0);
   for (int tt = 0; tt < tiles; tt += 2) {
-    issue(tt + RING - 2);
-    issue(tt + RING - 1);
-    wait_vmem<(RING - 2) * (KC * DPC + FD)>();  // tiles tt, tt + 1 have landed
+    issue(tt + RING - 2, true);
+    issue(tt + RING - 1, false);
+    wait_vmem<(RING - 2) * KC * DPC + (FP ? (RING - 2) / 2 : RING - 2) * FD>();  // tiles tt, tt + 1 have landed
     __builtin_amdgcn_sched_barrier(0);        // no LDS read of the slots moves above the wait
     const int env0 = wave_env0 + tt * 16 + i, env1 = env0 + 16;
     // forced byte of this lane's paired-epilogue cell (env0 for groups 0-1, env1 for 2-3), read before the
@@ -291,7 +303,8 @@ __global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : 
     uint32_t fpre = 0;
     if constexpr (FD) {
       const int envc = g < 2 ? env0 : env1;
-      const uint32_t w = fring[wave][(g < 2 ? tt : tt + 1) % RING][i];
+      const uint32_t w = FP ? fring[wave][(tt >> 1) % FSLOTS][(g < 2 ? 0 : 16) + i]
+                            : fring[wave][(g < 2 ? tt : tt + 1) % FSLOTS][i];
       fpre = (w >> (8 * (((uint32_t)(envc < a.E ? envc : 0) * (uint32_t)N + (uint32_t)k) & 3u))) & 0xFFu;
     }
     // the paired epilogue's Philox block, drawn here: inside the scheduling region of the tiles' MFMAs (the
