@@ -547,8 +547,13 @@ __global__ __launch_bounds__(256) void critic_dw1_reduce_kernel(int64_t n, int K
 using namespace d2d;
 
 static int critic_ht(int H) { return H <= 32 ? 2 : H <= 64 ? 4 : H <= 128 ? 8 : 0; }
-static int critic_st(int ht) { return ht <= 4 ? 4 : 2; }
-static int critic_kch(int ht) { return ht <= 4 ? 2 : 1; }  // chunks per iteration (LDS: 2 x KCH x 12 HT/4 KB)
+#ifndef D2D_CRITIC_ST4
+// sample tiles per wave / chunks per iteration at HT = 3..4 (A/B builds; the XL path needs 4 / 2)
+#define D2D_CRITIC_ST4 4
+#define D2D_CRITIC_KCH4 2
+#endif
+static int critic_st(int ht) { return ht <= 2 ? 4 : ht <= 4 ? D2D_CRITIC_ST4 : 2; }
+static int critic_kch(int ht) { return ht <= 2 ? 2 : ht <= 4 ? D2D_CRITIC_KCH4 : 1; }  // chunks per iteration (LDS: 2 x KCH x 12 HT/4 KB)
 static int critic_chunks(int ht, int S) { const int k = critic_kch(ht); return ((S + 31) / 32 + k - 1) / k * k; }
 
 extern "C" int32_t d2d_central_critic_blocks(int32_t H, int64_t B) {
@@ -592,7 +597,7 @@ extern "C" int d2d_central_critic_fwd(int32_t H, int64_t B, int32_t S, int64_t l
     hipLaunchKernelGGL((critic_fwd_kernel<2, 4, 2>), dim3(G), dim3(64 * D2D_CRITIC_WAVES), 0, s, a);
   } else if (ht == 4) {
     hipLaunchKernelGGL(critic_w1_image_kernel<4>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
-    hipLaunchKernelGGL((critic_fwd_kernel<4, 4, 2>), dim3(G), dim3(64 * D2D_CRITIC_WAVES), 0, s, a);
+    hipLaunchKernelGGL((critic_fwd_kernel<4, D2D_CRITIC_ST4, D2D_CRITIC_KCH4>), dim3(G), dim3(64 * D2D_CRITIC_WAVES), 0, s, a);
   } else {
     hipLaunchKernelGGL(critic_w1_image_kernel<8>, dim3(ig), dim3(256), 0, s, H, S, a.nchunk, w1, img);
     hipLaunchKernelGGL((critic_fwd_kernel<8, 2, 1>), dim3(G), dim3(64 * D2D_CRITIC_WAVES), 0, s, a);
