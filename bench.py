@@ -747,19 +747,30 @@ def d2denv_leg(args, rank, world, local):
         return {"env_steps_per_s": args.envs * world * steps / wall, "kernel_avg_us": kern_ms * 1e3,
                 "bytes_per_launch": bytes_launch, "achieved_GBps": achieved, "hbm_frac": achieved / HBM_PEAK_GBS}
 
-    f32 = run(False)
-    recd = run(True)
+    # --d2denv-env-only with --env-mode fp32 / record: one obs format only, so that every single_kernel dispatch of a
+    # PMC pass is that format's --envs launch (tools/gpu/profile_single.sh)
+    only = args.env_mode if args.d2denv_env_only and args.env_mode != "both" else None
+    f32 = run(False) if only != "record" else {}
+    recd = run(True) if only != "fp32" else {}
     del env, b, act, rec
     torch.cuda.empty_cache()
     out = {"agents": N, "envs_per_gpu": args.envs, "obs_dim": s.F, "neighbourhood": "ring {k-1,k,k+1}",
            "kernel": "d2d::single_kernel<2, false>", **f32,
            "record": dict(recd, what="the same steps emitting the compact obs record the learners consume (ABI 14: "
                                      f"{record_bytes(s.F)} B per agent-step instead of {4 * s.F} B of fp32 rows)")}
-    pmc, rel = load_profile_json("pmc_traffic_single.json")
-    if pmc and pmc.get("envs") == args.envs and pmc.get("agents") == N:
-        out["traffic"] = {"bytes_per_launch": pmc.get("bytes_per_launch"),
-                          "traffic_over_algorithmic": pmc.get("traffic_over_algorithmic"), "file": rel,
-                          "commit": pmc.get("commit")}
+
+    def traffic(name):
+        pmc, rel = load_profile_json(name)
+        if pmc and pmc.get("envs") == args.envs and pmc.get("agents") == N:
+            return {"bytes_per_launch": pmc.get("bytes_per_launch"),
+                    "traffic_over_algorithmic": pmc.get("traffic_over_algorithmic"), "file": rel,
+                    "commit": pmc.get("commit")}
+        return None
+    t32, trec = traffic("pmc_traffic_single.json"), traffic("pmc_traffic_single_record.json")
+    if t32:
+        out["traffic"] = t32
+    if trec:
+        out["record"]["traffic"] = trec
     if args.d2denv_env_only:  # PMC passes: every single_kernel dispatch is a --envs launch
         return out
     from algorithms.ippo import iPPO
