@@ -1,7 +1,7 @@
 # round-6 end, profiles stamped with the code commit: rocprofv3 kernel-trace stats of the env leg (the headline
 # kernel's duration), FETCH_SIZE / WRITE_SIZE passes -> HBM traffic per launch, then the per-leg SQ counter passes
 # of the MFMA kernels (tools/gpu/pmc_legs.sh: rollout, ppo, gru_slot, gru legs alone).
-# usage (GPU box): bash tools/gpu/run_r06z_prof.sh <commit>
+# usage (GPU box): bash tools/gpu/run_r06z_prof2.sh <commit>
 R="$GRAFT_REPO_ROOT"; COMMIT="$1"; cd "$R" || exit 9
 O="$R/gpurun_out/r06z_prof2"; mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
@@ -28,9 +28,9 @@ for leg in rollout ppo gru_slot gru; do
   cp "$R/gpurun_out/pmcl_r06/pmc_mfma_$leg.json" "$O/pmc_mfma_$leg.json"
   cp "$(ls "$R/gpurun_out/pmcl_r06/$leg/stats/"*kernel_stats.csv | head -1)" "$O/${leg}_kernel_stats.csv"
 done
-bash "$R/tools/gpu/profile_single.sh" r06z "$COMMIT" > "$O/profile_single.log" 2>&1
+bash "$R/tools/gpu/profile_single.sh" r06z2 "$COMMIT" > "$O/profile_single.log" 2>&1
 rc=$?; echo "single traffic rc=$rc"; [ $rc -eq 0 ] || exit $rc
-cp "$R/gpurun_out/prof_r06z2/pmc_traffic_single.json" "$O/pmc_traffic_single.json"
-cp "$(ls "$R"/gpurun_out/prof_r06z2/stats/*kernel_stats.csv | head -1)" "$O/single_kernel_stats.csv"
+cp "$R"/gpurun_out/prof_r06z2/pmc_traffic_single*.json "$R"/gpurun_out/prof_r06z2/single_*_kernel_stats.csv "$O/"
+rm -rf "$R/gpurun_out/prof_r06z2/fp32" "$R/gpurun_out/prof_r06z2/record"
 rm -rf "$R/gpurun_out/pmcl_r06" "$R/gpurun_out/prof_r06z2"
 exit 0
