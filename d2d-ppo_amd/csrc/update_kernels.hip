@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <type_traits>
 
 #include "ppo_epilogue.h"
@@ -1793,9 +1794,22 @@ static int64_t tensor_extent(const int64_t (&st)[3], int T, int E, int N) {
 #define D2D_UPD_MAX_WAVE_TILES 256
 #endif
 constexpr int64_t kMaxWaveTiles = D2D_UPD_MAX_WAVE_TILES;
+#ifndef D2D_UPD_MIN_ROUNDS
+// at least this many resident rounds of workgroups per launch (a small batch's waves then run fewer tiles each and the
+// last round's stragglers cost less); D2D_UPD_MIN_ROUNDS in the environment overrides it (A/B, read once per process)
+#define D2D_UPD_MIN_ROUNDS 1
+#endif
+static int upd_min_rounds() {
+  static const int r = [] {
+    const char* e = getenv("D2D_UPD_MIN_ROUNDS");
+    const int v = e ? atoi(e) : D2D_UPD_MIN_ROUNDS;
+    return v < 1 ? 1 : v > 8 ? 8 : v;
+  }();
+  return r;
+}
 static int update_blocks(int N, int64_t n_tiles, int resident) {
   const int64_t need = (int64_t)N * ((n_tiles + 4 * kMaxWaveTiles - 1) / (4 * kMaxWaveTiles));
-  const int64_t rounds = std::max<int64_t>(1, (need + resident - 1) / resident);
+  const int64_t rounds = std::max<int64_t>(upd_min_rounds(), (need + resident - 1) / resident);
   const int64_t G = (rounds * resident + N - 1) / N;
   // (grid.y <= 65535: past that, more tiles per wave)
   return (int)std::max<int64_t>(1, std::min<int64_t>({G, (n_tiles + 3) / 4, 65535}));
@@ -1822,7 +1836,7 @@ static int upd_resident() {
 // the workspace bound for any kernel's G: rounds x resident < need + resident <= need + 8 workgroups per CU
 static int update_blocks_bound(int N, int64_t n_tiles) {
   const int64_t need = (int64_t)N * ((n_tiles + 4 * kMaxWaveTiles - 1) / (4 * kMaxWaveTiles));
-  const int64_t G = (need + 8 * (int64_t)cu_count() + N - 1) / N;
+  const int64_t G = (std::max<int64_t>(need + 8 * (int64_t)cu_count(), (int64_t)upd_min_rounds() * 8 * cu_count()) + N - 1) / N;
   return (int)std::max<int64_t>(1, std::min<int64_t>({G, (n_tiles + 3) / 4, 65535}));
 }
 
