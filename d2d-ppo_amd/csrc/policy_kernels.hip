@@ -194,6 +194,11 @@ __device__ __forceinline__ void stage_record(float (&x)[KC][8], const uint32_t* 
 // waves per SIMD of the actor-only record instantiation (137 VGPRs at 3; 4 needs <= 128)
 #define D2D_POLICY_ACTOR_WAVES 3
 #endif
+#ifndef D2D_POLICY_AF8_WAVES
+// the same for the A = 8 instantiations (AF = 8: 124-133 VGPRs at 3, 128 with no spills at 4 -- the forced mode
+// 128.2 / 129.9 -> 124.0 / 124.8 us per 65,536-env slot, sampled and deterministic unchanged; profiles/r06/policy_waves_ab.json)
+#define D2D_POLICY_AF8_WAVES 4
+#endif
 // KC = input chunks of 32 (F + 1 <= 32*KC), HT = hidden tiles of 16 (H <= 16*HT, even);
 // U8: the inputs are the env kernel's compact obs record (D2D_OBS_U8)
 // AF: the action count as a compile-time constant (0: a.A at run time; 8: the combinatorial envs' 8 channels)
@@ -202,7 +207,7 @@ template <int KC, int HT, int KIND, bool CRITIC, int MODE, bool U8, int AF = 0>
 // actor alone on the record (137 VGPRs: test(), D2D-PPO,
 // and iPPO training rollouts whose values come from the first epoch's critic pass); H in (64, 128] -- the
 // learners' default hidden_size 128 -- or F + 1 > 32: one wave / SIMD with the doubled weight fragments)
-__global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : D2D_POLICY_ACTOR_WAVES) : 1) void policy_split_kernel(MlpArgs a) {
+__global__ __launch_bounds__(256, (KC == 1 && HT <= 4) ? ((CRITIC || !U8) ? 2 : AF == 8 ? D2D_POLICY_AF8_WAVES : D2D_POLICY_ACTOR_WAVES) : 1) void policy_split_kernel(MlpArgs a) {
   static_assert(HT % 2 == 0, "layer 2 consumes hidden tiles in pairs");
   // Philox step of the launch, read once before the obs pipeline starts (the optional device
   // offset of graph replays; a load inside the epilogue would add a wait to every tile pair)
